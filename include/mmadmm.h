@@ -1,0 +1,139 @@
+/*
+ * mmadmm.h -- C-ABI of the MI355X-native MM-ADMM engine (libmmadmm.so).
+ *
+ * Drop-in boundary for the hot path of connortannahill/MM-ADMM: the ADMM time step of the
+ * MMPDE integrator (MeshIntegrator<D>::step and what it calls).  Plain pointers and sizes
+ * only; every call returns MMADMM_OK (0) or an error code, and mmadmm_last_error() gives
+ * the message.  No C++ exception crosses this boundary.  All arrays are caller-owned and
+ * copied in or out.  The C++ mirror of the reference classes (Mesh<D>, MeshIntegrator<D>,
+ * MonitorFunction<D>) lives in include/mmadmm/ and is implemented on top of this ABI.
+ *
+ * Reference interface each entry point replaces (paths relative to the reference repo):
+ *   mmadmm_create            Mesh<D>::Mesh (src/Mesh.h:22-25, src/Mesh.cpp:384-494)
+ *                            + MeshIntegrator<D>::MeshIntegrator (src/MeshIntegrator.h:15,
+ *                              src/MeshIntegrator.cpp:15-62)
+ *   mmadmm_step              MeshIntegrator<D>::step (src/MeshIntegrator.h:17, .cpp:101-191)
+ *   mmadmm_euler_step        MeshIntegrator<D>::eulerStep (src/MeshIntegrator.h:18, .cpp:87-94)
+ *   mmadmm_energy            MeshIntegrator<D>::getEnergy (src/MeshIntegrator.h:20, .cpp:79-81)
+ *   mmadmm_done              MeshIntegrator<D>::done (src/MeshIntegrator.h:23, .cpp:193-196)
+ *   mmadmm_get("x"|"z")      MeshIntegrator<D>::outputX / outputZ (src/MeshIntegrator.h:21-22)
+ *   mmadmm_get("points")     Mesh<D>::outputPoints (src/Mesh.h:29, src/Mesh.cpp:1082-1095)
+ *   mmadmm_get_simplices     Mesh<D>::outputSimplices (src/Mesh.h:27, src/Mesh.cpp:1067-1080)
+ *   mmadmm_monitor_fn        MonitorFunction<D>::operator() (src/MonitorFunction.h:13),
+ *                            evaluated on the host at set-up only, as the reference does
+ *                            (src/MonitorFunction.cpp:16-32 via src/MeshInterpolator.cpp:254)
+ *   mmadmm_builtin_monitor   Experiments/TestMonitors/MEx*.h registry (main.cpp:836-864)
+ *   mmadmm_mesh_*            utils::generateUniformRectMesh / meshFromLevelSetFun /
+ *                            readTriangles (src/MeshUtils.h:82-335, 404-538, 669-733)
+ */
+#ifndef MMADMM_H
+#define MMADMM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMADMM_OK 0
+#define MMADMM_ERR_INVALID 1  /* bad argument / state */
+#define MMADMM_ERR_HIP 2      /* HIP runtime failure or no GPU */
+#define MMADMM_ERR_INVERTED 3 /* inverted element: the reference's assert(Edet > 0) */
+#define MMADMM_ERR_IO 4       /* file not readable / writable */
+#define MMADMM_ERR_RCCL 5     /* collective failure */
+
+/* Node types (src/NodeType.h:4-8); mask arrays use these values. */
+#define MMADMM_BOUNDARY_FREE 0
+#define MMADMM_BOUNDARY_FIXED 1
+#define MMADMM_INTERIOR 2
+
+typedef struct mmadmm_engine* mmadmm_handle;
+typedef struct mmadmm_meshbuf* mmadmm_mesh;
+
+/* Monitor tensor M(x) (D x D, row-major), called on the host at set-up. */
+typedef void (*mmadmm_monitor_fn)(int dim, const double* x, double* M_rowmajor, void* user);
+
+typedef struct mmadmm_params {
+  double dt;      /* time step (MeshIntegrator ctor dt) */
+  double tau;     /* mass-matrix weight (Mesh ctor tau) */
+  double rho;     /* ADMM penalty; w = 0.5*sqrt(rho) as in src/Mesh.cpp:451 */
+  int grad_use;   /* GradUse: predictor always uses the energy gradient */
+  int device;     /* HIP device ordinal, -1 = current device */
+  int rank;       /* element-partitioned run: this rank (0 for single GPU) */
+  int nranks;     /* number of ranks (1 for single GPU) */
+} mmadmm_params;
+
+typedef struct mmadmm_stats {
+  long long steps;        /* time steps taken */
+  long long admm_iters;   /* ADMM iterations executed */
+  long long bfgs_iters;   /* BFGS iterations summed over simplices */
+  int max_bfgs;           /* largest per-simplex BFGS count in the last prox */
+  double last_primal;     /* ||D x - z|| of the last ADMM iteration */
+  double last_dual;       /* ||z - zPrev|| of the last ADMM iteration */
+  double t_prox_ms;       /* device time in the prox kernel (timing on) */
+  double t_xupdate_ms;    /* device time in the x-update kernel (timing on) */
+  double t_step_ms;       /* device time of whole steps (timing on) */
+  long long n_prox;       /* prox launches timed */
+  long long n_xupdate;    /* x-update launches timed */
+  long long n_steps_timed;
+  double prox_bytes;      /* algorithmic HBM bytes of one prox launch */
+  double xupdate_bytes;   /* algorithmic HBM bytes of one x-update launch */
+} mmadmm_stats;
+
+const char* mmadmm_last_error(void);
+int mmadmm_version(void);
+
+/* built-in monitors MEx0..MEx5 (dim 2) and MEx0/13D/23D/33D/0/53D (dim 3) by MonType */
+int mmadmm_builtin_monitor(int dim, int mon_type, mmadmm_monitor_fn* fn, void** user);
+
+/* Mesh<D> + MeshIntegrator<D>.  Xp: nP x dim row-major; Xc: reference positions (CompMesh)
+ * or NULL; F: nF x (dim+1); mask: nP node types.  F is re-oriented (src/Mesh.cpp:243-260)
+ * and can be read back with mmadmm_get_simplices. */
+int mmadmm_create(int dim, int nP, const double* Xp, const double* Xc, int nF, const int32_t* F,
+                  const int32_t* mask, const mmadmm_params* p, mmadmm_monitor_fn fn, void* user,
+                  mmadmm_handle* out);
+/* One ADMM time step.  tol >= 0: the reference's early exit (primal < tol && dual < tol);
+ * tol < 0: exactly n_iters ADMM iterations (prox tolerance 1e-3 as main.cpp:184).
+ * *Ih = energy at the first prox of the step (the reference's return value). */
+int mmadmm_step(mmadmm_handle h, int n_iters, double tol, double* Ih, int* admm_iters);
+int mmadmm_euler_step(mmadmm_handle h, double* Ih);
+int mmadmm_energy(mmadmm_handle h, double* E);
+int mmadmm_done(mmadmm_handle h);
+/* what: "x", "xPrev", "xBar", "z", "u", "points", "hess", "grid", "Ehat" */
+int mmadmm_get(mmadmm_handle h, const char* what, double* out);
+int mmadmm_get_simplices(mmadmm_handle h, int32_t* F);
+int mmadmm_sizes(mmadmm_handle h, int* nP, int* nF, int* grid_rows);
+int mmadmm_set_timing(mmadmm_handle h, int on);
+int mmadmm_stats_get(mmadmm_handle h, mmadmm_stats* s);
+int mmadmm_stats_reset(mmadmm_handle h);
+int mmadmm_sync(mmadmm_handle h);
+int mmadmm_destroy(mmadmm_handle h);
+
+/* meshes: generators and readers (host) */
+int mmadmm_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, double ya, double yb,
+                     double za, double zb, int btype, mmadmm_mesh* out);
+/* compact_mask = 0 keeps the reference's pre-compaction mask indexing (MeshUtils.h:487) */
+int mmadmm_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int btype,
+                           int compact_mask, mmadmm_mesh* out);
+/* hexagonal disc of radius r centred (cx, cy): 3N(N+1)+1 nodes, 6N^2 triangles, rim FIXED */
+int mmadmm_mesh_hexdisc(int N, double r, double cx, double cy, int btype, mmadmm_mesh* out);
+int mmadmm_mesh_read(int dim, const char* tri, const char* pnts, const char* mask, mmadmm_mesh* out);
+int mmadmm_mesh_sizes(mmadmm_mesh m, int* dim, int* nP, int* nF, int* mask_len);
+int mmadmm_mesh_copy(mmadmm_mesh m, double* Xp, int32_t* F, int32_t* mask);
+int mmadmm_mesh_free(mmadmm_mesh m);
+/* writers byte-compatible with Mesh::outputPoints / outputSimplices (default ostream) */
+int mmadmm_write_points(const char* path, int dim, int nP, const double* Xp);
+int mmadmm_write_simplices(const char* path, int dim, int nF, const int32_t* F);
+
+/* one-simplex Mesh::computeBlockGrad on the device (tests): flags bit0 = gradient,
+ * bit1 = regularise with dxpu; out = {energy, Igt, grad[D(D+1)]} */
+int mmadmm_debug_blockgrad(mmadmm_handle h, int s, const double* z, const double* dxpu, int flags,
+                           double* out);
+
+/* device math self-test (correctly rounded powers): op 0 sqrt, 1 x^1.5, 2 x^-0.5, 3 x^2.25,
+ * 4 x^1.25 */
+int mmadmm_devmath(int op, int n, const double* in, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

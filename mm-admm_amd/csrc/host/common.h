@@ -1,0 +1,67 @@
+// common.h -- host-side helpers shared by the libmmadmm translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/mmadmm.h"
+
+namespace mmx {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& msg);
+
+#define MMX_HIP(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      throw ::mmx::Error(MMADMM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Run f, translate exceptions to status codes (no exception crosses the C-ABI).
+template <class Fn>
+int guarded(Fn&& f) {
+  try {
+    f();
+    return MMADMM_OK;
+  } catch (const Error& e) {
+    set_last_error(e.what());
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_last_error("out of host memory");
+    return MMADMM_ERR_INVALID;
+  } catch (const std::exception& e) {
+    set_last_error(e.what());
+    return MMADMM_ERR_INVALID;
+  }
+}
+
+// Built-in monitors (Experiments/TestMonitors/MEx*.h restated), by MonType
+void builtin_monitor_eval(int dim, int monType, const double* x, double* M);
+
+// Host mesh buffer behind mmadmm_mesh
+struct MeshBuf {
+  int dim = 2;
+  std::vector<double> Vp;
+  std::vector<int32_t> F;
+  std::vector<int32_t> mask;
+  int nP() const { return (int)(Vp.size() / dim); }
+  int nF() const { return (int)(F.size() / (dim + 1)); }
+};
+
+// Smoothed monitor grid (src/MeshInterpolator.cpp:68-130, 166-259, 366-404)
+struct HostGrid {
+  int nx = 0, ny = 0, nz = 0;
+  std::vector<double> gx, gy, gz;
+  std::vector<double> vals;  // rows x dim*dim
+};
+void build_monitor_grid(int dim, const double* X, int nP, mmadmm_monitor_fn fn, void* user,
+                        HostGrid& g);
+
+}  // namespace mmx

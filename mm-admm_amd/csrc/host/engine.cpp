@@ -1,0 +1,580 @@
+// engine.cpp -- the ADMM integrator on one MI355X: set-up, device state, step orchestration.
+//
+// Host mirror of Mesh<D> (src/Mesh.cpp:384-472) and MeshIntegrator<D> (src/MeshIntegrator.cpp).
+// All per-step work runs on the device on one HIP stream; the host only launches kernels and,
+// with the early exit enabled, reads back three scalars per ADMM iteration.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../kernels/admm_kernels.h"
+#include "common.h"
+
+namespace mmx {
+
+namespace {
+thread_local std::string g_last_error;
+}
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  void alloc(size_t count) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = count;
+    if (count) MMX_HIP(hipMalloc(&p, count * sizeof(T)));
+  }
+  void upload(const T* h, size_t count, hipStream_t st) {
+    alloc(count);
+    if (count) MMX_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
+  }
+};
+
+struct EngineBase {
+  virtual ~EngineBase() = default;
+  int dim = 2;
+  virtual void step(int nIters, double tol, double* Ih, int* iters) = 0;
+  virtual double eulerStep() = 0;
+  virtual double energy() = 0;
+  virtual void done() = 0;
+  virtual void get(const std::string& what, double* out) = 0;
+  virtual void getSimplices(int32_t* F) = 0;
+  virtual void sizes(int* nP, int* nF, int* gridRows) = 0;
+  virtual void setTiming(bool on) = 0;
+  virtual void stats(mmadmm_stats* s) = 0;
+  virtual void resetStats() = 0;
+  virtual void sync() = 0;
+  virtual void debugBlockGrad(int s, const double* z, const double* dx, int flags, double* out) = 0;
+};
+
+template <int D>
+class Engine final : public EngineBase {
+ public:
+  static constexpr int K = D * (D + 1);
+
+  Engine(int nP, const double* Xp, const double* Xc, int nF, const int32_t* F, const int32_t* mask,
+         const mmadmm_params& p, mmadmm_monitor_fn fn, void* user) {
+    dim = D;
+    nP_ = nP;
+    nF_ = nF;
+    prm_ = p;
+    if (p.device >= 0) MMX_HIP(hipSetDevice(p.device));
+    MMX_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    compMesh_ = (Xc != nullptr);
+    std::vector<double> Vp(Xp, Xp + (size_t)nP * D);
+    Fh_.assign(F, F + (size_t)nF * (D + 1));
+    for (int i = 0; i < nF * (D + 1); ++i)
+      if (Fh_[i] < 0 || Fh_[i] >= nP) throw Error(MMADMM_ERR_INVALID, "simplex vertex id out of range");
+    maskH_.assign(mask, mask + nP);
+    // Mesh::reOrientElements (src/Mesh.cpp:243-260): swap F(i,1), F(i,2) when det(E) < 0
+    for (int s = 0; s < nF; ++s) {
+      double E[3][3];
+      for (int j = 0; j < D; ++j)
+        for (int r = 0; r < D; ++r)
+          E[r][j] = Vp[(size_t)Fh_[(size_t)s * (D + 1) + j + 1] * D + r] - Vp[(size_t)Fh_[(size_t)s * (D + 1)] * D + r];
+      if (hostDet(E) < 0) std::swap(Fh_[(size_t)s * (D + 1) + 1], Fh_[(size_t)s * (D + 1) + 2]);
+    }
+    // monitor grid (MeshInterpolator set-up), once per run on the initial vertices
+    build_monitor_grid(D, Vp.data(), nP, fn, user, grid_);
+    // functional constants (src/AdaptationFunctional.cpp:176-220, src/Mesh.cpp:451)
+    const double w = 0.5 * sqrt(p.rho);
+    w_ = w;
+    double Ehat[3][3] = {{0}};
+    if (D == 2) {
+      Ehat[0][0] = 1.0;
+      Ehat[1][0] = 0.0;
+      Ehat[0][1] = 1.0 / 2.0;
+      Ehat[1][1] = sqrt(3) / 2.0;
+    } else {
+      const double v[3][3] = {{-2.0, 0.0, -2.0}, {0.0, -2.0, -2.0}, {-2.0, -2.0, 0.0}};
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) Ehat[r][c] = v[r][c];
+    }
+    const double dFact = (D == 2) ? 2.0 : 6.0;
+    const double s1 = pow((dFact / std::abs(hostDet(Ehat))), 1.0 / ((double)D));
+    for (int r = 0; r < D; ++r)
+      for (int c = 0; c < D; ++c) Ehat[r][c] *= s1;
+    const double s2 = (double)pow(nF, 1.0 / D);
+    for (int r = 0; r < D; ++r)
+      for (int c = 0; c < D; ++c) Ehat[r][c] /= s2;
+    for (int r = 0; r < D; ++r)
+      for (int c = 0; c < D; ++c) EhatH_[r * D + c] = Ehat[r][c];
+    const double d = (double)D, pp = 1.5;
+    powd_ = pow(d, d * pp / 2.0);
+    // node -> incident simplex slots, ascending simplex id (column-major D^T order)
+    std::vector<int> ptr(nP + 1, 0), off((size_t)nF * (D + 1));
+    for (int s = 0; s < nF; ++s)
+      for (int n = 0; n < D + 1; ++n) ptr[Fh_[(size_t)s * (D + 1) + n] + 1]++;
+    for (int v = 0; v < nP; ++v) ptr[v + 1] += ptr[v];
+    {
+      std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+      for (int s = 0; s < nF; ++s)
+        for (int n = 0; n < D + 1; ++n) off[fill[Fh_[(size_t)s * (D + 1) + n]]++] = s * K + n * D;
+    }
+    // t = M + dt^2 WD_T W D is block diagonal: t_vv = tau + dt^2 * (w*w summed valence times)
+    std::vector<double> invdiag(nP);
+    const double dtsq = p.dt * p.dt;
+    for (int v = 0; v < nP; ++v) {
+      double S = 0.0;
+      for (int c = 0; c < ptr[v + 1] - ptr[v]; ++c) S = (c == 0) ? (w * w) * 1.0 : S + (w * w) * 1.0;
+      invdiag[v] = 1.0 / (p.tau + dtsq * S);
+    }
+    std::vector<uint8_t> sbits(nF), interior(nP);
+    for (int v = 0; v < nP; ++v) interior[v] = maskH_[v] == MMADMM_INTERIOR ? 1 : 0;
+    for (int s = 0; s < nF; ++s) {
+      unsigned b = 0;
+      for (int n = 0; n < D + 1; ++n) {
+        const int t = maskH_[Fh_[(size_t)s * (D + 1) + n]];
+        if (t == MMADMM_BOUNDARY_FIXED) b |= 1u << n;
+        if (t != MMADMM_INTERIOR) b |= 1u << (4 + n);
+      }
+      sbits[s] = (uint8_t)b;
+    }
+    // device state
+    F_.upload(Fh_.data(), Fh_.size(), st_);
+    sbits_.upload(sbits.data(), sbits.size(), st_);
+    interior_.upload(interior.data(), interior.size(), st_);
+    incPtr_.upload(ptr.data(), ptr.size(), st_);
+    incOff_.upload(off.data(), off.size(), st_);
+    invdiag_.upload(invdiag.data(), invdiag.size(), st_);
+    if (compMesh_) Vc_.upload(Xc, (size_t)nP * D, st_);
+    gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
+    gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
+    if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
+    gvals_.upload(grid_.vals.data(), grid_.vals.size(), st_);
+    Vp_.upload(Vp.data(), Vp.size(), st_);  // Mesh::Vp
+    x_.upload(Vp.data(), Vp.size(), st_);   // MeshIntegrator ctor: x = xPrev = xBar = copyX(Vp)
+    xPrev_.upload(Vp.data(), Vp.size(), st_);
+    xBar_.upload(Vp.data(), Vp.size(), st_);
+    z_.alloc((size_t)nF * K);
+    u_.alloc((size_t)nF * K);
+    gs_.alloc((size_t)nF * K);
+    MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
+    {
+      std::vector<double> eye((size_t)nF * K * K, 0.0);  // hessInvs = I (src/Mesh.cpp:456-464)
+      for (int s = 0; s < nF; ++s)
+        for (int i = 0; i < K; ++i) eye[(size_t)s * K * K + i * K + i] = 1.0;
+      B_.upload(eye.data(), eye.size(), st_);
+    }
+    const size_t maxBlocks = std::max<size_t>(1, std::max((nF + 255) / 256, (nP + 255) / 256));
+    partA_.alloc(maxBlocks * kNumPartials);
+    partB_.alloc(maxBlocks * kNumPartials);
+    resultsCap_ = 0;
+    ensureResults(64);
+    m_ = makeView();
+    launch_gather_z<D>(m_, x_.p, z_.p, st_);  // z = D x
+    MMX_HIP(hipStreamSynchronize(st_));
+    MMX_HIP(hipGetLastError());
+  }
+
+  ~Engine() override {
+    for (auto& e : evPool_) (void)hipEventDestroy(e);
+    if (st_) (void)hipStreamDestroy(st_);
+  }
+
+  // MeshIntegrator<D>::step (src/MeshIntegrator.cpp:101-191)
+  void step(int nIters, double tol, double* Ih, int* itersOut) override {
+    if (nIters < 1) throw Error(MMADMM_ERR_INVALID, "step: nIters must be >= 1");
+    ensureResults(nIters);
+    const bool timing = timing_;
+    hipEvent_t eStep0 = nullptr, eStep1 = nullptr;
+    size_t evMark = evUsed_;
+    if (timing) {
+      eStep0 = nextEvent();
+      MMX_HIP(hipEventRecord(eStep0, st_));
+    }
+    const double dtOverTau = prm_.dt / prm_.tau;
+    // predictX (src/Mesh.cpp:649-674), then xPrev = x
+    if (prm_.grad_use || stepsTaken_ <= 2) {
+      int nb = 0;
+      launch_grad_simplex<D>(m_, x_.p, gs_.p, true, partA_.p, &nb, st_);
+      launch_predict<D>(m_, 0, gs_.p, x_.p, xPrev_.p, xBar_.p, dtOverTau, st_);
+    } else {
+      launch_predict<D>(m_, 1, nullptr, x_.p, xPrev_.p, xBar_.p, dtOverTau, st_);
+    }
+    // x = xBar; z = D x; first step: z = D xPrev
+    launch_gather_z<D>(m_, stepsTaken_ == 0 ? xPrev_.p : xBar_.p, z_.p, st_);
+    if (!stepTaken_) MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
+    StepScalars sc{prm_.tau, prm_.dt * prm_.dt, w_, dtOverTau};
+    int nbx = 0, nbp = 0;
+    launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, false, st_);
+    const bool early = tol >= 0;
+    int done = 0;
+    double primal = 0, dual = 0;
+    for (int i = 0; i < nIters; ++i) {
+      hipEvent_t a0 = nullptr, a1 = nullptr, b1 = nullptr;
+      if (timing) {
+        a0 = nextEvent();
+        MMX_HIP(hipEventRecord(a0, st_));
+      }
+      launch_prox<D>(m_, !hessComputed_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p, partA_.p, &nbp,
+                     st_);
+      if (timing) {
+        a1 = nextEvent();
+        MMX_HIP(hipEventRecord(a1, st_));
+      }
+      hessComputed_ = true;
+      stepTaken_ = true;
+      launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, true, st_);
+      if (timing) {
+        b1 = nextEvent();
+        MMX_HIP(hipEventRecord(b1, st_));
+        timed_.push_back({a0, a1, b1});
+      }
+      launch_reduce_partials(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, st_);
+      launch_reduce_partials(partB_.p, nbx, results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
+      done = i + 1;
+      if (early) {
+        double r[2 * kNumPartials];
+        MMX_HIP(hipMemcpyAsync(r, results_.p + (size_t)i * 2 * kNumPartials, sizeof(r), hipMemcpyDeviceToHost, st_));
+        MMX_HIP(hipStreamSynchronize(st_));
+        primal = sqrt(r[kNumPartials + 2]);
+        dual = sqrt(r[1]);
+        if (r[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element in prox (reference: assert(Edet > 0))");
+        if (primal < tol && dual < tol) break;
+      }
+    }
+    // Mesh::updateAfterStep: Vp = x
+    MMX_HIP(hipMemcpyAsync(Vp_.p, x_.p, (size_t)nP_ * D * sizeof(double), hipMemcpyDeviceToDevice, st_));
+    if (timing) {
+      eStep1 = nextEvent();
+      MMX_HIP(hipEventRecord(eStep1, st_));
+    }
+    hostRes_.resize((size_t)done * 2 * kNumPartials);
+    MMX_HIP(hipMemcpyAsync(hostRes_.data(), results_.p, hostRes_.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    MMX_HIP(hipGetLastError());
+    bool bad = false;
+    long long bf = 0;
+    int mx = 0;
+    for (int i = 0; i < done; ++i) {
+      const double* r = &hostRes_[(size_t)i * 2 * kNumPartials];
+      bad |= r[4] > 0;
+      bf += (long long)r[3];
+      mx = std::max(mx, (int)r[5]);
+    }
+    const double* last = &hostRes_[(size_t)(done - 1) * 2 * kNumPartials];
+    primal = sqrt(last[kNumPartials + 2]);
+    dual = sqrt(last[1]);
+    st_stats_.admm_iters += done;
+    st_stats_.bfgs_iters += bf;
+    st_stats_.max_bfgs = mx;
+    st_stats_.last_primal = primal;
+    st_stats_.last_dual = dual;
+    st_stats_.steps += 1;
+    if (timing) {
+      float ms = 0;
+      MMX_HIP(hipEventElapsedTime(&ms, eStep0, eStep1));
+      st_stats_.t_step_ms += ms;
+      st_stats_.n_steps_timed += 1;
+      for (auto& t : timed_) {
+        MMX_HIP(hipEventElapsedTime(&ms, t.a0, t.a1));
+        st_stats_.t_prox_ms += ms;
+        st_stats_.n_prox += 1;
+        MMX_HIP(hipEventElapsedTime(&ms, t.a1, t.b1));
+        st_stats_.t_xupdate_ms += ms;
+        st_stats_.n_xupdate += 1;
+      }
+      timed_.clear();
+      evUsed_ = evMark;
+    }
+    stepsTaken_++;
+    if (bad) throw Error(MMADMM_ERR_INVERTED, "inverted element in prox (reference: assert(Edet > 0))");
+    if (Ih) *Ih = hostRes_[0];  // Ihstart
+    if (itersOut) *itersOut = done;
+  }
+
+  // MeshIntegrator::eulerStep -> Mesh::eulerStepMod (src/Mesh.cpp:532-579)
+  double eulerStep() override {
+    int nb = 0;
+    launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
+    launch_reduce_partials(partA_.p, nb, results_.p, st_);
+    launch_euler_apply<D>(m_, gs_.p, x_.p, prm_.dt / prm_.tau, st_);
+    double r[kNumPartials];
+    MMX_HIP(hipMemcpyAsync(r, results_.p, sizeof(r), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    if (r[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element (reference: assert(Edet > 0))");
+    return r[0];
+  }
+
+  // Mesh::computeEnergy on Vp (src/Mesh.cpp:496-530)
+  double energy() override {
+    int nb = 0;
+    launch_energy<D>(m_, Vp_.p, partA_.p, &nb, st_);
+    launch_reduce_partials(partA_.p, nb, results_.p, st_);
+    double r[kNumPartials];
+    MMX_HIP(hipMemcpyAsync(r, results_.p, sizeof(r), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    return r[0];
+  }
+
+  void done() override {
+    MMX_HIP(hipMemcpyAsync(Vp_.p, x_.p, (size_t)nP_ * D * sizeof(double), hipMemcpyDeviceToDevice, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+  }
+
+  void get(const std::string& what, double* out) override {
+    const DevBuf<double>* b = nullptr;
+    if (what == "x") b = &x_;
+    else if (what == "xPrev") b = &xPrev_;
+    else if (what == "xBar") b = &xBar_;
+    else if (what == "z") b = &z_;
+    else if (what == "u") b = &u_;
+    else if (what == "points") b = &Vp_;
+    else if (what == "hess") b = &B_;
+    else if (what == "gs") b = &gs_;
+    else if (what == "grid") {
+      std::memcpy(out, grid_.vals.data(), grid_.vals.size() * sizeof(double));
+      return;
+    } else if (what == "Ehat") {
+      std::memcpy(out, EhatH_, D * D * sizeof(double));
+      return;
+    } else {
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_get: unknown field '" + what + "'");
+    }
+    MMX_HIP(hipMemcpyAsync(out, b->p, b->n * sizeof(double), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+  }
+
+  void getSimplices(int32_t* F) override { std::memcpy(F, Fh_.data(), Fh_.size() * sizeof(int32_t)); }
+
+  void sizes(int* nP, int* nF, int* gridRows) override {
+    if (nP) *nP = nP_;
+    if (nF) *nF = nF_;
+    if (gridRows) *gridRows = (int)(grid_.vals.size() / (D * D));
+  }
+
+  void setTiming(bool on) override { timing_ = on; }
+
+  void stats(mmadmm_stats* s) override {
+    *s = st_stats_;
+    // algorithmic HBM bytes per launch: prox reads F, sbits, z, u, Bkinv,
+    // writes z, u, Bkinv; x is gathered once per node.  x-update reads the incidence CSR,
+    // z and u once each, xBar and invdiag, writes x.
+    const double nF = nF_, nP = nP_;
+    s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2) + nP * 8.0 * D;
+    s->xupdate_bytes = 4.0 * (nP + 1) + 4.0 * (D + 1) * nF + 16.0 * K * nF + 8.0 * D * nP * 2 + 8.0 * nP;
+  }
+
+  void resetStats() override {
+    const mmadmm_stats z{};
+    st_stats_ = z;
+  }
+
+  void sync() override { MMX_HIP(hipStreamSynchronize(st_)); }
+
+  void debugBlockGrad(int s, const double* z, const double* dx, int flags, double* out) override {
+    if (s < 0 || s >= nF_) throw Error(MMADMM_ERR_INVALID, "debug_blockgrad: simplex out of range");
+    DevBuf<double> dz, ddx, dout;
+    dz.upload(z, K, st_);
+    ddx.upload(dx, K, st_);
+    dout.alloc(K + 2);
+    launch_debug_blockgrad<D>(m_, s, dz.p, ddx.p, dout.p, flags, st_);
+    MMX_HIP(hipMemcpyAsync(out, dout.p, (K + 2) * sizeof(double), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+  }
+
+ private:
+  struct Timed {
+    hipEvent_t a0, a1, b1;
+  };
+
+  static double hostDet(const double (&a)[3][3]) {  // Eigen 2x2 / 3x3 determinant
+    if (D == 2) return a[0][0] * a[1][1] - a[1][0] * a[0][1];
+    const double h0 = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]);
+    const double h1 = a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]);
+    const double h2 = a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
+    return h0 - h1 + h2;
+  }
+
+  DeviceMesh<D> makeView() const {
+    DeviceMesh<D> m{};
+    m.nP = nP_;
+    m.nF = nF_;
+    m.F = F_.p;
+    m.sbits = sbits_.p;
+    m.nodeInterior = interior_.p;
+    m.inc_ptr = incPtr_.p;
+    m.inc_off = incOff_.p;
+    m.invdiag = invdiag_.p;
+    m.Vc = compMesh_ ? Vc_.p : nullptr;
+    m.gx = gx_.p;
+    m.gy = gy_.p;
+    m.gz = (D == 3) ? gz_.p : gy_.p;
+    m.gvals = gvals_.p;
+    m.gnx = grid_.nx;
+    m.gny = grid_.ny;
+    m.gnz = grid_.nz;
+    for (int i = 0; i < D * D; ++i) m.Ehat[i] = EhatH_[i];
+    m.powd = powd_;
+    m.w = w_;
+    m.compMesh = compMesh_ ? 1 : 0;
+    return m;
+  }
+
+  void ensureResults(int nIters) {
+    if (nIters <= resultsCap_) return;
+    resultsCap_ = std::max(nIters, 64);
+    results_.alloc((size_t)resultsCap_ * 2 * kNumPartials);
+  }
+
+  hipEvent_t nextEvent() {
+    if (evUsed_ == evPool_.size()) {
+      hipEvent_t e;
+      MMX_HIP(hipEventCreate(&e));
+      evPool_.push_back(e);
+    }
+    return evPool_[evUsed_++];
+  }
+
+  int nP_ = 0, nF_ = 0;
+  mmadmm_params prm_{};
+  bool compMesh_ = false;
+  double w_ = 0, powd_ = 0;
+  double EhatH_[9] = {0};
+  std::vector<int32_t> Fh_, maskH_;
+  HostGrid grid_;
+  hipStream_t st_ = nullptr;
+  DevBuf<int32_t> F_, incPtr_, incOff_;
+  DevBuf<uint8_t> sbits_, interior_;
+  DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_;
+  DevBuf<double> partA_, partB_, results_;
+  int resultsCap_ = 0;
+  std::vector<double> hostRes_;
+  DeviceMesh<D> m_{};
+  bool hessComputed_ = false, stepTaken_ = false;
+  int stepsTaken_ = 0;
+  bool timing_ = false;
+  std::vector<hipEvent_t> evPool_;
+  size_t evUsed_ = 0;
+  std::vector<Timed> timed_;
+  mmadmm_stats st_stats_{};
+};
+
+}  // namespace mmx
+
+using mmx::EngineBase;
+using mmx::Error;
+using mmx::guarded;
+
+struct mmadmm_engine {
+  std::unique_ptr<EngineBase> e;
+};
+
+static EngineBase& eng(mmadmm_handle h) {
+  if (!h || !h->e) throw Error(MMADMM_ERR_INVALID, "null engine handle");
+  return *h->e;
+}
+
+extern "C" {
+
+const char* mmadmm_last_error(void) { return mmx::g_last_error.c_str(); }
+int mmadmm_version(void) { return 100; }
+
+int mmadmm_create(int dim, int nP, const double* Xp, const double* Xc, int nF, const int32_t* F, const int32_t* mask,
+                  const mmadmm_params* p, mmadmm_monitor_fn fn, void* user, mmadmm_handle* out) {
+  return guarded([&] {
+    if (!out) throw Error(MMADMM_ERR_INVALID, "mmadmm_create: out is NULL");
+    *out = nullptr;
+    if ((dim != 2 && dim != 3) || nP < dim + 1 || nF < 1 || !Xp || !F || !mask || !p || !fn)
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_create: bad arguments");
+    if (!(p->dt > 0) || !(p->tau > 0) || !(p->rho > 0))
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_create: dt, tau, rho must be positive");
+    if (p->nranks > 1) throw Error(MMADMM_ERR_INVALID, "mmadmm_create: use mmadmm_create_partition for nranks > 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+      throw Error(MMADMM_ERR_HIP, "mmadmm_create: no HIP device (the engine has no CPU fallback)");
+    auto* h = new mmadmm_engine();
+    try {
+      if (dim == 2)
+        h->e.reset(new mmx::Engine<2>(nP, Xp, Xc, nF, F, mask, *p, fn, user));
+      else
+        h->e.reset(new mmx::Engine<3>(nP, Xp, Xc, nF, F, mask, *p, fn, user));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int mmadmm_step(mmadmm_handle h, int n_iters, double tol, double* Ih, int* admm_iters) {
+  return guarded([&] { eng(h).step(n_iters, tol, Ih, admm_iters); });
+}
+int mmadmm_euler_step(mmadmm_handle h, double* Ih) {
+  return guarded([&] {
+    const double r = eng(h).eulerStep();
+    if (Ih) *Ih = r;
+  });
+}
+int mmadmm_energy(mmadmm_handle h, double* E) {
+  return guarded([&] {
+    const double r = eng(h).energy();
+    if (E) *E = r;
+  });
+}
+int mmadmm_done(mmadmm_handle h) {
+  return guarded([&] { eng(h).done(); });
+}
+int mmadmm_get(mmadmm_handle h, const char* what, double* out) {
+  return guarded([&] {
+    if (!what || !out) throw Error(MMADMM_ERR_INVALID, "mmadmm_get: NULL argument");
+    eng(h).get(what, out);
+  });
+}
+int mmadmm_get_simplices(mmadmm_handle h, int32_t* F) {
+  return guarded([&] { eng(h).getSimplices(F); });
+}
+int mmadmm_sizes(mmadmm_handle h, int* nP, int* nF, int* grid_rows) {
+  return guarded([&] { eng(h).sizes(nP, nF, grid_rows); });
+}
+int mmadmm_set_timing(mmadmm_handle h, int on) {
+  return guarded([&] { eng(h).setTiming(on != 0); });
+}
+int mmadmm_stats_get(mmadmm_handle h, mmadmm_stats* s) {
+  return guarded([&] {
+    if (!s) throw Error(MMADMM_ERR_INVALID, "NULL stats");
+    eng(h).stats(s);
+  });
+}
+int mmadmm_stats_reset(mmadmm_handle h) {
+  return guarded([&] { eng(h).resetStats(); });
+}
+int mmadmm_sync(mmadmm_handle h) {
+  return guarded([&] { eng(h).sync(); });
+}
+int mmadmm_debug_blockgrad(mmadmm_handle h, int s, const double* z, const double* dxpu, int flags, double* out) {
+  return guarded([&] {
+    if (!z || !dxpu || !out) throw Error(MMADMM_ERR_INVALID, "mmadmm_debug_blockgrad: NULL argument");
+    eng(h).debugBlockGrad(s, z, dxpu, flags, out);
+  });
+}
+int mmadmm_destroy(mmadmm_handle h) {
+  return guarded([&] { delete h; });
+}
+
+int mmadmm_devmath(int op, int n, const double* in, double* out) {
+  return guarded([&] {
+    if (n < 0 || (n && (!in || !out))) throw Error(MMADMM_ERR_INVALID, "mmadmm_devmath: bad arguments");
+    mmx::DevBuf<double> a, b;
+    a.upload(in, n, nullptr);
+    b.alloc(n);
+    mmx::launch_devmath(op, n, a.p, b.p, nullptr);
+    MMX_HIP(hipMemcpy(out, b.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,366 @@
+// meshgen.cpp -- host mesh generators, reader and writers.
+//
+//   mmadmm_mesh_rect        utils::generateUniformRectMesh<D> (src/MeshUtils.h:82-335), including
+//                           its int truncation of xa..zb and its 2D jOff = i/(ny+1) boundary rule
+//   mmadmm_mesh_levelset2d  utils::meshFromLevelSetFun 2D with circlePhi (src/MeshUtils.h:404-538,
+//                           main.cpp:33-40); the O(nP*nF) remap loop (510-518) is replaced by an
+//                           O(N) ascending-rank compaction with the same result
+//   mmadmm_mesh_hexdisc     a well-shaped disc mesh (not in the reference)
+//   mmadmm_mesh_read        utils::readTriangles (src/MeshUtils.h:669-733)
+//   mmadmm_write_points / mmadmm_write_simplices: Mesh::outputPoints / outputSimplices
+//                           (src/Mesh.cpp:1067-1095), default ostream formatting (%.6g)
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+#include <string>
+
+#include "common.h"
+
+namespace mmx {
+namespace {
+
+constexpr int kFree = MMADMM_BOUNDARY_FREE, kFixed = MMADMM_BOUNDARY_FIXED, kInterior = MMADMM_INTERIOR;
+
+void rect2d(int nx, int ny, int xa, int xb, int ya, int yb, int bType, MeshBuf& m) {
+  const double hx = (xb - xa) / ((double)nx), hy = (yb - ya) / ((double)ny);
+  const int nP = (nx + 1) * (ny + 1) + nx * ny;
+  m.dim = 2;
+  m.Vp.assign((size_t)nP * 2, 0.0);
+  m.F.assign((size_t)4 * nx * ny * 3, 0);
+  m.mask.assign(nP, kInterior);
+  size_t off = 0;
+  for (int j = 0; j <= ny; j++)
+    for (int i = 0; i <= nx; i++, off++) {
+      m.Vp[off * 2] = xa + hx * i;
+      m.Vp[off * 2 + 1] = ya + hy * j;
+    }
+  for (int j = 0; j < ny; j++)  // cell midpoints
+    for (int i = 0; i < nx; i++, off++) {
+      m.Vp[off * 2] = xa + hx * i + hx / 2.0;
+      m.Vp[off * 2 + 1] = ya + hy * j + hy / 2.0;
+    }
+  const int stride = (nx + 1) * (ny + 1);
+  int32_t* F = m.F.data();
+  size_t t = 0;
+  auto tri = [&](int a, int b, int c) {
+    F[t * 3] = a;
+    F[t * 3 + 1] = b;
+    F[t * 3 + 2] = c;
+    ++t;
+  };
+  for (int j = 0; j < ny; j++)
+    for (int i = 0; i < nx; i++) {
+      const int c00 = i + j * (nx + 1), c10 = i + 1 + j * (nx + 1);
+      const int c01 = i + (j + 1) * (nx + 1), c11 = i + 1 + (j + 1) * (nx + 1);
+      const int mid = stride + i + j * nx;
+      tri(c00, mid, c01);  // left
+      tri(mid, c11, c01);  // top
+      tri(mid, c11, c10);  // right
+      tri(c00, c10, mid);  // bottom
+    }
+  for (int i = 0; i < (nx + 1) * (ny + 1); i++) {
+    const int iOff = i % (nx + 1), jOff = i / (ny + 1);
+    const bool boundary = (iOff == 0) || (iOff == nx) || (jOff == 0) || (jOff == ny);
+    m.mask[i] = boundary ? bType : kInterior;
+    const bool corner = (iOff == 0 || iOff == nx) && (jOff == 0 || jOff == ny);
+    if (corner) m.mask[i] = kFixed;
+  }
+}
+
+void rect3d(int nx, int ny, int nz, int xa, int xb, int ya, int yb, int za, int zb, int bType, MeshBuf& m) {
+  const double hx = (xb - xa) / ((double)nx), hy = (yb - ya) / ((double)ny), hz = (zb - za) / ((double)nz);
+  const int nP = (nx + 1) * (ny + 1) * (nz + 1) + nx * ny * nz;
+  m.dim = 3;
+  m.Vp.assign((size_t)nP * 3, 0.0);
+  m.F.assign((size_t)12 * nx * ny * nz * 4, 0);
+  m.mask.assign(nP, kInterior);
+  size_t off = 0;
+  for (int k = 0; k <= nz; k++)
+    for (int j = 0; j <= ny; j++)
+      for (int i = 0; i <= nx; i++, off++) {
+        m.Vp[off * 3] = xa + hx * i;
+        m.Vp[off * 3 + 1] = ya + hy * j;
+        m.Vp[off * 3 + 2] = za + hz * k;
+      }
+  for (int k = 0; k < nz; k++)
+    for (int j = 0; j < ny; j++)
+      for (int i = 0; i < nx; i++, off++) {
+        m.Vp[off * 3] = xa + hx * i + hx / 2.0;
+        m.Vp[off * 3 + 1] = ya + hy * j + hy / 2.0;
+        m.Vp[off * 3 + 2] = za + hz * k + hz / 2.0;
+      }
+  const int stride = (nx + 1) * (ny + 1) * (nz + 1);
+  const int sy = nx + 1, sz = (nx + 1) * (ny + 1);
+  int32_t* F = m.F.data();
+  size_t t = 0;
+  for (int k = 0; k < nz; k++)
+    for (int j = 0; j < ny; j++)
+      for (int i = 0; i < nx; i++) {
+        const int mid = stride + i + j * nx + k * (nx * ny);
+        auto P = [&](int di, int dj, int dk) { return (i + di) + (j + dj) * sy + (k + dk) * sz; };
+        // 12 tets per cell, two per face, each closed by the cell centre
+        const int faces[12][3][3] = {
+            {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}}, {{0, 0, 0}, {0, 1, 0}, {1, 1, 0}},  // z-
+            {{0, 0, 1}, {1, 0, 1}, {1, 1, 1}}, {{0, 0, 1}, {0, 1, 1}, {1, 1, 1}},  // z+
+            {{0, 0, 0}, {0, 1, 0}, {0, 1, 1}}, {{0, 0, 0}, {0, 0, 1}, {0, 1, 1}},  // x-
+            {{1, 0, 0}, {1, 1, 0}, {1, 1, 1}}, {{1, 0, 0}, {1, 0, 1}, {1, 1, 1}},  // x+
+            {{0, 0, 0}, {1, 0, 0}, {0, 0, 1}}, {{1, 0, 0}, {1, 0, 1}, {0, 0, 1}},  // y-
+            {{0, 1, 0}, {1, 1, 0}, {0, 1, 1}}, {{1, 1, 0}, {1, 1, 1}, {0, 1, 1}}};  // y+
+        for (int q = 0; q < 12; ++q, ++t) {
+          for (int v = 0; v < 3; ++v) F[t * 4 + v] = P(faces[q][v][0], faces[q][v][1], faces[q][v][2]);
+          F[t * 4 + 3] = mid;
+        }
+      }
+  for (int k = 0; k < nz + 1; k++)
+    for (int i = 0; i < (nx + 1) * (ny + 1); i++) {
+      const int iOff = i / (nx + 1), jOff = i % (ny + 1);
+      const bool boundary = iOff == 0 || iOff == nx || jOff == 0 || jOff == ny || k == 0 || k == nz;
+      const int o = k * (nx + 1) * (ny + 1) + i;
+      if (boundary) m.mask[o] = bType;
+      const bool ie = (iOff == 0 || iOff == nx), je = (jOff == 0 || jOff == ny), ke = (k == 0 || k == nz);
+      if ((ie && je) || (ie && ke) || (ke && je)) m.mask[o] = kFixed;  // the 12 cube edges
+    }
+}
+
+double circlePhi(double x, double y) {  // main.cpp:33-40
+  const double r = 0.35, cx = 0.5, cy = 0.5;
+  const double xval = (x - cx), yval = (y - cy);
+  return sqrt(xval * xval + yval * yval) - r;
+}
+
+void levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int bType, bool compact, MeshBuf& m) {
+  const double EPS = 1e-12;
+  MeshBuf g;
+  rect2d(nx, ny, (int)xa, (int)xb, (int)ya, (int)yb, bType, g);
+  for (auto& v : g.mask) v = kInterior;
+  const int nF0 = g.nF(), nP0 = g.nP();
+  std::vector<int> keep;
+  keep.reserve(nF0);
+  for (int s = 0; s < nF0; ++s) {  // drop simplices with every vertex outside (phi > -EPS)
+    bool out = true;
+    for (int j = 0; j < 3; ++j) {
+      const int v = g.F[(size_t)s * 3 + j];
+      out = out && circlePhi(g.Vp[(size_t)v * 2], g.Vp[(size_t)v * 2 + 1]) > -EPS;
+    }
+    if (!out) keep.push_back(s);
+  }
+  std::vector<char> used(nP0, 0);
+  for (int s : keep)
+    for (int j = 0; j < 3; ++j) used[g.F[(size_t)s * 3 + j]] = 1;
+  for (int p = 0; p < nP0; ++p) {  // project outside / on-boundary points (369-386, 478-491)
+    if (!used[p]) continue;
+    double X = g.Vp[(size_t)p * 2], Y = g.Vp[(size_t)p * 2 + 1];
+    const double phi = circlePhi(X, Y);
+    if (std::abs(phi) < EPS || phi > 0) {
+      const double xv = X - 0.5, yv = Y - 0.5;
+      const double n0 = xv / sqrt(xv * xv + yv * yv), n1 = yv / sqrt(xv * xv + yv * yv);
+      const double ph = circlePhi(X, Y);
+      X = X - ph * n0;
+      Y = Y - ph * n1;
+      g.mask[p] = bType;
+    }
+    g.Vp[(size_t)p * 2] = X;
+    g.Vp[(size_t)p * 2 + 1] = Y;
+  }
+  std::vector<int> rank(nP0, -1);
+  int cnt = 0;
+  for (int p = 0; p < nP0; ++p)
+    if (used[p]) rank[p] = cnt++;
+  m.dim = 2;
+  m.Vp.resize((size_t)cnt * 2);
+  for (int p = 0; p < nP0; ++p)
+    if (used[p]) {
+      m.Vp[(size_t)rank[p] * 2] = g.Vp[(size_t)p * 2];
+      m.Vp[(size_t)rank[p] * 2 + 1] = g.Vp[(size_t)p * 2 + 1];
+    }
+  m.F.resize(keep.size() * 3);
+  for (size_t i = 0; i < keep.size(); ++i)
+    for (int j = 0; j < 3; ++j) m.F[i * 3 + j] = rank[g.F[(size_t)keep[i] * 3 + j]];
+  if (compact) {
+    m.mask.assign(cnt, kInterior);
+    for (int p = 0; p < nP0; ++p)
+      if (used[p]) m.mask[rank[p]] = g.mask[p];
+  } else {
+    m.mask = g.mask;  // the reference leaves it indexed by pre-compaction ids
+  }
+  for (int p = 0; p < cnt; ++p)
+    if (std::abs(circlePhi(m.Vp[(size_t)p * 2], m.Vp[(size_t)p * 2 + 1])) < EPS) m.mask[p] = kFixed;
+}
+
+void hexdisc(int N, double r, double cx, double cy, int bType, MeshBuf& m) {
+  const long nP = 3L * N * (N + 1) + 1;
+  m.dim = 2;
+  m.Vp.assign((size_t)nP * 2, 0.0);
+  m.mask.assign(nP, kInterior);
+  m.Vp[0] = cx;
+  m.Vp[1] = cy;
+  const double third_pi = 1.0471975511965976;  // pi / 3
+  for (int k = 1; k <= N; ++k) {
+    const long base = 1 + 3L * k * (k - 1);
+    const double rad = r * k / N;
+    for (int j = 0; j < 6 * k; ++j) {
+      const double th = third_pi * ((double)j / k);
+      m.Vp[(size_t)(base + j) * 2] = cx + rad * cos(th);
+      m.Vp[(size_t)(base + j) * 2 + 1] = cy + rad * sin(th);
+      if (k == N) m.mask[base + j] = bType;
+    }
+  }
+  auto gid = [](int k, int s, int t) -> int32_t {
+    if (k == 0) return 0;
+    s = (s + t / k) % 6;
+    t = t % k;
+    return (int32_t)(1 + 3L * k * (k - 1) + (long)s * k + t);
+  };
+  m.F.clear();
+  m.F.reserve((size_t)6 * N * N * 3);
+  for (int k = 1; k <= N; ++k)
+    for (int s = 0; s < 6; ++s) {
+      for (int t = 0; t < k; ++t) {
+        m.F.push_back(gid(k, s, t));
+        m.F.push_back(gid(k, s, t + 1));
+        m.F.push_back(k > 1 ? gid(k - 1, s, t) : 0);
+      }
+      for (int t = 0; t < k - 1; ++t) {
+        m.F.push_back(gid(k - 1, s, t));
+        m.F.push_back(gid(k, s, t + 1));
+        m.F.push_back(gid(k - 1, s, t + 1));
+      }
+    }
+}
+
+void readMesh(int dim, const char* tri, const char* pnts, const char* mask, MeshBuf& m) {
+  m.dim = dim;
+  std::string line, word;
+  std::ifstream ft(tri);
+  if (!ft) throw Error(MMADMM_ERR_IO, std::string("cannot read ") + tri);
+  std::vector<int32_t> triData;
+  while (std::getline(ft, line)) {
+    std::stringstream s(line);
+    while (std::getline(s, word, ',')) triData.push_back(std::stoi(word));
+  }
+  std::ifstream fp(pnts);
+  if (!fp) throw Error(MMADMM_ERR_IO, std::string("cannot read ") + pnts);
+  std::vector<double> pd;
+  while (std::getline(fp, line)) {
+    std::stringstream s(line);
+    while (std::getline(s, word, ',')) pd.push_back(std::stod(word));
+  }
+  std::ifstream fm(mask);
+  if (!fm) throw Error(MMADMM_ERR_IO, std::string("cannot read ") + mask);
+  m.mask.clear();
+  int tmp;
+  while (fm >> tmp) m.mask.push_back(tmp);
+  const size_t nF = triData.size() / (dim + 1), nP = pd.size() / dim;
+  m.F.assign(triData.begin(), triData.begin() + nF * (dim + 1));
+  m.Vp.assign(pd.begin(), pd.begin() + nP * dim);
+}
+
+}  // namespace
+}  // namespace mmx
+
+using mmx::Error;
+using mmx::guarded;
+using mmx::MeshBuf;
+
+extern "C" {
+
+int mmadmm_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za,
+                     double zb, int btype, mmadmm_mesh* out) {
+  return guarded([&] {
+    if (!out || (dim != 2 && dim != 3) || nx < 1 || ny < 1 || (dim == 3 && nz < 1))
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_rect: bad arguments");
+    auto* m = new MeshBuf();
+    if (dim == 2)
+      mmx::rect2d(nx, ny, (int)xa, (int)xb, (int)ya, (int)yb, btype, *m);
+    else
+      mmx::rect3d(nx, ny, nz, (int)xa, (int)xb, (int)ya, (int)yb, (int)za, (int)zb, btype, *m);
+    *out = reinterpret_cast<mmadmm_mesh>(m);
+  });
+}
+
+int mmadmm_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int btype, int compact_mask,
+                           mmadmm_mesh* out) {
+  return guarded([&] {
+    if (!out || nx < 1 || ny < 1) throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_levelset2d: bad arguments");
+    auto* m = new MeshBuf();
+    mmx::levelset2d(nx, ny, xa, xb, ya, yb, btype, compact_mask != 0, *m);
+    *out = reinterpret_cast<mmadmm_mesh>(m);
+  });
+}
+
+int mmadmm_mesh_hexdisc(int N, double r, double cx, double cy, int btype, mmadmm_mesh* out) {
+  return guarded([&] {
+    if (!out || N < 1 || !(r > 0)) throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_hexdisc: bad arguments");
+    auto* m = new MeshBuf();
+    mmx::hexdisc(N, r, cx, cy, btype, *m);
+    *out = reinterpret_cast<mmadmm_mesh>(m);
+  });
+}
+
+int mmadmm_mesh_read(int dim, const char* tri, const char* pnts, const char* mask, mmadmm_mesh* out) {
+  return guarded([&] {
+    if (!out || !tri || !pnts || !mask || (dim != 2 && dim != 3))
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_read: bad arguments");
+    auto* m = new MeshBuf();
+    try {
+      mmx::readMesh(dim, tri, pnts, mask, *m);
+    } catch (...) {
+      delete m;
+      throw;
+    }
+    *out = reinterpret_cast<mmadmm_mesh>(m);
+  });
+}
+
+int mmadmm_mesh_sizes(mmadmm_mesh h, int* dim, int* nP, int* nF, int* mask_len) {
+  return guarded([&] {
+    if (!h) throw Error(MMADMM_ERR_INVALID, "null mesh");
+    const auto* m = reinterpret_cast<const MeshBuf*>(h);
+    if (dim) *dim = m->dim;
+    if (nP) *nP = m->nP();
+    if (nF) *nF = m->nF();
+    if (mask_len) *mask_len = (int)m->mask.size();
+  });
+}
+
+int mmadmm_mesh_copy(mmadmm_mesh h, double* Xp, int32_t* F, int32_t* mask) {
+  return guarded([&] {
+    if (!h) throw Error(MMADMM_ERR_INVALID, "null mesh");
+    const auto* m = reinterpret_cast<const MeshBuf*>(h);
+    if (Xp) std::copy(m->Vp.begin(), m->Vp.end(), Xp);
+    if (F) std::copy(m->F.begin(), m->F.end(), F);
+    if (mask) std::copy(m->mask.begin(), m->mask.end(), mask);
+  });
+}
+
+int mmadmm_mesh_free(mmadmm_mesh h) {
+  delete reinterpret_cast<MeshBuf*>(h);
+  return MMADMM_OK;
+}
+
+int mmadmm_write_points(const char* path, int dim, int nP, const double* Xp) {
+  return guarded([&] {
+    FILE* f = std::fopen(path, "w");
+    if (!f) throw Error(MMADMM_ERR_IO, std::string("cannot write ") + path);
+    for (int i = 0; i < nP; ++i) {
+      for (int j = 0; j < dim - 1; ++j) std::fprintf(f, "%.6g, ", Xp[(size_t)i * dim + j]);
+      std::fprintf(f, "%.6g\n", Xp[(size_t)i * dim + dim - 1]);
+    }
+    std::fclose(f);
+  });
+}
+
+int mmadmm_write_simplices(const char* path, int dim, int nF, const int32_t* F) {
+  return guarded([&] {
+    FILE* f = std::fopen(path, "w");
+    if (!f) throw Error(MMADMM_ERR_IO, std::string("cannot write ") + path);
+    for (int i = 0; i < nF; ++i) {
+      for (int j = 0; j < dim; ++j) std::fprintf(f, "%d, ", F[(size_t)i * (dim + 1) + j]);
+      std::fprintf(f, "%d\n", F[(size_t)i * (dim + 1) + dim]);
+    }
+    std::fclose(f);
+  });
+}
+
+}  // extern "C"

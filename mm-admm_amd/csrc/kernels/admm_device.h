@@ -1,0 +1,340 @@
+// admm_device.h -- per-simplex Huang-functional arithmetic for the CDNA4 ADMM kernels.
+//
+// One lane owns one simplex.  Every function follows the operation order of the reference
+// (src/AdaptationFunctional.cpp:102-287, src/MeshInterpolator.cpp:287-342,
+// src/MeshUtils.h:45-80) with the small-matrix conventions documented in DESIGN.md
+// (Eigen 3.4 closed-form 2x2/3x3 determinant and inverse, ascending inner sums).  The
+// translation unit is compiled with -ffp-contract=off, so no multiply-add is fused unless
+// written as fma(); the powers go through crmath.h.  The result is bit-identical to the
+// CPU oracle run with correctly rounded pow (tests/test_gpu_parity.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crmath.h"
+
+namespace mmx {
+
+enum : int { BOUNDARY_FREE = 0, BOUNDARY_FIXED = 1, INTERIOR = 2 };  // src/NodeType.h:4-8
+
+template <int D>
+struct GridView {  // the smoothed monitor grid, rows of D*D doubles
+  const double* gx;
+  const double* gy;
+  const double* gz;
+  const double* vals;
+  int nx, ny, nz;
+};
+
+template <int D>
+struct FunctionalConsts {
+  double Ehat[D * D];  // row-major, !CompMesh reference simplex (host computed, std::pow)
+  double powd;         // pow(d, d*p/2) computed on the host with std::pow
+  double w;            // 0.5*sqrt(rho)
+  int compMesh;
+};
+
+template <int D>
+struct M {  // row-major small matrix
+  double m[D][D];
+};
+
+template <int D>
+__device__ __forceinline__ double det(const M<D>& a) {
+  if constexpr (D == 2) {
+    return a.m[0][0] * a.m[1][1] - a.m[1][0] * a.m[0][1];
+  } else {
+    const double h0 = a.m[0][0] * (a.m[1][1] * a.m[2][2] - a.m[1][2] * a.m[2][1]);
+    const double h1 = a.m[0][1] * (a.m[1][0] * a.m[2][2] - a.m[1][2] * a.m[2][0]);
+    const double h2 = a.m[0][2] * (a.m[1][0] * a.m[2][1] - a.m[1][1] * a.m[2][0]);
+    return h0 - h1 + h2;
+  }
+}
+
+__device__ __forceinline__ double cof3(const M<3>& a, int i, int j) {
+  const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+  return a.m[i1][j1] * a.m[i2][j2] - a.m[i1][j2] * a.m[i2][j1];
+}
+
+template <int D>
+__device__ __forceinline__ M<D> inverse(const M<D>& a) {
+  M<D> r;
+  if constexpr (D == 2) {
+    const double invdet = 1.0 / det<D>(a);
+    r.m[0][0] = a.m[1][1] * invdet;
+    r.m[1][0] = -a.m[1][0] * invdet;
+    r.m[0][1] = -a.m[0][1] * invdet;
+    r.m[1][1] = a.m[0][0] * invdet;
+  } else {
+    const double c0 = cof3(a, 0, 0), c1 = cof3(a, 1, 0), c2 = cof3(a, 2, 0);
+    const double dt = (c0 * a.m[0][0] + c1 * a.m[1][0]) + c2 * a.m[2][0];
+    const double invdet = 1.0 / dt;
+#pragma unroll
+    for (int i = 1; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) r.m[i][j] = cof3(a, j, i) * invdet;
+    r.m[0][0] = c0 * invdet;
+    r.m[0][1] = c1 * invdet;
+    r.m[0][2] = c2 * invdet;
+  }
+  return r;
+}
+
+template <int D>
+__device__ __forceinline__ M<D> mul(const M<D>& a, const M<D>& b) {
+  M<D> c;
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      double s = a.m[i][0] * b.m[0][j];
+#pragma unroll
+      for (int k = 1; k < D; ++k) s += a.m[i][k] * b.m[k][j];
+      c.m[i][j] = s;
+    }
+  return c;
+}
+
+template <int D>
+__device__ __forceinline__ M<D> transpose(const M<D>& a) {
+  M<D> t;
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) t.m[i][j] = a.m[j][i];
+  return t;
+}
+
+template <int D>
+__device__ __forceinline__ double trace(const M<D>& a) {
+  double s = a.m[0][0];
+#pragma unroll
+  for (int i = 1; i < D; ++i) s += a.m[i][i];
+  return s;
+}
+
+// utils::findLimInfMeshPoint (src/MeshUtils.h:45-54): (int) cast, then uint32 clamp
+__device__ __forceinline__ int findLimInf(double w, const double* m, int size) {
+  uint32_t guess = (uint32_t)(int)((w - m[0]) / (m[1] - m[0]));
+  if (guess > (uint32_t)(size - 2)) guess = (uint32_t)(size - 2);
+  return (int)guess;
+}
+
+// MeshInterpolator<D>::evalMonitorOnGrid (src/MeshInterpolator.cpp:287-342)
+template <int D>
+__device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* pnt, M<D>& mv) {
+  const int xInd = findLimInf(pnt[0], g.gx, g.nx + 1);
+  const int yInd = findLimInf(pnt[1], g.gy, g.ny + 1);
+  const int nx = g.nx;
+  if constexpr (D == 2) {
+    const double xm0 = g.gx[xInd], xm1 = g.gx[xInd + 1], ym0 = g.gy[yInd], ym1 = g.gy[yInd + 1];
+    const double x = pnt[0], y = pnt[1];
+    const double norm = (1 / ((xm1 - xm0) * (ym1 - ym0)));
+    const double c0 = norm * (xm1 - x) * (ym1 - y), c1 = norm * (x - xm0) * (ym1 - y);
+    const double c2 = norm * (xm1 - x) * (y - ym0), c3 = norm * (x - xm0) * (y - ym0);
+    const double2* r0 = reinterpret_cast<const double2*>(g.vals + ((size_t)yInd * (nx + 1) + xInd) * 4);
+    const double2* r1 = reinterpret_cast<const double2*>(g.vals + ((size_t)(yInd + 1) * (nx + 1) + xInd) * 4);
+    const double2 a0 = r0[0], a1 = r0[1], b0 = r0[2], b1 = r0[3];  // g00, g10
+    const double2 e0 = r1[0], e1 = r1[1], f0 = r1[2], f1 = r1[3];  // g01, g11
+    mv.m[0][0] = c0 * a0.x + c1 * b0.x + c2 * e0.x + c3 * f0.x;
+    mv.m[0][1] = c0 * a0.y + c1 * b0.y + c2 * e0.y + c3 * f0.y;
+    mv.m[1][0] = c0 * a1.x + c1 * b1.x + c2 * e1.x + c3 * f1.x;
+    mv.m[1][1] = c0 * a1.y + c1 * b1.y + c2 * e1.y + c3 * f1.y;
+  } else {
+    const int zInd = findLimInf(pnt[2], g.gz, g.nz + 1);
+    const double xd = (pnt[0] - g.gx[xInd]) / (g.gx[xInd + 1] - g.gx[xInd]);
+    const double yd = (pnt[1] - g.gy[yInd]) / (g.gy[yInd + 1] - g.gy[yInd]);
+    const double zd = (pnt[2] - g.gz[zInd]) / (g.gz[zInd + 1] - g.gz[zInd]);
+    const double c[8] = {(1 - xd) * (1 - yd) * (1 - zd), xd * (1 - yd) * (1 - zd),
+                         (1 - xd) * yd * (1 - zd),       xd * yd * (1 - zd),
+                         (1 - xd) * (1 - yd) * zd,       xd * (1 - yd) * zd,
+                         (1 - xd) * yd * zd,             xd * yd * zd};
+    const size_t P = (size_t)(nx + 1) * (g.ny + 1);
+    const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
+    const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
+                            base + P, base + P + 1, base + P + nx + 1, base + P + nx + 2};
+    double f[9];
+#pragma unroll
+    for (int n = 0; n < 9; ++n) f[n] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double* r = g.vals + rows[q] * 9;
+#pragma unroll
+      for (int n = 0; n < 9; ++n) f[n] += c[q] * r[n];
+    }
+#pragma unroll
+    for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = f[n];
+  }
+}
+
+// exponents d*p/2, d*p/2-1 for this dimension
+template <int D>
+__device__ __forceinline__ double pow_dp2(double x) {
+  if constexpr (D == 2) return cr_pow_p15(x);
+  else return cr_pow_p225(x);
+}
+template <int D>
+__device__ __forceinline__ double pow_dp2m1(double x) {
+  if constexpr (D == 2) return cr_pow_p05(x);
+  else return cr_pow_p125(x);
+}
+
+// AdaptationFunctional<D>::blockGrad (src/AdaptationFunctional.cpp:102-287).
+// Returns the (regularised if REG) energy, sets Igt = |K| G, grad (if GRAD).
+// An inverted element (assert(Edet > 0), line 174) returns NaN and a NaN gradient.
+template <int D, bool GRAD, bool REG>
+__device__ __forceinline__ double blockGrad(const GridView<D>& g, const FunctionalConsts<D>& fc,
+                                            const double* z, const double* xi, const double* dxpu,
+                                            double* grad, double& Igt) {
+  constexpr int K = D * (D + 1);
+  const double dFact = (D == 2) ? 2.0 : 6.0;
+  M<D> mPre[D + 1], Msum;
+#pragma unroll
+  for (int i = 0; i < D + 1; i++) {
+    evalMonitor<D>(g, &z[i * D], mPre[i]);
+#pragma unroll
+    for (int r = 0; r < D; ++r)
+#pragma unroll
+      for (int c = 0; c < D; ++c) Msum.m[r][c] = ((i == 0) ? 0.0 : Msum.m[r][c]) + mPre[i].m[r][c];
+  }
+  M<D> Minv = inverse<D>(Msum);
+#pragma unroll
+  for (int r = 0; r < D; ++r)
+#pragma unroll
+    for (int c = 0; c < D; ++c) Minv.m[r][c] = Minv.m[r][c] / ((double)D + 1);
+  M<D> E, Ehat;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      E.m[r][j] = z[D * (j + 1) + r] - z[r];
+      Ehat.m[r][j] = fc.compMesh ? (xi[D * (j + 1) + r] - xi[r]) : fc.Ehat[r * D + j];
+    }
+  }
+  const double Edet = det<D>(E);
+  if (!(Edet > 0)) {
+    const double nan = __builtin_nan("");
+    if constexpr (GRAD) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) grad[i] = nan;
+    }
+    Igt = nan;
+    return nan;
+  }
+  const M<D> Einv = inverse<D>(E);
+  const M<D> FJ = mul<D>(Ehat, Einv);
+  const double detFJ = det<D>(FJ);
+  const double d = (double)D;
+  const double p = 1.5;
+  const double theta = 1.0 / 3.0;
+  const M<D> FJt = transpose<D>(FJ);
+  const M<D> MinvJt = mul<D>(Minv, FJt);
+  const M<D> JMJt = mul<D>(FJ, MinvJt);
+  const double trJMJt = trace<D>(JMJt);
+  const double detM = cr_sqrt(1.0 / det<D>(Minv));
+  const double tr_dp2 = pow_dp2<D>(trJMJt);
+  const double G = theta * detM * tr_dp2 + (1.0 - 2.0 * theta) * fc.powd * detM * cr_pow_p15(detFJ / detM);
+  const double absK = __builtin_fabs(Edet / dFact);
+  double sq = 0.0;
+  if constexpr (REG) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const double t = dxpu[i] - z[i];
+      sq = (i == 0) ? t * t : sq + t * t;
+    }
+  }
+  if constexpr (!GRAD) {
+    Igt = absK * G;
+    if constexpr (REG) return absK * G + 0.5 * fc.w * fc.w * sq;
+    return absK * G;
+  } else {
+    const double tr_dp2m1 = pow_dp2m1<D>(trJMJt);
+    const double detM_1mp = cr_pow_m05(detM);
+    M<D> dGdJ;
+    {
+      const double s = d * p * theta * detM * tr_dp2m1;
+#pragma unroll
+      for (int r = 0; r < D; ++r)
+#pragma unroll
+        for (int c = 0; c < D; ++c) dGdJ.m[r][c] = s * MinvJt.m[r][c];
+    }
+    const double dGddet = p * (1.0 - 2.0 * theta) * fc.powd * detM_1mp * cr_pow_p05(detFJ);
+    M<D> dGdM;
+    {
+      const double s1 = -0.5 * theta * d * p * detM * tr_dp2m1;
+      const M<D> MinvT = transpose<D>(Minv);
+      M<D> T;
+#pragma unroll
+      for (int r = 0; r < D; ++r)
+#pragma unroll
+        for (int c = 0; c < D; ++c) T.m[r][c] = s1 * MinvT.m[r][c];
+      T = mul<D>(mul<D>(mul<D>(T, FJt), FJ), Minv);
+      const double s2 = 0.5 * theta * detM * tr_dp2 +
+                        ((0.5 - theta) * (1.0 - p) * fc.powd) * detM_1mp * cr_pow_p15(detFJ);
+#pragma unroll
+      for (int r = 0; r < D; ++r)
+#pragma unroll
+        for (int c = 0; c < D; ++c) dGdM.m[r][c] = T.m[r][c] + s2 * Minv.m[r][c];
+    }
+    double basisComb[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) basisComb[c] = 0.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      M<D> dm;
+#pragma unroll
+      for (int r = 0; r < D; ++r)
+#pragma unroll
+        for (int c = 0; c < D; ++c) dm.m[r][c] = mPre[j + 1].m[r][c] - mPre[0].m[r][c];
+      const double tr = trace<D>(mul<D>(dGdM, dm));
+#pragma unroll
+      for (int c = 0; c < D; ++c) basisComb[c] += Einv.m[j][c] * tr;
+    }
+    const double c1 = (-G + dGddet * detFJ);
+    M<D> vLoc;
+    {
+      const M<D> P = mul<D>(mul<D>(Einv, dGdJ), FJ);
+#pragma unroll
+      for (int r = 0; r < D; ++r)
+#pragma unroll
+        for (int c = 0; c < D; ++c) vLoc.m[r][c] = c1 * Einv.m[r][c] + P.m[r][c];
+    }
+#pragma unroll
+    for (int n = 0; n < D; n++)
+#pragma unroll
+      for (int c = 0; c < D; ++c) vLoc.m[n][c] -= (basisComb[c]) / ((double)D + 1.0);
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int n = 0; n < D; n++) s += vLoc.m[n][c];
+      grad[c] = s + (basisComb[c] + 0.0);
+    }
+#pragma unroll
+    for (int n = 1; n < D + 1; n++)
+#pragma unroll
+      for (int l = 0; l < D; l++) grad[D * n + l] = -vLoc.m[n - 1][l];
+#pragma unroll
+    for (int i = 0; i < K; ++i) grad[i] *= absK;
+    double Ih = absK * G;
+    Igt = Ih;
+    if constexpr (REG) {
+      Ih += 0.5 * fc.w * fc.w * sq;
+#pragma unroll
+      for (int i = 0; i < K; ++i) grad[i] += fc.w * fc.w * (-dxpu[i] + z[i]);
+    }
+    return Ih;
+  }
+}
+
+// Mesh<D>::computeBlockGrad (src/Mesh.cpp:755-772): zero the gradient of FIXED vertices
+template <int D>
+__device__ __forceinline__ void zeroFixed(double* grad, unsigned fixedBits) {
+#pragma unroll
+  for (int i = 0; i < D + 1; i++)
+    if (fixedBits & (1u << i))
+#pragma unroll
+      for (int m = 0; m < D; ++m) grad[D * i + m] = 0.0;
+}
+
+}  // namespace mmx

@@ -1,0 +1,69 @@
+// admm_kernels.h -- host-side launch interface of the ADMM HIP kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mmx {
+
+// Slot partial-sum record written by one workgroup; reduced in a fixed order.
+// v[0] = sum Ih (BFGS entry energies), v[1] = sum |z_new - z_old|^2, v[2] = sum |Dx - z|^2,
+// v[3] = BFGS iterations, v[4] = error flags (inverted element), v[5] = max BFGS iters.
+constexpr int kNumPartials = 6;
+
+template <int D>
+struct DeviceMesh {
+  int nP, nF;
+  const int* F;           // nF x (D+1)
+  const uint8_t* sbits;   // per simplex: bit n = vertex n FIXED, bit 4+n = vertex n not INTERIOR
+  const uint8_t* nodeInterior;  // per node 1 if INTERIOR
+  const int* inc_ptr;     // nP+1, node -> incident slots, ascending simplex id
+  const int* inc_off;     // offset s*K + n*D of each incident slot
+  const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)
+  const double* Vc;       // nP x D reference positions (CompMesh) or nullptr
+  // monitor grid
+  const double* gx;
+  const double* gy;
+  const double* gz;
+  const double* gvals;
+  int gnx, gny, gnz;
+  // functional constants
+  double Ehat[9];
+  double powd, w;
+  int compMesh;
+};
+
+struct StepScalars {
+  double tau, dtsq, w, dt_over_tau;
+};
+
+template <int D>
+void launch_gather_z(const DeviceMesh<D>& m, const double* x, double* z, hipStream_t st);
+template <int D>
+void launch_grad_simplex(const DeviceMesh<D>& m, const double* x, double* gs, bool zeroFixed,
+                         double* partials, int* nblocks, hipStream_t st);
+template <int D>
+void launch_predict(const DeviceMesh<D>& m, int mode, const double* gs, double* x, double* xPrev,
+                    double* xBar, double dt_over_tau, hipStream_t st);
+template <int D>
+void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar,
+                    const double* z, const double* u, double* x, double* partials, int* nblocks,
+                    bool resid, hipStream_t st);
+template <int D>
+void launch_prox(const DeviceMesh<D>& m, bool first, double tol, const double* x, double* z,
+                 double* u, double* B, double* partials, int* nblocks, hipStream_t st);
+template <int D>
+void launch_energy(const DeviceMesh<D>& m, const double* x, double* partials, int* nblocks,
+                   hipStream_t st);
+template <int D>
+void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
+                        hipStream_t st);
+void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st);
+
+template <int D>
+void launch_debug_blockgrad(const DeviceMesh<D>& m, int s, const double* z, const double* dx, double* out,
+                            int flags, hipStream_t st);
+
+// device math self test: op 0 sqrt, 1 x^1.5, 2 x^-0.5, 3 x^2.25, 4 x^1.25
+void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st);
+
+}  // namespace mmx

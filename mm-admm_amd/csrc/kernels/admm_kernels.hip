@@ -1,0 +1,618 @@
+// admm_kernels.hip -- CDNA4 (gfx950) kernels of one ADMM time step of the MMPDE integrator.
+//
+// Reference hot path: MeshIntegrator<D>::step (src/MeshIntegrator.cpp:101-191) ->
+// Mesh<D>::prox (src/Mesh.cpp:930-994) -> bfgsOptSimplex (777-872) -> blockGrad
+// (src/AdaptationFunctional.cpp:102-287), plus the Eigen consensus algebra (D x, D^T v,
+// block-diagonal CG).  Kernels per ADMM iteration:
+//   k_prox     one lane per simplex: gather DXpU = D x + u, BFGS prox (persistent Bkinv),
+//              u <- DXpU - z, partial sums of energy, |z - zPrev|^2, BFGS iterations.
+//   k_xupdate  one lane per node: x = (tau xBar + dt^2 sum_{s ∋ v} w (w (z - u))) / t_vv in
+//              ascending simplex order (Eigen's column-major D^T product order), and
+//              partial sums of |D x - z|^2.
+// Partial sums go to per-workgroup slots and are reduced in a fixed order (deterministic).
+// Build: -ffp-contract=off (no fused multiply-add unless written), see DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include "admm_device.h"
+#include "admm_kernels.h"
+
+namespace mmx {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Workgroup reduction of NV values into partials[blockIdx.x * kNumPartials + i].
+// Values 0..3 are summed, 4 is or-ed (as a sum of flags), 5 is a max.
+template <int NV>
+__device__ __forceinline__ void block_partials(double (&v)[NV], double* partials) {
+  __shared__ double red[kBlock / 64][kNumPartials];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = (i == 5) ? wave_max(v[i]) : wave_sum(v[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < kNumPartials; ++i) red[wid][i] = (i < NV) ? v[i] : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < kNumPartials) {
+    double s = red[0][threadIdx.x];
+    for (int w = 1; w < kBlock / 64; ++w)
+      s = (threadIdx.x == 5) ? fmax(s, red[w][threadIdx.x]) : s + red[w][threadIdx.x];
+    partials[(size_t)blockIdx.x * kNumPartials + threadIdx.x] = s;
+  }
+}
+
+template <int D>
+__device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
+  GridView<D> g;
+  g.gx = m.gx;
+  g.gy = m.gy;
+  g.gz = m.gz;
+  g.vals = m.gvals;
+  g.nx = m.gnx;
+  g.ny = m.gny;
+  g.nz = m.gnz;
+  return g;
+}
+
+template <int D>
+__device__ __forceinline__ FunctionalConsts<D> constsOf(const DeviceMesh<D>& m) {
+  FunctionalConsts<D> c;
+#pragma unroll
+  for (int i = 0; i < D * D; ++i) c.Ehat[i] = m.Ehat[i];
+  c.powd = m.powd;
+  c.w = m.w;
+  c.compMesh = m.compMesh;
+  return c;
+}
+
+template <int D>
+__device__ __forceinline__ void loadVerts(const DeviceMesh<D>& m, int s, int (&f)[D + 1]) {
+#pragma unroll
+  for (int n = 0; n < D + 1; ++n) f[n] = m.F[(size_t)s * (D + 1) + n];
+}
+
+template <int D>
+__device__ __forceinline__ void gatherX(const double* x, const int (&f)[D + 1], double* out) {
+#pragma unroll
+  for (int n = 0; n < D + 1; ++n) {
+    if constexpr (D == 2) {
+      const double2 v = *reinterpret_cast<const double2*>(x + (size_t)f[n] * 2);
+      out[n * 2] = v.x;
+      out[n * 2 + 1] = v.y;
+    } else {
+#pragma unroll
+      for (int c = 0; c < D; ++c) out[n * D + c] = x[(size_t)f[n] * D + c];
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void loadXi(const DeviceMesh<D>& m, const int (&f)[D + 1], double* xi) {
+  if (m.compMesh) gatherX<D>(m.Vc, f, xi);
+}
+
+// z = D x (Dmat * x, src/MeshIntegrator.cpp:121,126): exact gather into simplex copies
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_gather_z(DeviceMesh<D> m, const double* __restrict__ x,
+                                                      double* __restrict__ z) {
+  constexpr int K = D * (D + 1);
+  const int s = blockIdx.x * kBlock + threadIdx.x;
+  if (s >= m.nF) return;
+  int f[D + 1];
+  loadVerts<D>(m, s, f);
+  double v[K];
+  gatherX<D>(x, f, v);
+#pragma unroll
+  for (int i = 0; i < K; ++i) z[(size_t)s * K + i] = v[i];
+}
+
+// per-simplex gradient of the unregularised functional (Mesh::eulerGrad / eulerStepMod)
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_grad_simplex(DeviceMesh<D> m, const double* __restrict__ x,
+                                                          double* __restrict__ gs, int zeroFixedRows,
+                                                          double* __restrict__ partials) {
+  constexpr int K = D * (D + 1);
+  const int s = blockIdx.x * kBlock + threadIdx.x;
+  double pv[5] = {0, 0, 0, 0, 0};
+  if (s < m.nF) {
+    int f[D + 1];
+    loadVerts<D>(m, s, f);
+    double z[K], xi[K], g[K], Igt;
+    gatherX<D>(x, f, z);
+    loadXi<D>(m, f, xi);
+    const double e = blockGrad<D, true, false>(gridOf<D>(m), constsOf<D>(m), z, xi, nullptr, g, Igt);
+    if (zeroFixedRows) zeroFixed<D>(g, m.sbits[s] & 0xF);
+#pragma unroll
+    for (int i = 0; i < K; ++i) gs[(size_t)s * K + i] = g[i];
+    pv[0] = e;
+    pv[4] = (e == e) ? 0.0 : 1.0;
+  }
+  block_partials<5>(pv, partials);
+}
+
+// predictX (src/Mesh.cpp:649-674) fused with xPrev = x (src/MeshIntegrator.cpp:119):
+// mode 0: xBar = x - (dt/tau) * sum_{s ∋ v} gs (ascending s);  mode 1: xBar = 2x - xPrev
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, const double* __restrict__ gs,
+                                                     const double* __restrict__ x, double* __restrict__ xPrev,
+                                                     double* __restrict__ xBar, double dt_over_tau) {
+  const int v = blockIdx.x * kBlock + threadIdx.x;
+  if (v >= m.nP) return;
+  double xv[D], xb[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) xv[c] = x[(size_t)v * D + c];
+  if (mode == 0) {
+    double g[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) g[c] = 0.0;
+    const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
+    for (int t = b; t < e; ++t) {
+      const int off = m.inc_off[t];
+#pragma unroll
+      for (int c = 0; c < D; ++c) g[c] += gs[(size_t)off + c];
+    }
+#pragma unroll
+    for (int c = 0; c < D; ++c) xb[c] = xv[c] - dt_over_tau * g[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < D; ++c) xb[c] = 2 * xv[c] - xPrev[(size_t)v * D + c];
+  }
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    xBar[(size_t)v * D + c] = xb[c];
+    xPrev[(size_t)v * D + c] = xv[c];
+  }
+}
+
+// x-update: vec = tau*xBar + dt^2 WD_T (w (z - u)), x = vec / t_vv (block-diagonal t),
+// optional |D x - z|^2 partial sums (primal residual, src/MeshIntegrator.cpp:162)
+template <int D, bool RESID>
+__global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
+                                                     const double* __restrict__ xBar,
+                                                     const double* __restrict__ z,
+                                                     const double* __restrict__ u, double* __restrict__ x,
+                                                     double* __restrict__ partials) {
+  const int v = blockIdx.x * kBlock + threadIdx.x;
+  double pv[3] = {0, 0, 0};
+  if (v < m.nP) {
+    double acc[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) acc[c] = 0.0;
+    const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
+    for (int t = b; t < e; ++t) {
+      const size_t off = (size_t)m.inc_off[t];
+#pragma unroll
+      for (int c = 0; c < D; ++c) acc[c] += sc.w * (sc.w * (z[off + c] - u[off + c]));
+    }
+    const double inv = m.invdiag[v];
+    double xn[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      xn[c] = ((sc.tau * xBar[(size_t)v * D + c]) + sc.dtsq * acc[c]) * inv;
+      x[(size_t)v * D + c] = xn[c];
+    }
+    if constexpr (RESID) {
+      double r2 = 0.0;
+      for (int t = b; t < e; ++t) {
+        const size_t off = (size_t)m.inc_off[t];
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+          const double d = xn[c] - z[off + c];
+          r2 += d * d;
+        }
+      }
+      pv[2] = r2;
+    }
+  }
+  if constexpr (RESID) block_partials<3>(pv, partials);
+}
+
+// k x k inverse: unblocked partial-pivot LU + substitution (mirrors the oracle's restatement
+// of Eigen PartialPivLU::inverse, src/Mesh.cpp:816).  Dynamic pivoting: first prox only.
+template <int K>
+__device__ void invertK(double* A) {
+  double lu[K * K];
+  int perm[K];
+  for (int i = 0; i < K; ++i) {
+    perm[i] = i;
+    for (int j = 0; j < K; ++j) lu[i * K + j] = A[i * K + j];
+  }
+  for (int k = 0; k < K; ++k) {
+    int piv = k;
+    double big = __builtin_fabs(lu[k * K + k]);
+    for (int i = k + 1; i < K; ++i)
+      if (__builtin_fabs(lu[i * K + k]) > big) {
+        big = __builtin_fabs(lu[i * K + k]);
+        piv = i;
+      }
+    if (big != 0.0) {
+      if (piv != k) {
+        for (int j = 0; j < K; ++j) {
+          const double t = lu[k * K + j];
+          lu[k * K + j] = lu[piv * K + j];
+          lu[piv * K + j] = t;
+        }
+        const int t = perm[k];
+        perm[k] = perm[piv];
+        perm[piv] = t;
+      }
+      for (int i = k + 1; i < K; ++i) lu[i * K + k] /= lu[k * K + k];
+    }
+    for (int i = k + 1; i < K; ++i)
+      for (int j = k + 1; j < K; ++j) lu[i * K + j] -= lu[i * K + k] * lu[k * K + j];
+  }
+  for (int c = 0; c < K; ++c) {
+    double xc[K];
+    for (int i = 0; i < K; ++i) xc[i] = (perm[i] == c) ? 1.0 : 0.0;
+    for (int i = 0; i < K; ++i) {
+      const double b = xc[i];
+      for (int r = i + 1; r < K; ++r) xc[r] -= b * lu[r * K + i];
+    }
+    for (int i = K - 1; i >= 0; --i) {
+      const double a = 1.0 / lu[i * K + i];
+      const double b = (xc[i] *= a);
+      for (int r = 0; r < i; ++r) xc[r] -= b * lu[r * K + i];
+    }
+    for (int i = 0; i < K; ++i) A[i * K + c] = xc[i];
+  }
+}
+
+// The prox (src/Mesh.cpp:930-994 / 777-872), one lane per simplex.  FIRST = the first prox of
+// the run, which builds the finite-difference Hessian and inverts it.
+template <int D, bool FIRST>
+__global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+                                                  double* __restrict__ zg, double* __restrict__ ug,
+                                                  double* __restrict__ Bg, double* __restrict__ partials) {
+  constexpr int K = D * (D + 1);
+  const int s = blockIdx.x * kBlock + threadIdx.x;
+  double pv[6] = {0, 0, 0, 0, 0, 0};
+  if (s < m.nF) {
+    const GridView<D> g = gridOf<D>(m);
+    const FunctionalConsts<D> fc = constsOf<D>(m);
+    int f[D + 1];
+    loadVerts<D>(m, s, f);
+    const unsigned bits = m.sbits[s];
+    const unsigned fixedBits = bits & 0xF;
+    double xi[K];
+    loadXi<D>(m, f, xi);
+    double dx[K], z[K], zold[K];
+    gatherX<D>(x, f, dx);
+    double* zs = zg + (size_t)s * K;
+    double* us = ug + (size_t)s * K;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      dx[i] = dx[i] + us[i];  // DXpU = D x + uBar
+      z[i] = zs[i];
+      zold[i] = z[i];
+    }
+    double B[K * K];
+    double* Bs = Bg + (size_t)s * K * K;
+    if constexpr (!FIRST) {
+#pragma unroll
+      for (int i = 0; i < K * K; ++i) B[i] = Bs[i];
+    }
+    double G[K], G1[K], Igt;
+    bool bad = false;
+    {
+      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G, Igt);
+      bad |= (e != e);
+    }
+    zeroFixed<D>(G, fixedBits);
+    const double Ihsave = Igt;
+    if constexpr (FIRST) {
+      const double h = 2.0 * cr_sqrt(2.220446049250313080847e-16);
+      double zp[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) zp[i] = z[i];
+      for (int i = 0; i < K; i++) {
+        zp[i] += h;
+        double Ig2;
+        blockGrad<D, true, true>(g, fc, zp, xi, dx, G1, Ig2);
+        zeroFixed<D>(G1, fixedBits);
+#pragma unroll
+        for (int r = 0; r < K; ++r) B[r * K + i] = (G1[r] - G[r]) / h;
+        zp[i] = z[i];
+      }
+#pragma unroll
+      for (int n = 0; n < D + 1; n++)
+        if (bits & (1u << (4 + n)))
+#pragma unroll
+          for (int c = 0; c < D; c++) B[(D * n + c) * K + D * n + c] = 1.0;
+      invertK<K>(B);
+    }
+    int iter;
+    for (iter = 0; iter < 50; iter++) {
+      double pk[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        double sacc = (-B[i * K]) * G[0];
+#pragma unroll
+        for (int j = 1; j < K; ++j) sacc += (-B[i * K + j]) * G[j];
+        pk[i] = sacc;
+      }
+#pragma unroll
+      for (int i = 0; i < K; ++i) z[i] += pk[i];
+      {
+        const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G1, Igt);
+        bad |= (e != e);
+      }
+      zeroFixed<D>(G1, fixedBits);
+      double Ix = 0;
+#pragma unroll
+      for (int i = 0; i < K; i++) Ix += __builtin_fabs(G1[i]);
+      double yk[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) yk[i] = G1[i] - G[i];
+      double c2 = pk[0] * yk[0];
+#pragma unroll
+      for (int i = 1; i < K; ++i) c2 += pk[i] * yk[i];
+      double yBy = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        double by = B[i * K] * yk[0];
+#pragma unroll
+        for (int j = 1; j < K; ++j) by += B[i * K + j] * yk[j];
+        yBy = (i == 0) ? yk[0] * by : yBy + yk[i] * by;
+      }
+      const double c1 = (c2 + yBy) / cr_pow_2(c2);
+      double yB[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        double sacc = yk[0] * B[j];
+#pragma unroll
+        for (int i = 1; i < K; ++i) sacc += yk[i] * B[i * K + j];
+        yB[j] = sacc;
+      }
+      // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        double row[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          double by = B[i * K] * (yk[0] * pk[j]);
+#pragma unroll
+          for (int q = 1; q < K; ++q) by += B[i * K + q] * (yk[q] * pk[j]);
+          row[j] = B[i * K + j] + (((c1 * (pk[i] * pk[j])) - by / c2) - (pk[i] * yB[j]) / c2);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) B[i * K + j] = row[j];
+      }
+#pragma unroll
+      for (int i = 0; i < K; ++i) G[i] = G1[i];
+      if (Ix < tol) break;
+    }
+    const int its = (iter == 50) ? 50 : iter + 1;
+    double dual2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      zs[i] = z[i];
+      us[i] = dx[i] - z[i];  // uBar = DXpU - z
+      const double d = z[i] - zold[i];
+      dual2 += d * d;
+    }
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) Bs[i] = B[i];
+    pv[0] = Ihsave;
+    pv[1] = dual2;
+    pv[3] = (double)its;
+    pv[4] = bad ? 1.0 : 0.0;
+    pv[5] = (double)its;
+  }
+  block_partials<6>(pv, partials);
+}
+
+// Mesh::computeEnergy (src/Mesh.cpp:496-530) on positions x
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_energy(DeviceMesh<D> m, const double* __restrict__ x,
+                                                    double* __restrict__ partials) {
+  constexpr int K = D * (D + 1);
+  const int s = blockIdx.x * kBlock + threadIdx.x;
+  double pv[5] = {0, 0, 0, 0, 0};
+  if (s < m.nF) {
+    int f[D + 1];
+    loadVerts<D>(m, s, f);
+    double z[K], xi[K], Igt;
+    gatherX<D>(x, f, z);
+    loadXi<D>(m, f, xi);
+    const double e = blockGrad<D, false, false>(gridOf<D>(m), constsOf<D>(m), z, xi, nullptr, nullptr, Igt);
+    pv[0] = e;
+    pv[4] = (e == e) ? 0.0 : 1.0;
+  }
+  block_partials<5>(pv, partials);
+}
+
+// Mesh::eulerStepMod scatter (src/Mesh.cpp:566-572): INTERIOR nodes only; x -= (dt/tau) grad
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_euler_apply(DeviceMesh<D> m, const double* __restrict__ gs,
+                                                         double* __restrict__ x, double dt_over_tau) {
+  const int v = blockIdx.x * kBlock + threadIdx.x;
+  if (v >= m.nP) return;
+  double g[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) g[c] = 0.0;
+  if (m.nodeInterior[v]) {
+    const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
+    for (int t = b; t < e; ++t) {
+      const int off = m.inc_off[t];
+#pragma unroll
+      for (int c = 0; c < D; ++c) g[c] += gs[(size_t)off + c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < D; ++c) x[(size_t)v * D + c] -= dt_over_tau * g[c];
+}
+
+__global__ void __launch_bounds__(kBlock) k_reduce_partials(const double* __restrict__ partials, int nblocks,
+                                                             double* __restrict__ out) {
+  // one workgroup; lane-strided partial sums then a fixed-shape tree
+  __shared__ double red[kBlock][kNumPartials];
+  double acc[kNumPartials];
+#pragma unroll
+  for (int i = 0; i < kNumPartials; ++i) acc[i] = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+#pragma unroll
+    for (int i = 0; i < kNumPartials; ++i) {
+      const double v = partials[(size_t)b * kNumPartials + i];
+      acc[i] = (i == 5) ? fmax(acc[i], v) : acc[i] + v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kNumPartials; ++i) red[threadIdx.x][i] = acc[i];
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+#pragma unroll
+      for (int i = 0; i < kNumPartials; ++i)
+        red[threadIdx.x][i] = (i == 5) ? fmax(red[threadIdx.x][i], red[threadIdx.x + w][i])
+                                       : red[threadIdx.x][i] + red[threadIdx.x + w][i];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < kNumPartials) out[threadIdx.x] = red[0][threadIdx.x];
+}
+
+// one-simplex evaluation for tests: Mesh::computeBlockGrad (regularised, FIXED rows zeroed)
+template <int D>
+__global__ void k_debug_blockgrad(DeviceMesh<D> m, int s, const double* __restrict__ zin,
+                                  const double* __restrict__ dxin, double* __restrict__ out, int flags) {
+  constexpr int K = D * (D + 1);
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int f[D + 1];
+  loadVerts<D>(m, s, f);
+  double z[K], dx[K], xi[K], g[K], Igt = 0;
+  for (int i = 0; i < K; ++i) {
+    z[i] = zin[i];
+    dx[i] = dxin[i];
+    g[i] = 0;
+  }
+  loadXi<D>(m, f, xi);
+  double e;
+  if (flags & 1) {
+    e = (flags & 2) ? blockGrad<D, true, true>(gridOf<D>(m), constsOf<D>(m), z, xi, dx, g, Igt)
+                    : blockGrad<D, true, false>(gridOf<D>(m), constsOf<D>(m), z, xi, dx, g, Igt);
+    zeroFixed<D>(g, m.sbits[s] & 0xF);
+  } else {
+    e = (flags & 2) ? blockGrad<D, false, true>(gridOf<D>(m), constsOf<D>(m), z, xi, dx, g, Igt)
+                    : blockGrad<D, false, false>(gridOf<D>(m), constsOf<D>(m), z, xi, dx, g, Igt);
+  }
+  out[0] = e;
+  out[1] = Igt;
+  for (int i = 0; i < K; ++i) out[2 + i] = g[i];
+}
+
+__global__ void k_devmath(int op, int n, const double* __restrict__ in, double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = in[i];
+  double r;
+  switch (op) {
+    case 0: r = cr_sqrt(x); break;
+    case 1: r = cr_pow_p15(x); break;
+    case 2: r = cr_pow_m05(x); break;
+    case 3: r = cr_pow_p225(x); break;
+    default: r = cr_pow_p125(x); break;
+  }
+  out[i] = r;
+}
+
+// ---------------------------------------------------------------------------------------
+static inline int nblk(int n) { return (n + kBlock - 1) / kBlock; }
+
+template <int D>
+void launch_gather_z(const DeviceMesh<D>& m, const double* x, double* z, hipStream_t st) {
+  if (m.nF == 0) return;
+  hipLaunchKernelGGL(k_gather_z<D>, dim3(nblk(m.nF)), dim3(kBlock), 0, st, m, x, z);
+}
+template <int D>
+void launch_grad_simplex(const DeviceMesh<D>& m, const double* x, double* gs, bool zeroFixedRows,
+                         double* partials, int* nblocks, hipStream_t st) {
+  *nblocks = nblk(m.nF);
+  if (m.nF == 0) return;
+  hipLaunchKernelGGL(k_grad_simplex<D>, dim3(*nblocks), dim3(kBlock), 0, st, m, x, gs,
+                     zeroFixedRows ? 1 : 0, partials);
+}
+template <int D>
+void launch_predict(const DeviceMesh<D>& m, int mode, const double* gs, double* x, double* xPrev,
+                    double* xBar, double dt_over_tau, hipStream_t st) {
+  if (m.nP == 0) return;
+  hipLaunchKernelGGL(k_predict<D>, dim3(nblk(m.nP)), dim3(kBlock), 0, st, m, mode, gs, x, xPrev, xBar,
+                     dt_over_tau);
+}
+template <int D>
+void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar, const double* z,
+                    const double* u, double* x, double* partials, int* nblocks, bool resid, hipStream_t st) {
+  *nblocks = nblk(m.nP);
+  if (m.nP == 0) return;
+  if (resid)
+    hipLaunchKernelGGL((k_xupdate<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
+                       partials);
+  else
+    hipLaunchKernelGGL((k_xupdate<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
+                       partials);
+}
+template <int D>
+void launch_prox(const DeviceMesh<D>& m, bool first, double tol, const double* x, double* z, double* u,
+                 double* B, double* partials, int* nblocks, hipStream_t st) {
+  *nblocks = nblk(m.nF);
+  if (m.nF == 0) return;
+  if (first)
+    hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
+  else
+    hipLaunchKernelGGL((k_prox<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
+}
+template <int D>
+void launch_energy(const DeviceMesh<D>& m, const double* x, double* partials, int* nblocks, hipStream_t st) {
+  *nblocks = nblk(m.nF);
+  if (m.nF == 0) return;
+  hipLaunchKernelGGL(k_energy<D>, dim3(*nblocks), dim3(kBlock), 0, st, m, x, partials);
+}
+template <int D>
+void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
+                        hipStream_t st) {
+  if (m.nP == 0) return;
+  hipLaunchKernelGGL(k_euler_apply<D>, dim3(nblk(m.nP)), dim3(kBlock), 0, st, m, gs, x, dt_over_tau);
+}
+void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, st, partials, nblocks, out);
+}
+template <int D>
+void launch_debug_blockgrad(const DeviceMesh<D>& m, int s, const double* z, const double* dx, double* out, int flags,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(k_debug_blockgrad<D>, dim3(1), dim3(64), 0, st, m, s, z, dx, out, flags);
+}
+template void launch_debug_blockgrad<2>(const DeviceMesh<2>&, int, const double*, const double*, double*, int,
+                                        hipStream_t);
+template void launch_debug_blockgrad<3>(const DeviceMesh<3>&, int, const double*, const double*, double*, int,
+                                        hipStream_t);
+void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_devmath, dim3((n + 255) / 256), dim3(256), 0, st, op, n, in, out);
+}
+
+#define MMX_INST(D)                                                                                     \
+  template void launch_gather_z<D>(const DeviceMesh<D>&, const double*, double*, hipStream_t);          \
+  template void launch_grad_simplex<D>(const DeviceMesh<D>&, const double*, double*, bool, double*, int*, \
+                                       hipStream_t);                                                    \
+  template void launch_predict<D>(const DeviceMesh<D>&, int, const double*, double*, double*, double*,   \
+                                  double, hipStream_t);                                                 \
+  template void launch_xupdate<D>(const DeviceMesh<D>&, const StepScalars&, const double*, const double*, \
+                                  const double*, double*, double*, int*, bool, hipStream_t);            \
+  template void launch_prox<D>(const DeviceMesh<D>&, bool, double, const double*, double*, double*,      \
+                               double*, double*, int*, hipStream_t);                                    \
+  template void launch_energy<D>(const DeviceMesh<D>&, const double*, double*, int*, hipStream_t);       \
+  template void launch_euler_apply<D>(const DeviceMesh<D>&, const double*, double*, double, hipStream_t);
+MMX_INST(2)
+MMX_INST(3)
+
+}  // namespace mmx

@@ -1,0 +1,344 @@
+// crmath.h -- correctly rounded fractional powers for the Huang functional.
+//
+// AdaptationFunctional<D>::blockGrad (reference src/AdaptationFunctional.cpp:219-236) calls
+// std::pow with the exponents d*p/2, d*p/2-1, p, 1-p, p-1 (p = 1.5):
+//   D = 2: 1.5, 0.5, 1.5, -0.5, 0.5        D = 3: 2.25, 1.25, 1.5, -0.5, 0.5
+// The GPU evaluates each power as a double-double (relative error < 2^-100) built on the
+// correctly rounded sqrt and explicit fma, and rounds it once.  When the double-double sits
+// within 2^-95 of a rounding midpoint (arguments a few ulps from 1 do this systematically),
+// an exact comparison decides the rounding: x^(p/q) > m  <=>  x^p > m^q, evaluated with
+// Shewchuk expansion arithmetic.  The result is the correctly rounded power (round to nearest,
+// ties to even); tests/test_crmath.py and tests/test_gpu_parity.py check it against
+// __float128 powq.  This matters: the first prox builds a finite-difference Hessian with
+// h = 2*sqrt(eps) (reference src/Mesh.cpp:780), which amplifies any last-bit difference in
+// the gradient by 1/h ~ 3e7.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define MMX_HD __host__ __device__ __forceinline__
+#define MMX_HD_COLD __host__ __device__ __attribute__((noinline))
+#else
+#define MMX_HD inline
+#define MMX_HD_COLD inline
+#endif
+
+namespace mmx {
+
+MMX_HD double cr_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+MMX_HD double cr_sqrt(double x) { return __builtin_sqrt(x); }
+
+// argument ranges in which the exact fallback (x^p and m^q as expansions) cannot over- or
+// underflow; outside them (never met by the functional) the device libm pow is used.
+MMX_HD bool cr_in(double x, double lo, double hi) { return x > lo && x < hi; }
+
+// ---------------------------------------------------------------- exact expansions
+namespace xp {
+constexpr int kCap = 48;
+struct Ex {
+  double t[kCap];  // nonoverlapping, increasing magnitude
+  int n;
+};
+
+MMX_HD void two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+MMX_HD void fast_two_sum(double a, double b, double& s, double& e) {  // |a| >= |b|
+  s = a + b;
+  e = b - (s - a);
+}
+MMX_HD void two_prod(double a, double b, double& p, double& e) {
+  p = a * b;
+  e = cr_fma(a, b, -p);
+}
+
+// h = e * b  (Shewchuk scale_expansion_zeroelim)
+MMX_HD_COLD void scale(const Ex& e, double b, Ex& h) {
+  h.n = 0;
+  if (e.n == 0) return;
+  double Q, hh, p1, p0, sum;
+  two_prod(e.t[0], b, Q, hh);
+  if (hh != 0) h.t[h.n++] = hh;
+  for (int i = 1; i < e.n; ++i) {
+    two_prod(e.t[i], b, p1, p0);
+    two_sum(Q, p0, sum, hh);
+    if (hh != 0 && h.n < kCap) h.t[h.n++] = hh;
+    fast_two_sum(p1, sum, Q, hh);
+    if (hh != 0 && h.n < kCap) h.t[h.n++] = hh;
+  }
+  if ((Q != 0 || h.n == 0) && h.n < kCap) h.t[h.n++] = Q;
+}
+
+// h = e + f  (Shewchuk fast_expansion_sum_zeroelim)
+MMX_HD_COLD void sum(const Ex& e, const Ex& f, Ex& h) {
+  h.n = 0;
+  int ei = 0, fi = 0;
+  double Q, Qn, hh;
+  double enow = e.n ? e.t[0] : 0.0, fnow = f.n ? f.t[0] : 0.0;
+  if (e.n == 0 && f.n == 0) return;
+  if (fi >= f.n || (ei < e.n && ((fnow > enow) == (fnow > -enow)))) {
+    Q = enow;
+    ++ei;
+    enow = (ei < e.n) ? e.t[ei] : 0.0;
+  } else {
+    Q = fnow;
+    ++fi;
+    fnow = (fi < f.n) ? f.t[fi] : 0.0;
+  }
+  if (ei < e.n && fi < f.n) {
+    if ((fnow > enow) == (fnow > -enow)) {
+      fast_two_sum(enow, Q, Qn, hh);
+      ++ei;
+      enow = (ei < e.n) ? e.t[ei] : 0.0;
+    } else {
+      fast_two_sum(fnow, Q, Qn, hh);
+      ++fi;
+      fnow = (fi < f.n) ? f.t[fi] : 0.0;
+    }
+    Q = Qn;
+    if (hh != 0 && h.n < kCap) h.t[h.n++] = hh;
+    while (ei < e.n && fi < f.n) {
+      if ((fnow > enow) == (fnow > -enow)) {
+        two_sum(Q, enow, Qn, hh);
+        ++ei;
+        enow = (ei < e.n) ? e.t[ei] : 0.0;
+      } else {
+        two_sum(Q, fnow, Qn, hh);
+        ++fi;
+        fnow = (fi < f.n) ? f.t[fi] : 0.0;
+      }
+      Q = Qn;
+      if (hh != 0 && h.n < kCap) h.t[h.n++] = hh;
+    }
+  }
+  while (ei < e.n) {
+    two_sum(Q, enow, Qn, hh);
+    ++ei;
+    enow = (ei < e.n) ? e.t[ei] : 0.0;
+    Q = Qn;
+    if (hh != 0 && h.n < kCap) h.t[h.n++] = hh;
+  }
+  while (fi < f.n) {
+    two_sum(Q, fnow, Qn, hh);
+    ++fi;
+    fnow = (fi < f.n) ? f.t[fi] : 0.0;
+    Q = Qn;
+    if (hh != 0 && h.n < kCap) h.t[h.n++] = hh;
+  }
+  if ((Q != 0 || h.n == 0) && h.n < kCap) h.t[h.n++] = Q;
+}
+
+// Shewchuk compress: shortens an expansion without changing its value
+MMX_HD_COLD void compress(Ex& e) {
+  if (e.n <= 1) return;
+  double g[kCap];
+  int bottom = e.n - 1;
+  double Q = e.t[bottom], q, Qn;
+  for (int i = e.n - 2; i >= 0; --i) {
+    fast_two_sum(Q, e.t[i], Qn, q);
+    if (q != 0) {
+      g[bottom--] = Qn;
+      Q = q;
+    } else {
+      Q = Qn;
+    }
+  }
+  g[bottom] = Q;
+  int top = 0;
+  for (int i = bottom + 1; i < e.n; ++i) {
+    fast_two_sum(g[i], Q, Qn, q);
+    Q = Qn;
+    if (q != 0) e.t[top++] = q;
+  }
+  e.t[top++] = Q;
+  e.n = top;
+}
+
+MMX_HD_COLD void mul(const Ex& a, const Ex& b, Ex& out) {
+  Ex acc, part, tmp;
+  acc.n = 0;
+  for (int j = 0; j < b.n; ++j) {
+    scale(a, b.t[j], part);
+    sum(acc, part, tmp);
+    compress(tmp);
+    acc = tmp;
+  }
+  out = acc;
+}
+
+MMX_HD void single(double v, Ex& e) {
+  e.t[0] = v;
+  e.n = 1;
+}
+
+MMX_HD_COLD void ipow(double x, int p, Ex& out) {  // x^p exactly, p >= 1
+  Ex base, r, t;
+  single(x, base);
+  single(1.0, r);
+  while (p) {
+    if (p & 1) {
+      mul(r, base, t);
+      r = t;
+    }
+    p >>= 1;
+    if (p) {
+      mul(base, base, t);
+      base = t;
+    }
+  }
+  out = r;
+}
+
+MMX_HD int sign(const Ex& e) {  // sign of the largest nonzero component
+  for (int i = e.n - 1; i >= 0; --i) {
+    if (e.t[i] > 0) return 1;
+    if (e.t[i] < 0) return -1;
+  }
+  return 0;
+}
+}  // namespace xp
+
+MMX_HD double next_toward(double h, int dir) {  // neighbouring double (h > 0)
+  uint64_t b;
+  std::memcpy(&b, &h, 8);
+  b = (dir > 0) ? b + 1 : b - 1;
+  double r;
+  std::memcpy(&r, &b, 8);
+  return r;
+}
+
+// Exact decision of round(x^(num/den)) between h and its neighbour in direction dir:
+// compares x^num with m^den (num > 0) or x^(-num) * m^den with 1 (num < 0), m = midpoint.
+MMX_HD_COLD double cr_resolve(double x, int num, int den, double h, int dir) {
+  const double nb = next_toward(h, dir);
+  const double mhi = h, mlo = (nb - h) * 0.5;  // m = h + (nb - h)/2 exactly (two terms)
+  xp::Ex m, mp, lhs, diff, neg;
+  if (std::fabs(mlo) < std::fabs(mhi)) {
+    m.t[0] = mlo;
+    m.t[1] = mhi;
+    m.n = 2;
+  } else {
+    xp::single(mhi, m);
+  }
+  // m^den
+  mp = m;
+  for (int i = 1; i < den; ++i) {
+    xp::Ex t;
+    xp::mul(mp, m, t);
+    mp = t;
+  }
+  int s;
+  if (num > 0) {  // sign(x^num - m^den)
+    xp::ipow(x, num, lhs);
+    neg = mp;
+    for (int i = 0; i < neg.n; ++i) neg.t[i] = -neg.t[i];
+    xp::sum(lhs, neg, diff);
+    s = xp::sign(diff);
+  } else {  // v > m  <=>  1 > m^den * x^(-num)
+    xp::Ex xn, prod, one;
+    xp::ipow(x, -num, xn);
+    xp::mul(mp, xn, prod);
+    for (int i = 0; i < prod.n; ++i) prod.t[i] = -prod.t[i];
+    xp::single(1.0, one);
+    xp::sum(one, prod, diff);
+    s = xp::sign(diff);
+  }
+  // s > 0: v above m; s < 0: below; s == 0: exact tie -> even mantissa
+  const bool vAboveM = (s > 0);
+  if (s == 0) {
+    uint64_t b;
+    std::memcpy(&b, &h, 8);
+    return (b & 1) ? nb : h;
+  }
+  if (dir > 0) return vAboveM ? nb : h;
+  return vAboveM ? h : nb;
+}
+
+// Round a normalised double-double (hi = RN(hi + lo)) that approximates x^(num/den) with
+// relative error < 2^-100; falls back to the exact decision near a midpoint.
+MMX_HD double cr_round(double x, int num, int den, double hi, double lo) {
+  double h, l;
+  xp::two_sum(hi, lo, h, l);
+  if (l == 0.0) {
+    // v within 2^-100 |h| of a double: decided unless h itself is near a midpoint (no)
+    return h;
+  }
+  const int dir = (l > 0) ? 1 : -1;
+  const double nb = next_toward(h, dir);
+  const double half = std::fabs(nb - h) * 0.5;
+  const double dist = half - std::fabs(l);  // distance of the dd value to the midpoint
+  if (dist > std::fabs(h) * 0x1p-95) return h;
+  return cr_resolve(x, num, den, h, dir);
+}
+
+// sqrt(x) = s + e, |error| < 2^-104 |s|
+MMX_HD void cr_sqrt_dd(double x, double& s, double& e) {
+  s = cr_sqrt(x);
+  const double r = cr_fma(-s, s, x);
+  e = r / (2.0 * s);
+}
+
+// x^0.5 -- correctly rounded sqrt
+MMX_HD double cr_pow_p05(double x) { return cr_sqrt(x); }
+
+// x^1.5
+MMX_HD double cr_pow_p15(double x) {
+  if (!cr_in(x, 1e-90, 1e90)) return ::pow(x, 1.5);
+  double s, e;
+  cr_sqrt_dd(x, s, e);
+  const double p = x * s;
+  const double lo = cr_fma(x, s, -p) + x * e;
+  return cr_round(x, 3, 2, p, lo);
+}
+
+// x^-0.5
+MMX_HD double cr_pow_m05(double x) {
+  if (!cr_in(x, 1e-100, 1e100)) return ::pow(x, -0.5);
+  double s, e;
+  cr_sqrt_dd(x, s, e);
+  const double q = 1.0 / s;
+  const double d = cr_fma(-q, s, 1.0);  // 1 - q*s, exact
+  const double u = d - q * e;           // 1 - q*(s + e)
+  return cr_round(x, -1, 2, q, q * u);
+}
+
+// x^0.25 as hi + lo, |error| < 2^-103 |hi|
+MMX_HD void cr_qrt_dd(double x, double& hi, double& lo) {
+  double s, e;
+  cr_sqrt_dd(x, s, e);  // sqrt(x) = s + e
+  double b, eb;
+  cr_sqrt_dd(s, b, eb);  // sqrt(s) = b + eb
+  hi = b;
+  lo = eb + b * (e / (2.0 * s));  // sqrt(s + e) = sqrt(s) (1 + e/(2s) - ...)
+}
+
+// x^2.25 = x^2 * x^0.25
+MMX_HD double cr_pow_p225(double x) {
+  if (!cr_in(x, 1e-30, 1e30)) return ::pow(x, 2.25);
+  double b, lo4;
+  cr_qrt_dd(x, b, lo4);
+  const double X2 = x * x;
+  const double X2e = cr_fma(x, x, -X2);
+  const double hi = X2 * b;
+  const double lo = cr_fma(X2, b, -hi) + (X2 * lo4 + X2e * b);
+  return cr_round(x, 9, 4, hi, lo);
+}
+
+// x^1.25 = x * x^0.25
+MMX_HD double cr_pow_p125(double x) {
+  if (!cr_in(x, 1e-50, 1e50)) return ::pow(x, 1.25);
+  double b, lo4;
+  cr_qrt_dd(x, b, lo4);
+  const double hi = x * b;
+  const double lo = cr_fma(x, b, -hi) + x * lo4;
+  return cr_round(x, 5, 4, hi, lo);
+}
+
+// c2^2 (reference src/Mesh.cpp:847 pow(c2, 2.0)) is exactly the rounded square.
+MMX_HD double cr_pow_2(double x) { return x * x; }
+
+}  // namespace mmx

@@ -1,0 +1,370 @@
+"""mmadmm_amd -- Python mirror of connortannahill/MM-ADMM's integrator surface on libmmadmm.so.
+
+The classes keep the reference's names and argument meaning:
+  MonitorFunction          src/MonitorFunction.h:9-21 (operator()(x, M) fills the D x D tensor)
+  Mesh(Xp, F, mask, Mon, numThreads, rho, w, tau, integrationMode, gradUse)
+                           src/Mesh.h:22-25 (w is ignored: w = 0.5*sqrt(rho), src/Mesh.cpp:451)
+  MeshIntegrator(dt, mesh) src/MeshIntegrator.h:12-51: step(nIters, tol), eulerStep(tol),
+                           getEnergy(), done(), outputX/outputZ(fname), proxTime/predTime
+Everything runs through the C-ABI in include/mmadmm.h; there is no CPU fallback: importing
+this module fails loudly when the HIP library is missing.
+"""
+import ctypes
+import os
+import time
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MMADMM_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmmadmm.so"))
+
+MMADMM_OK = 0
+BOUNDARY_FREE, BOUNDARY_FIXED, INTERIOR = 0, 1, 2
+
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_int_p = ctypes.POINTER(ctypes.c_int32)
+MONITOR_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, c_double_p, c_double_p, ctypes.c_void_p)
+
+
+class mmadmm_params(ctypes.Structure):
+    _fields_ = [("dt", ctypes.c_double), ("tau", ctypes.c_double), ("rho", ctypes.c_double),
+                ("grad_use", ctypes.c_int), ("device", ctypes.c_int), ("rank", ctypes.c_int),
+                ("nranks", ctypes.c_int)]
+
+
+class mmadmm_stats(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_longlong), ("admm_iters", ctypes.c_longlong),
+                ("bfgs_iters", ctypes.c_longlong), ("max_bfgs", ctypes.c_int),
+                ("last_primal", ctypes.c_double), ("last_dual", ctypes.c_double),
+                ("t_prox_ms", ctypes.c_double), ("t_xupdate_ms", ctypes.c_double),
+                ("t_step_ms", ctypes.c_double), ("n_prox", ctypes.c_longlong),
+                ("n_xupdate", ctypes.c_longlong), ("n_steps_timed", ctypes.c_longlong),
+                ("prox_bytes", ctypes.c_double), ("xupdate_bytes", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class MMADMMError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"mmadmm error {code}: {msg}")
+        self.code = code
+
+
+class InvertedElementError(MMADMMError):
+    """The reference aborts on assert(Edet > 0) (src/AdaptationFunctional.cpp:174)."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libmmadmm.so not built ({LIB_PATH}); run `make -C mm-admm_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    L.mmadmm_last_error.restype = ctypes.c_char_p
+    L.mmadmm_builtin_monitor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(MONITOR_FN),
+                                         ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_create.argtypes = [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, ctypes.c_int, c_int_p,
+                                c_int_p, ctypes.POINTER(mmadmm_params), MONITOR_FN, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_step.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, c_double_p,
+                              ctypes.POINTER(ctypes.c_int)]
+    L.mmadmm_euler_step.argtypes = [ctypes.c_void_p, c_double_p]
+    L.mmadmm_energy.argtypes = [ctypes.c_void_p, c_double_p]
+    L.mmadmm_done.argtypes = [ctypes.c_void_p]
+    L.mmadmm_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, c_double_p]
+    L.mmadmm_get_simplices.argtypes = [ctypes.c_void_p, c_int_p]
+    L.mmadmm_sizes.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 3
+    L.mmadmm_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.mmadmm_stats_get.argtypes = [ctypes.c_void_p, ctypes.POINTER(mmadmm_stats)]
+    L.mmadmm_stats_reset.argtypes = [ctypes.c_void_p]
+    L.mmadmm_sync.argtypes = [ctypes.c_void_p]
+    L.mmadmm_destroy.argtypes = [ctypes.c_void_p]
+    L.mmadmm_mesh_rect.argtypes = [ctypes.c_int] * 4 + [ctypes.c_double] * 6 + [ctypes.c_int,
+                                                                                 ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_mesh_levelset2d.argtypes = [ctypes.c_int] * 2 + [ctypes.c_double] * 4 + [
+        ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_mesh_hexdisc.argtypes = [ctypes.c_int] + [ctypes.c_double] * 3 + [ctypes.c_int,
+                                                                               ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_mesh_read.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                   ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_mesh_sizes.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 4
+    L.mmadmm_mesh_copy.argtypes = [ctypes.c_void_p, c_double_p, c_int_p, c_int_p]
+    L.mmadmm_mesh_free.argtypes = [ctypes.c_void_p]
+    L.mmadmm_write_points.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, c_double_p]
+    L.mmadmm_write_simplices.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, c_int_p]
+    L.mmadmm_debug_blockgrad.argtypes = [ctypes.c_void_p, ctypes.c_int, c_double_p, c_double_p, ctypes.c_int,
+                                         c_double_p]
+    L.mmadmm_devmath.argtypes = [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != MMADMM_OK:
+        msg = lib().mmadmm_last_error().decode(errors="replace")
+        if rc == 3:
+            raise InvertedElementError(rc, msg)
+        raise MMADMMError(rc, msg)
+
+
+def _dp(a):
+    return a.ctypes.data_as(c_double_p)
+
+
+def _ip(a):
+    return a.ctypes.data_as(c_int_p)
+
+
+# ---------------------------------------------------------------- meshes (src/MeshUtils.h)
+class MeshData:
+    """Vertices Xp (nP x D), simplices F (nF x D+1), node mask (NodeType values)."""
+
+    def __init__(self, dim, Xp, F, mask):
+        self.dim = dim
+        self.Xp = np.ascontiguousarray(Xp, dtype=np.float64)
+        self.F = np.ascontiguousarray(F, dtype=np.int32)
+        self.mask = np.ascontiguousarray(mask, dtype=np.int32)
+
+    @property
+    def nP(self):
+        return self.Xp.shape[0]
+
+    @property
+    def nF(self):
+        return self.F.shape[0]
+
+    @staticmethod
+    def _take(h):
+        L = lib()
+        d, nP, nF, ml = (ctypes.c_int() for _ in range(4))
+        _check(L.mmadmm_mesh_sizes(h, ctypes.byref(d), ctypes.byref(nP), ctypes.byref(nF), ctypes.byref(ml)))
+        Xp = np.zeros((nP.value, d.value))
+        F = np.zeros((nF.value, d.value + 1), dtype=np.int32)
+        mask = np.zeros(ml.value, dtype=np.int32)
+        _check(L.mmadmm_mesh_copy(h, _dp(Xp), _ip(F), _ip(mask)))
+        L.mmadmm_mesh_free(h)
+        return MeshData(d.value, Xp, F, mask)
+
+    @staticmethod
+    def rect(dim, n, xa=0, xb=1, ya=0, yb=1, za=0, zb=1, btype=BOUNDARY_FIXED):
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_mesh_rect(dim, n, n, n if dim == 3 else 0, xa, xb, ya, yb, za, zb, btype,
+                                      ctypes.byref(h)))
+        return MeshData._take(h)
+
+    @staticmethod
+    def levelset2d(n, xa=0.0, xb=1.0, ya=0.0, yb=1.0, btype=BOUNDARY_FIXED, compact_mask=True):
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_mesh_levelset2d(n, n, xa, xb, ya, yb, btype, int(compact_mask), ctypes.byref(h)))
+        return MeshData._take(h)
+
+    @staticmethod
+    def hexdisc(N, r=0.5, cx=0.5, cy=0.5, btype=BOUNDARY_FIXED):
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_mesh_hexdisc(N, r, cx, cy, btype, ctypes.byref(h)))
+        return MeshData._take(h)
+
+    @staticmethod
+    def read(dim, tri, pnts, mask):
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_mesh_read(dim, tri.encode(), pnts.encode(), mask.encode(), ctypes.byref(h)))
+        return MeshData._take(h)
+
+
+def write_points(path, Xp):
+    Xp = np.ascontiguousarray(Xp, dtype=np.float64)
+    _check(lib().mmadmm_write_points(path.encode(), Xp.shape[1], Xp.shape[0], _dp(Xp)))
+
+
+def write_simplices(path, F):
+    F = np.ascontiguousarray(F, dtype=np.int32)
+    _check(lib().mmadmm_write_simplices(path.encode(), F.shape[1] - 1, F.shape[0], _ip(F)))
+
+
+# ---------------------------------------------------------------- monitors
+class MonitorFunction:
+    """User monitor (src/MonitorFunction.h:13): override __call__(x, M) to fill M (D x D)."""
+
+    dim = 2
+
+    def __call__(self, x, M):
+        raise NotImplementedError
+
+    def _cfunc(self):
+        def tramp(dim, xp, Mp, _user):
+            x = np.ctypeslib.as_array(xp, shape=(dim,))
+            M = np.ctypeslib.as_array(Mp, shape=(dim, dim))
+            self(x, M)
+
+        self._keep = MONITOR_FN(tramp)
+        return self._keep, None
+
+
+class BuiltinMonitor(MonitorFunction):
+    """Experiments/TestMonitors/MEx* by MonType (main.cpp:836-864), evaluated natively."""
+
+    def __init__(self, dim, mon_type):
+        self.dim = dim
+        self.mon_type = mon_type
+
+    def _cfunc(self):
+        fn = MONITOR_FN()
+        user = ctypes.c_void_p()
+        _check(lib().mmadmm_builtin_monitor(self.dim, self.mon_type, ctypes.byref(fn), ctypes.byref(user)))
+        return fn, user
+
+
+# ---------------------------------------------------------------- Mesh<D> / MeshIntegrator<D>
+class Mesh:
+    """Mesh<D> (src/Mesh.h:16-126).  Holds the problem; the device state is created by
+    MeshIntegrator, which knows dt (src/MeshIntegrator.cpp:15-62)."""
+
+    def __init__(self, Xp, F, boundaryMask, Mon, numThreads=1, rho=50.0, w=None, tau=0.5,
+                 integrationMode=0, gradUse=False, Xc=None, device=-1):
+        self.Xp = np.ascontiguousarray(Xp, dtype=np.float64)
+        self.dim = self.Xp.shape[1]
+        self.F = np.ascontiguousarray(F, dtype=np.int32)
+        self.mask = np.ascontiguousarray(np.asarray(boundaryMask)[: self.Xp.shape[0]], dtype=np.int32)
+        self.Mon = Mon
+        self.numThreads = numThreads
+        self.rho = float(rho)
+        self.w = 0.5 * np.sqrt(self.rho)  # src/Mesh.cpp:451 ignores the w argument
+        self.tau = float(tau)
+        self.integrationMode = integrationMode
+        self.gradUse = bool(gradUse)
+        self.Xc = None if Xc is None else np.ascontiguousarray(Xc, dtype=np.float64)
+        self.device = device
+
+
+class Engine:
+    """Direct handle on one libmmadmm integrator (what MeshIntegrator wraps)."""
+
+    def __init__(self, mesh, dt):
+        L = lib()
+        p = mmadmm_params(dt=float(dt), tau=mesh.tau, rho=mesh.rho, grad_use=int(mesh.gradUse),
+                          device=mesh.device, rank=0, nranks=1)
+        fn, user = mesh.Mon._cfunc()
+        self._fn = fn
+        h = ctypes.c_void_p()
+        Xc = _dp(mesh.Xc) if mesh.Xc is not None else None
+        _check(L.mmadmm_create(mesh.dim, mesh.Xp.shape[0], _dp(mesh.Xp), Xc, mesh.F.shape[0], _ip(mesh.F),
+                               _ip(mesh.mask), ctypes.byref(p), fn, user, ctypes.byref(h)))
+        self.h = h
+        self.dim = mesh.dim
+        nP, nF, gr = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(L.mmadmm_sizes(h, ctypes.byref(nP), ctypes.byref(nF), ctypes.byref(gr)))
+        self.nP, self.nF, self.gridRows = nP.value, nF.value, gr.value
+        self.K = self.dim * (self.dim + 1)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mmadmm_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def step(self, nIters, tol=1e-3):
+        Ih = ctypes.c_double()
+        it = ctypes.c_int()
+        _check(lib().mmadmm_step(self.h, nIters, tol, ctypes.byref(Ih), ctypes.byref(it)))
+        return Ih.value, it.value
+
+    def euler_step(self):
+        Ih = ctypes.c_double()
+        _check(lib().mmadmm_euler_step(self.h, ctypes.byref(Ih)))
+        return Ih.value
+
+    def energy(self):
+        E = ctypes.c_double()
+        _check(lib().mmadmm_energy(self.h, ctypes.byref(E)))
+        return E.value
+
+    def done(self):
+        _check(lib().mmadmm_done(self.h))
+
+    def get(self, what):
+        n = {"x": self.nP * self.dim, "xPrev": self.nP * self.dim, "xBar": self.nP * self.dim,
+             "points": self.nP * self.dim, "z": self.nF * self.K, "u": self.nF * self.K,
+             "hess": self.nF * self.K * self.K, "gs": self.nF * self.K, "grid": self.gridRows * self.dim * self.dim,
+             "Ehat": self.dim * self.dim}[what]
+        out = np.zeros(n)
+        _check(lib().mmadmm_get(self.h, what.encode(), _dp(out)))
+        return out
+
+    def simplices(self):
+        F = np.zeros((self.nF, self.dim + 1), dtype=np.int32)
+        _check(lib().mmadmm_get_simplices(self.h, _ip(F)))
+        return F
+
+    def set_timing(self, on):
+        _check(lib().mmadmm_set_timing(self.h, int(on)))
+
+    def stats(self):
+        s = mmadmm_stats()
+        _check(lib().mmadmm_stats_get(self.h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        _check(lib().mmadmm_stats_reset(self.h))
+
+    def sync(self):
+        _check(lib().mmadmm_sync(self.h))
+
+    def block_grad(self, sid, z, dxpu=None, computeGrad=True, regularize=False):
+        """Device Mesh::computeBlockGrad of one simplex -> (energy, grad, Igt)."""
+        z = np.ascontiguousarray(z, dtype=np.float64)
+        dx = np.ascontiguousarray(dxpu if dxpu is not None else z, dtype=np.float64)
+        out = np.zeros(self.K + 2)
+        _check(lib().mmadmm_debug_blockgrad(self.h, sid, _dp(z), _dp(dx),
+                                            int(computeGrad) | (2 * int(regularize)), _dp(out)))
+        return out[0], out[2:], out[1]
+
+
+class MeshIntegrator:
+    """MeshIntegrator<D> (src/MeshIntegrator.h:12-51)."""
+
+    def __init__(self, dt, a):
+        self.a = a
+        self.dt = float(dt)
+        self.engine = Engine(a, dt)
+        self.proxTime = 0.0
+        self.predTime = 0.0
+        self.stepsTaken = 0
+
+    def step(self, nIters, tol):
+        t0 = time.perf_counter()
+        Ih, _ = self.engine.step(nIters, tol)
+        self.proxTime += time.perf_counter() - t0
+        self.stepsTaken += 1
+        return Ih
+
+    def eulerStep(self, tol=1e-3):
+        return self.engine.euler_step()
+
+    def backwardsEulerStep(self, dt, tol):
+        raise NotImplementedError("method 2 (backward Euler + LASolver) runs through mmx_sparse; "
+                                  "see include/mmx_sparse.h")
+
+    def getEnergy(self):
+        return self.engine.energy()
+
+    def done(self):
+        self.engine.done()
+
+    def outputX(self, fname):
+        write_points(fname, self.engine.get("x").reshape(-1, self.a.dim))
+
+    def outputZ(self, fname):
+        write_points(fname, self.engine.get("z").reshape(-1, self.a.dim))
+
+
+def devmath(op, x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.zeros_like(x)
+    _check(lib().mmadmm_devmath(op, x.size, _dp(x), _dp(out)))
+    return out

@@ -36,8 +36,25 @@
 #ifdef _OPENMP
 #include <omp.h>
 #endif
+#include <quadmath.h>
 
 namespace orc {
+
+// powMode 1: correctly rounded pow (long double, with a __float128 fallback when the
+// 64-bit result sits within 2 ulps of a double rounding midpoint).  powMode 0 is glibc pow,
+// i.e. the reference's semantics; glibc misrounds ~1 in 1200 calls by one ulp.
+static double crpow(double x, double y) {
+  const long double r = powl((long double)x, (long double)y);
+  if (!(r > 0) || !std::isfinite((double)r)) return pow(x, y);
+  uint64_t mant;
+  std::memcpy(&mant, &r, sizeof(mant));  // x87: 64-bit explicit mantissa in the low 8 bytes
+  const uint64_t low = mant & 0x7FF;
+  if (low >= 0x3FE && low <= 0x402) return (double)powq((__float128)x, (__float128)y);
+  if (low <= 0x002 || low >= 0x7FE) return (double)powq((__float128)x, (__float128)y);
+  return (double)r;
+}
+static int g_powMode = 0;
+static inline double opow(double x, double y) { return g_powMode ? crpow(x, y) : pow(x, y); }
 
 enum NodeType { BOUNDARY_FREE = 0, BOUNDARY_FIXED = 1, INTERIOR = 2 };  // src/NodeType.h:4-8
 
@@ -382,8 +399,10 @@ static double circlePhi(double x, double y) {  // main.cpp:33-40
 // MeshUtils.h:404-538 restated with an O(N) ascending-rank compaction in place of the
 // O(nP*nF) remap loop at 510-518 (same result).  The mask is NOT compacted: entries
 // are written at old point ids (487) and then at new ids (534-535), as in the reference.
+// compactMask != 0 remaps the mask to the new ids (the evident intent; without it the
+// reference's quirk leaves all-FIXED simplices that make bfgsOptSimplex divide 0/0).
 static void genLevelSet2D(int nx, int ny, double xa, double xb, double ya, double yb, int bType,
-                          MeshData& m) {
+                          int compactMask, MeshData& m) {
   const double EPS = 1e-12;
   MeshData g;
   genRect(2, nx, ny, 0, xa, xb, ya, yb, 0, 0, bType, g);
@@ -432,7 +451,13 @@ static void genLevelSet2D(int nx, int ny, double xa, double xb, double ya, doubl
   m.F.resize(keep.size() * 3);
   for (size_t i = 0; i < keep.size(); ++i)
     for (int j = 0; j < 3; ++j) m.F[i * 3 + j] = newId[g.F[keep[i] * 3 + j]];
-  m.mask = g.mask;  // length nP0 (uncompacted)
+  if (compactMask) {
+    m.mask.assign(cnt, INTERIOR);
+    for (int p = 0; p < nP0; ++p)
+      if (used[p]) m.mask[newId[p]] = g.mask[p];
+  } else {
+    m.mask = g.mask;  // length nP0 (uncompacted, MeshUtils.h:487)
+  }
   for (int p = 0; p < cnt; ++p) {
     const double phi = circlePhi(m.Vp[p * 2], m.Vp[p * 2 + 1]);
     if (std::abs(phi) < EPS) m.mask[p] = BOUNDARY_FIXED;
@@ -870,8 +895,8 @@ struct Integrator : Base {
     const Mat<D> JMJt = mul<D>(FJ, MinvJt);
     const double trJMJt = trace<D>(JMJt);
     const double detM = sqrt(1.0 / det<D>(Minv));
-    const double G = theta * detM * pow(trJMJt, d * p / 2.0) +
-                     (1.0 - 2.0 * theta) * pow(d, d * p / 2.0) * detM * pow(detFJ / detM, p);
+    const double G = theta * detM * opow(trJMJt, d * p / 2.0) +
+                     (1.0 - 2.0 * theta) * pow(d, d * p / 2.0) * detM * opow(detFJ / detM, p);
     const double absK = std::abs(Edet / dFact);
     auto regTerm = [&]() {
       double sq = 0.0;
@@ -887,21 +912,21 @@ struct Integrator : Base {
     }
     Mat<D> dGdJ;
     {
-      const double s = d * p * theta * detM * pow(trJMJt, d * p / 2.0 - 1);
+      const double s = d * p * theta * detM * opow(trJMJt, d * p / 2.0 - 1);
       for (int r = 0; r < D; ++r)
         for (int c = 0; c < D; ++c) dGdJ.m[r][c] = s * MinvJt.m[r][c];
     }
-    const double dGddet = p * (1.0 - 2.0 * theta) * pow(d, (d * p) / 2.0) * pow(detM, 1.0 - p) * pow(detFJ, p - 1);
+    const double dGddet = p * (1.0 - 2.0 * theta) * pow(d, (d * p) / 2.0) * opow(detM, 1.0 - p) * opow(detFJ, p - 1);
     Mat<D> dGdM;
     {
-      const double s1 = -0.5 * theta * d * p * detM * pow(trJMJt, d * p / 2.0 - 1);
+      const double s1 = -0.5 * theta * d * p * detM * opow(trJMJt, d * p / 2.0 - 1);
       Mat<D> T;
       const Mat<D> MinvT = transpose<D>(Minv);
       for (int r = 0; r < D; ++r)
         for (int c = 0; c < D; ++c) T.m[r][c] = s1 * MinvT.m[r][c];
       T = mul<D>(mul<D>(mul<D>(T, FJt), FJ), Minv);
-      const double s2 = 0.5 * theta * detM * pow(trJMJt, d * p / 2.0) +
-                        ((0.5 - theta) * (1.0 - p) * pow(d, d * p / 2.0)) * pow(detM, 1 - p) * pow(detFJ, p);
+      const double s2 = 0.5 * theta * detM * opow(trJMJt, d * p / 2.0) +
+                        ((0.5 - theta) * (1.0 - p) * pow(d, d * p / 2.0)) * opow(detM, 1 - p) * opow(detFJ, p);
       for (int r = 0; r < D; ++r)
         for (int c = 0; c < D; ++c) dGdM.m[r][c] = T.m[r][c] + s2 * Minv.m[r][c];
     }
@@ -1275,9 +1300,10 @@ void* orc_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, doubl
   genRect(dim, nx, ny, nz, xa, xb, ya, yb, za, zb, btype, *m);
   return m;
 }
-void* orc_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int btype) {
+void* orc_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int btype,
+                          int compactMask) {
   auto* m = new MeshData();
-  genLevelSet2D(nx, ny, xa, xb, ya, yb, btype, *m);
+  genLevelSet2D(nx, ny, xa, xb, ya, yb, btype, compactMask, *m);
   return m;
 }
 void* orc_mesh_read(int dim, const char* tri, const char* pnts, const char* mask) {
@@ -1420,6 +1446,8 @@ void orc_eval_monitor(void* h, const double* pnt, double* M) {
            });
 }
 void orc_monitor_at(int dim, int monType, const double* x, double* M) { monitorAt(dim, monType, x, M); }
+void orc_set_pow_mode(int mode) { g_powMode = mode; }
+double orc_crpow(double x, double y) { return crpow(x, y); }
 void orc_destroy(void* h) { delete (Base*)h; }
 
 }  // extern "C"

@@ -28,7 +28,7 @@ extern "C" {
 void* orc_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, double ya,
                     double yb, double za, double zb, int btype);
 void* orc_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb,
-                          int btype);
+                          int btype, int compactMask);
 void* orc_mesh_read(int dim, const char* tri, const char* pnts, const char* mask);
 void orc_mesh_sizes(void* m, int* nP, int* nF, int* maskLen);
 void orc_mesh_copy(void* m, double* Vp, int* F, int* mask);
@@ -56,6 +56,9 @@ double orc_block_grad(void* h, int sid, const double* z, const double* dxpu, dou
 void orc_eval_monitor(void* h, const double* pnt, double* M);
 void orc_monitor_at(int dim, int monType, const double* x, double* M);
 void orc_destroy(void* h);
+/* 0: glibc pow (reference semantics, default); 1: correctly rounded pow in blockGrad */
+void orc_set_pow_mode(int mode);
+double orc_crpow(double x, double y);
 
 #ifdef __cplusplus
 }

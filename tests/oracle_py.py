@@ -32,7 +32,7 @@ def lib():
         L.orc_mesh_rect.restype = ctypes.c_void_p
         L.orc_mesh_rect.argtypes = [ctypes.c_int] * 4 + [ctypes.c_double] * 6 + [ctypes.c_int]
         L.orc_mesh_levelset2d.restype = ctypes.c_void_p
-        L.orc_mesh_levelset2d.argtypes = [ctypes.c_int] * 2 + [ctypes.c_double] * 4 + [ctypes.c_int]
+        L.orc_mesh_levelset2d.argtypes = [ctypes.c_int] * 2 + [ctypes.c_double] * 4 + [ctypes.c_int] * 2
         L.orc_mesh_read.restype = ctypes.c_void_p
         L.orc_mesh_read.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.orc_mesh_sizes.argtypes = [ctypes.c_void_p, c_int_p, c_int_p, c_int_p]
@@ -109,8 +109,8 @@ class Mesh:
         return Mesh._from_handle(dim, h)
 
     @staticmethod
-    def levelset2d(n, xa=0.0, xb=1.0, ya=0.0, yb=1.0, btype=1):
-        h = lib().orc_mesh_levelset2d(n, n, xa, xb, ya, yb, btype)
+    def levelset2d(n, xa=0.0, xb=1.0, ya=0.0, yb=1.0, btype=1, compact_mask=True):
+        h = lib().orc_mesh_levelset2d(n, n, xa, xb, ya, yb, btype, int(compact_mask))
         return Mesh._from_handle(2, h)
 
     @staticmethod
@@ -204,3 +204,17 @@ def monitor_at(dim, monType, x):
     M = np.zeros(dim * dim)
     lib().orc_monitor_at(dim, monType, _dp(x), _dp(M))
     return M
+
+
+def set_pow_mode(mode):
+    """0: glibc pow (reference semantics); 1: correctly rounded pow (bitwise GPU parity)."""
+    L = lib()
+    L.orc_set_pow_mode.argtypes = [ctypes.c_int]
+    L.orc_set_pow_mode(int(mode))
+
+
+def crpow(x, y):
+    L = lib()
+    L.orc_crpow.restype = ctypes.c_double
+    L.orc_crpow.argtypes = [ctypes.c_double, ctypes.c_double]
+    return L.orc_crpow(float(x), float(y))

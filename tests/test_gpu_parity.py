@@ -1,0 +1,138 @@
+"""GPU (libmmadmm, HIP on MI355X) against the CPU oracle, through the C-ABI.
+
+Two bars:
+  * bit-for-bit: oracle with correctly rounded pow and the exact block-diagonal solve (the
+    arithmetic the kernels implement) -- x, z, u and Bkinv must be identical after several
+    steps with fixed ADMM iteration counts;
+  * reference semantics: oracle with glibc pow and Eigen's Jacobi-CG solve -- relative node
+    position error <= 1e-10 (north-star tolerance), energies <= 1e-12.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import mmadmm_amd as mx
+import oracle_py
+from conftest import GOLDEN, circle_mesh
+
+pytestmark = pytest.mark.gpu
+
+POS_TOL = 1e-10
+
+
+@pytest.fixture(autouse=True)
+def _pow_mode_reset():
+    yield
+    oracle_py.set_pow_mode(0)
+
+
+def cases():
+    return {
+        "C1_circle24_mex5": (lambda: circle_mesh("CircleEx24"), 5, 0.05, 0.1, 5.0, False),
+        "rect10_mex3": (lambda: oracle_py.Mesh.rect(2, 10), 3, 0.025, 0.5, 1000.0, False),
+        "rect16_mex2": (lambda: oracle_py.Mesh.rect(2, 16), 2, 0.025, 0.5, 100.0, False),
+        "hexdisc12_mex1": (lambda: _hexdisc(12), 1, 0.055, 0.5, 50.0, False),
+        "rect3d_3_mex1": (lambda: oracle_py.Mesh.rect(3, 3), 1, 0.025, 0.5, 50.0, False),
+        "circle3d6_compmesh": (lambda: circle_mesh("3DCircleEx6"), 5, 0.1, 0.1, 0.5, True),
+    }
+
+
+def _hexdisc(N):
+    m = mx.MeshData.hexdisc(N)
+    return oracle_py.Mesh(2, m.Xp, m.F, m.mask)
+
+
+def make_pair(mesh, mon, dt, tau, rho, comp, pow_mode, cg_mode, gradUse=False):
+    oracle_py.set_pow_mode(pow_mode)
+    Vc = mesh.Vp.copy() if comp else None
+    O = oracle_py.Integrator(mesh, mon, dt, tau, rho, gradUse=gradUse, Vc=Vc, cgMode=cg_mode)
+    M = mx.Mesh(mesh.Vp, mesh.F, mesh.mask, mx.BuiltinMonitor(mesh.dim, mon), rho=rho, tau=tau,
+                gradUse=gradUse, Xc=Vc)
+    G = mx.Engine(M, dt)
+    return O, G
+
+
+def test_devmath_correctly_rounded():
+    rng = np.random.default_rng(1)
+    x = np.exp(rng.uniform(-30, 30, 200000))
+    np.testing.assert_array_equal(mx.devmath(0, x), np.sqrt(x))
+    sub = x[:4000]
+    for op, y in ((1, 1.5), (2, -0.5), (3, 2.25), (4, 1.25)):
+        ref = np.array([oracle_py.crpow(v, y) for v in sub])
+        np.testing.assert_array_equal(mx.devmath(op, sub), ref)
+
+
+@pytest.mark.parametrize("name", list(cases()))
+def test_setup_identical(name):
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    O, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    np.testing.assert_array_equal(G.get("grid"), O.get("grid"))
+    np.testing.assert_array_equal(G.simplices(), O.F())
+    np.testing.assert_array_equal(G.get("Ehat"), O.get("Ehat"))
+    np.testing.assert_array_equal(G.get("x"), O.get("x"))
+    np.testing.assert_array_equal(G.get("z"), O.get("z"))
+    e_o, e_g = O.energy(), G.energy()
+    assert abs(e_o - e_g) <= 1e-13 * abs(e_o)
+
+
+@pytest.mark.parametrize("name", list(cases()))
+def test_steps_bitwise(name):
+    """Fixed iteration counts, cr pow, exact diagonal solve: bit-identical device state."""
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    O, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    nsteps = 4 if mesh.dim == 2 else 3
+    for s in range(nsteps):
+        ih_o = O.step(5, -1.0)[0]
+        ih_g = G.step(5, -1.0)[0]
+        assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
+        for f in ("x", "z", "u", "xBar"):
+            np.testing.assert_array_equal(G.get(f), O.get(f), err_msg=f"{f} step {s}")
+    np.testing.assert_array_equal(G.get("hess"), O.get("hess"))
+    assert G.stats()["bfgs_iters"] == O.bfgs_iters()
+
+
+@pytest.mark.parametrize("name", list(cases()))
+def test_steps_reference_semantics(name):
+    """glibc pow + Eigen Jacobi-CG (the reference's arithmetic): <= 1e-10 node positions."""
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    O, G = make_pair(mesh, mon, dt, tau, rho, comp, 0, 0)
+    for s in range(5):
+        ih_o, it_o = O.step(10, 1e-3)[:2]
+        ih_g, it_g = G.step(10, 1e-3)
+        assert it_o == it_g, f"ADMM iteration count differs at step {s}"
+        assert abs(ih_o - ih_g) <= 1e-11 * abs(ih_o)
+    xo, xg = O.get("x"), G.get("x")
+    err = np.abs(xo - xg).max() / np.abs(xo).max()
+    assert err <= POS_TOL, err
+
+
+def test_euler_step_parity():
+    mesh = oracle_py.Mesh.rect(2, 12)
+    O, G = make_pair(mesh, 3, 0.025, 0.5, 1000.0, False, 1, 1)
+    for _ in range(3):
+        a, b = O.euler_step(), G.euler_step()
+        assert abs(a - b) <= 1e-12 * abs(a)
+        np.testing.assert_array_equal(G.get("x"), O.get("x"))
+
+
+def test_grad_use_predictor():
+    mesh = oracle_py.Mesh.rect(2, 8)
+    O, G = make_pair(mesh, 4, 0.005, 0.1, 50.0, False, 1, 1, gradUse=True)
+    for _ in range(4):
+        O.step(3, -1.0)
+        G.step(3, -1.0)
+    np.testing.assert_array_equal(G.get("x"), O.get("x"))
+
+
+def test_inverted_element_reported():
+    """The reference aborts on assert(Edet > 0); the engine returns MMADMM_ERR_INVERTED."""
+    mesh = oracle_py.Mesh.levelset2d(40, compact_mask=False)  # reference quirk: all-FIXED simplices
+    M = mx.Mesh(mesh.Vp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5)
+    G = mx.Engine(M, 0.055)
+    with pytest.raises(mx.InvertedElementError):
+        for _ in range(3):
+            G.step(10, -1.0)
