@@ -3,8 +3,8 @@
 // MeshInterpolator<D>::updateMesh + interpolateMonitor (src/MeshInterpolator.cpp:68-130,
 // 244-259): grid size (int)pow(nP*D, 1/D) over the initial mesh bounding box, monitor at
 // every vertex, nearest vertex per grid point, then Jacobi smoothing (5 passes 2D, 2 passes
-// 3D; 366-404).  The reference's nanoflann kNN(k=1) is replaced by an exact bucket-grid
-// search; ties between equidistant vertices resolve to the lowest vertex id.
+// 3D; 366-404).  The reference's nanoflann kNN(k=1) is replaced by an exact k-d tree search;
+// ties between equidistant vertices resolve to the lowest vertex id.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -19,101 +19,90 @@ void linspace(double xa, double xb, int ns, std::vector<double>& x) {  // src/Me
   for (int i = 0; i < ns + 1; i++) x[i] = xa + ((double)i) * (xb - xa) / ns;
 }
 
+// Exact nearest vertex by a median-split k-d tree (the role of nanoflann's KDTreeSingleIndexAdaptor,
+// src/MeshInterpolator.h:61-84).  Distances are nanoflann's L2_Simple_Adaptor sums of squared
+// differences; a far subtree is pruned only when its lower bound strictly exceeds the best
+// distance, so equidistant vertices resolve to the lowest id.
 template <int D>
-class BucketNN {
+class KdNN {
  public:
-  BucketNN(const double* X, int n) : X_(X), n_(n) {
-    double hi[3];
-    for (int d = 0; d < D; ++d) {
-      lo_[d] = INFINITY;
-      hi[d] = -INFINITY;
-    }
-    for (int i = 0; i < n; ++i)
-      for (int d = 0; d < D; ++d) {
-        lo_[d] = std::min(lo_[d], X[(size_t)i * D + d]);
-        hi[d] = std::max(hi[d], X[(size_t)i * D + d]);
-      }
-    const double per = (D == 2) ? std::sqrt((double)n / 2.0) : std::cbrt((double)n / 2.0);
-    long tot = 1;
-    for (int d = 0; d < D; ++d) {
-      nb_[d] = std::max(1, (int)per);
-      h_[d] = (hi[d] - lo_[d]) / nb_[d];
-      if (!(h_[d] > 0)) h_[d] = 1.0;
-      tot *= nb_[d];
-    }
-    start_.assign(tot + 1, 0);
-    std::vector<int> cell(n);
-    for (int i = 0; i < n; ++i) {
-      cell[i] = cellOf(&X[(size_t)i * D]);
-      start_[cell[i] + 1]++;
-    }
-    for (long c = 0; c < tot; ++c) start_[c + 1] += start_[c];
-    items_.resize(n);
-    std::vector<int> fill(start_.begin(), start_.end() - 1);
-    for (int i = 0; i < n; ++i) items_[fill[cell[i]]++] = i;
+  KdNN(const double* X, int n) : X_(X), idx_(n) {
+    for (int i = 0; i < n; ++i) idx_[i] = i;
+    nodes_.reserve(2 * (n / kLeaf + 1));
+    build(0, n);
   }
 
   int nearest(const double* q) const {
-    int c[3] = {0, 0, 0};
-    for (int d = 0; d < D; ++d) c[d] = coord(q[d], d);
     double best = INFINITY;
     int bi = -1;
-    const int maxr = std::max(nb_[0], std::max(nb_[1], D == 3 ? nb_[2] : 1));
-    for (int r = 0; r <= maxr; ++r) {
-      const int zr = (D == 3) ? r : 0;
-      for (int dz = -zr; dz <= zr; ++dz)
-        for (int dy = -r; dy <= r; ++dy)
-          for (int dx = -r; dx <= r; ++dx) {
-            if (std::max(std::abs(dx), std::max(std::abs(dy), std::abs(dz))) != r) continue;
-            const int cx = c[0] + dx, cy = c[1] + dy, cz = (D == 3) ? c[2] + dz : 0;
-            if (cx < 0 || cx >= nb_[0] || cy < 0 || cy >= nb_[1]) continue;
-            if (D == 3 && (cz < 0 || cz >= nb_[2])) continue;
-            const long cell = cx + (long)nb_[0] * (cy + (long)nb_[1] * cz);
-            for (int t = start_[cell]; t < start_[cell + 1]; ++t) {
-              const int i = items_[t];
-              double dd = 0.0;  // nanoflann L2_Simple_Adaptor: sum of squared differences
-              for (int d = 0; d < D; ++d) {
-                const double df = q[d] - X_[(size_t)i * D + d];
-                dd += df * df;
-              }
-              if (dd < best || (dd == best && i < bi)) {
-                best = dd;
-                bi = i;
-              }
-            }
-          }
-      double guard = INFINITY;  // distance from q to the unsearched region
-      for (int d = 0; d < D; ++d) {
-        if (c[d] - r > 0) guard = std::min(guard, q[d] - (lo_[d] + (c[d] - r) * h_[d]));
-        if (c[d] + r + 1 < nb_[d]) guard = std::min(guard, (lo_[d] + (c[d] + r + 1) * h_[d]) - q[d]);
-      }
-      if (bi >= 0) {
-        if (guard == INFINITY) break;
-        const double g = guard * (1.0 - 1e-9);
-        if (g > 0 && best < g * g) break;
-      }
-    }
+    search(0, q, best, bi);
     return bi;
   }
 
  private:
-  int coord(double v, int d) const {
-    const int c = (int)std::floor((v - lo_[d]) / h_[d]);
-    return std::min(std::max(c, 0), nb_[d] - 1);
+  static constexpr int kLeaf = 8;
+  struct Node {
+    int lo, hi;    // point range (leaf) or split position (inner: [lo, mid), [mid, hi))
+    int axis;      // -1 for a leaf
+    double split;
+    int left, right;
+  };
+
+  int build(int lo, int hi) {
+    const int id = (int)nodes_.size();
+    nodes_.push_back(Node{lo, hi, -1, 0.0, -1, -1});
+    if (hi - lo <= kLeaf) return id;
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int t = lo; t < hi; ++t)
+      for (int d = 0; d < D; ++d) {
+        const double v = X_[(size_t)idx_[t] * D + d];
+        mn[d] = std::min(mn[d], v);
+        mx[d] = std::max(mx[d], v);
+      }
+    int axis = 0;
+    for (int d = 1; d < D; ++d)
+      if (mx[d] - mn[d] > mx[axis] - mn[axis]) axis = d;
+    const int mid = lo + (hi - lo) / 2;
+    std::nth_element(idx_.begin() + lo, idx_.begin() + mid, idx_.begin() + hi, [&](int a, int b) {
+      const double va = X_[(size_t)a * D + axis], vb = X_[(size_t)b * D + axis];
+      return va < vb || (va == vb && a < b);
+    });
+    const double split = X_[(size_t)idx_[mid] * D + axis];
+    const int l = build(lo, mid);
+    const int r = build(mid, hi);
+    nodes_[id].axis = axis;
+    nodes_[id].split = split;
+    nodes_[id].left = l;
+    nodes_[id].right = r;
+    return id;
   }
-  int cellOf(const double* p) const {
-    int c = 0, mul = 1;
-    for (int d = 0; d < D; ++d) {
-      c += coord(p[d], d) * mul;
-      mul *= nb_[d];
+
+  void search(int id, const double* q, double& best, int& bi) const {
+    const Node& nd = nodes_[id];
+    if (nd.axis < 0) {
+      for (int t = nd.lo; t < nd.hi; ++t) {
+        const int i = idx_[t];
+        double dd = 0.0;
+        for (int d = 0; d < D; ++d) {
+          const double df = q[d] - X_[(size_t)i * D + d];
+          dd += df * df;
+        }
+        if (dd < best || (dd == best && i < bi)) {
+          best = dd;
+          bi = i;
+        }
+      }
+      return;
     }
-    return c;
+    const double diff = q[nd.axis] - nd.split;
+    const int nearC = (diff < 0) ? nd.left : nd.right, farC = (diff < 0) ? nd.right : nd.left;
+    search(nearC, q, best, bi);
+    if (diff * diff <= best) search(farC, q, best, bi);
   }
+
   const double* X_;
-  int n_;
-  double lo_[3], h_[3];
-  int nb_[3];
-  std::vector<int> start_, items_;
+  std::vector<int> idx_;
+  std::vector<Node> nodes_;
 };
 
 template <int D>
@@ -143,7 +132,7 @@ void buildGrid(const double* X, int nP, mmadmm_monitor_fn fn, void* user, HostGr
     fn(D, &X[(size_t)v * D], M, user);
     std::memcpy(&monVals[(size_t)v * DD], M, DD * sizeof(double));
   }
-  BucketNN<D> nn(X, nP);
+  KdNN<D> nn(X, nP);
   const int nx = g.nx, ny = g.ny;
   if (D == 2) {
 #pragma omp parallel for schedule(dynamic, 16)

@@ -17,7 +17,7 @@
 //    (src/MeshIntegrator.cpp:51-55,138,160) restated exactly (cgMode 0); cgMode 1
 //    returns the exact block-diagonal solution x = vec / t_ii.
 //  * nanoflann kNN(k=1) in the monitor-grid set-up (src/MeshInterpolator.cpp:166-241):
-//    exact nearest vertex, ties -> lowest vertex id (nanoflann's tie order is
+//    exact nearest vertex by a k-d tree, ties -> lowest vertex id (nanoflann's tie order is
 //    tree dependent; unpinned on exact ties).
 #include "oracle.h"
 
@@ -504,58 +504,45 @@ struct Grid {
   int rows() const { return (int)(vals.size() / (D * D)); }
 };
 
-// Exact nearest neighbour (ties -> lowest id) with a uniform bucket grid.
+// Exact nearest neighbour (ties -> lowest id): recursive k-d tree over index ranges.
 template <int D>
 struct NN {
-  const double* X;
-  int n;
-  double lo[3], h[3];
-  int nb[3];
-  std::vector<int> start, items;
+  const double* X = nullptr;
+  std::vector<int> ord;
+  struct Split {
+    int axis;
+    double val;
+  };
+  std::vector<Split> splits;  // implicit tree over [lo, hi) ranges, heap-indexed
   void build(const double* Xin, int nin) {
     X = Xin;
-    n = nin;
-    double hi[3];
+    ord.resize(nin);
+    for (int i = 0; i < nin; ++i) ord[i] = i;
+    splits.assign(4 * (size_t)std::max(nin, 1), Split{-1, 0.0});
+    rec(1, 0, nin);
+  }
+  void rec(size_t node, int lo, int hi) {
+    if (hi - lo <= 6) return;
+    int axis = 0;
+    double best = -1;
     for (int d = 0; d < D; ++d) {
-      lo[d] = INFINITY;
-      hi[d] = -INFINITY;
-    }
-    for (int i = 0; i < n; ++i)
-      for (int d = 0; d < D; ++d) {
-        lo[d] = std::min(lo[d], X[i * D + d]);
-        hi[d] = std::max(hi[d], X[i * D + d]);
+      double a = INFINITY, b = -INFINITY;
+      for (int t = lo; t < hi; ++t) {
+        a = std::min(a, X[ord[t] * D + d]);
+        b = std::max(b, X[ord[t] * D + d]);
       }
-    const double per = (D == 2) ? std::sqrt((double)n / 2.0) : std::cbrt((double)n / 2.0);
-    long tot = 1;
-    for (int d = 0; d < D; ++d) {
-      nb[d] = std::max(1, (int)per);
-      h[d] = (hi[d] - lo[d]) / nb[d];
-      if (!(h[d] > 0)) h[d] = 1.0;
-      tot *= nb[d];
+      if (b - a > best) {
+        best = b - a;
+        axis = d;
+      }
     }
-    std::vector<int> cnt(tot + 1, 0);
-    std::vector<int> cell(n);
-    for (int i = 0; i < n; ++i) {
-      cell[i] = cellOf(&X[i * D]);
-      cnt[cell[i] + 1]++;
-    }
-    for (long c = 0; c < tot; ++c) cnt[c + 1] += cnt[c];
-    start = cnt;
-    items.resize(n);
-    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (int i = 0; i < n; ++i) items[fill[cell[i]]++] = i;  // ascending ids per cell
-  }
-  int coord(double v, int d) const {
-    int c = (int)std::floor((v - lo[d]) / h[d]);
-    return std::min(std::max(c, 0), nb[d] - 1);
-  }
-  int cellOf(const double* p) const {
-    int c = 0, mul = 1;
-    for (int d = 0; d < D; ++d) {
-      c += coord(p[d], d) * mul;
-      mul *= nb[d];
-    }
-    return c;
+    const int mid = (lo + hi) / 2;
+    std::nth_element(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, [&](int p, int q) {
+      return X[p * D + axis] < X[q * D + axis] || (X[p * D + axis] == X[q * D + axis] && p < q);
+    });
+    splits[node] = Split{axis, X[ord[mid] * D + axis]};
+    rec(2 * node, lo, mid);
+    rec(2 * node + 1, mid, hi);
   }
   static double dist(const double* q, const double* p) {  // nanoflann L2_Simple_Adaptor
     double r = 0.0;
@@ -565,47 +552,32 @@ struct NN {
     }
     return r;
   }
+  void visit(size_t node, int lo, int hi, const double* q, double& best, int& bi) const {
+    if (hi - lo <= 6) {
+      for (int t = lo; t < hi; ++t) {
+        const double dd = dist(q, &X[ord[t] * D]);
+        if (dd < best || (dd == best && ord[t] < bi)) {
+          best = dd;
+          bi = ord[t];
+        }
+      }
+      return;
+    }
+    const int mid = (lo + hi) / 2;
+    const Split s = splits[node];
+    const double diff = q[s.axis] - s.val;
+    if (diff < 0) {
+      visit(2 * node, lo, mid, q, best, bi);
+      if (diff * diff <= best) visit(2 * node + 1, mid, hi, q, best, bi);
+    } else {
+      visit(2 * node + 1, mid, hi, q, best, bi);
+      if (diff * diff <= best) visit(2 * node, lo, mid, q, best, bi);
+    }
+  }
   int query(const double* q) const {
-    int c[3] = {0, 0, 0};
-    for (int d = 0; d < D; ++d) c[d] = coord(q[d], d);
     double best = INFINITY;
     int bi = -1;
-    const int maxr = std::max(nb[0], std::max(nb[1], D == 3 ? nb[2] : 1));
-    for (int r = 0; r <= maxr; ++r) {
-      // visit cells at Chebyshev distance exactly r
-      const int zr = (D == 3) ? r : 0;
-      for (int dz = -zr; dz <= zr; ++dz)
-        for (int dy = -r; dy <= r; ++dy)
-          for (int dx = -r; dx <= r; ++dx) {
-            const int m = std::max(std::abs(dx), std::max(std::abs(dy), std::abs(dz)));
-            if (m != r) continue;
-            const int cx = c[0] + dx, cy = c[1] + dy, cz = (D == 3) ? c[2] + dz : 0;
-            if (cx < 0 || cx >= nb[0] || cy < 0 || cy >= nb[1]) continue;
-            if (D == 3 && (cz < 0 || cz >= nb[2])) continue;
-            const long cell = cx + (long)nb[0] * (cy + (long)nb[1] * cz);
-            for (int t = start[cell]; t < start[cell + 1]; ++t) {
-              const int i = items[t];
-              const double dd = dist(q, &X[i * D]);
-              if (dd < best || (dd == best && i < bi)) {
-                best = dd;
-                bi = i;
-              }
-            }
-          }
-      // guaranteed radius after ring r: distance from q to the outside of the searched box
-      double guard = INFINITY;
-      for (int d = 0; d < D; ++d) {
-        const double lo_e = lo[d] + (c[d] - r) * h[d], hi_e = lo[d] + (c[d] + r + 1) * h[d];
-        const bool openLo = (c[d] - r) > 0, openHi = (c[d] + r + 1) < nb[d];
-        if (openLo) guard = std::min(guard, q[d] - lo_e);
-        if (openHi) guard = std::min(guard, hi_e - q[d]);
-      }
-      if (bi >= 0) {
-        if (guard == INFINITY) break;
-        const double g = guard * (1.0 - 1e-9);
-        if (g > 0 && best < g * g) break;
-      }
-    }
+    visit(1, 0, (int)ord.size(), q, best, bi);
     return bi;
   }
 };
