@@ -139,7 +139,7 @@ def main():
                                % (args.disc_n, mesh.nP, mesh.nF, args.admm_iter),
                    "nodes_per_gpu": mesh.nP, "simplices_per_gpu": mesh.nF, "admm_iter": args.admm_iter,
                    "parallelism": "replicas" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": "k_prox<2,false>",
+        "roofline": {"bound": "hbm", "kernel": "k_prox_lds<2>",
                      "achieved": round(prox_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": st["prox_bytes"],

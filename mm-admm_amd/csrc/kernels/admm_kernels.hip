@@ -19,6 +19,7 @@
 namespace mmx {
 
 constexpr int kBlock = 256;
+constexpr int kLdsStride = kBlock + 1;  // padded SoA stride of the LDS Bkinv image
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -268,6 +269,103 @@ __device__ void invertK(double* A) {
   }
 }
 
+
+// Bkinv accessors: registers (first prox) or the workgroup's LDS image (steady state)
+template <int K>
+struct RegB {
+  static constexpr bool kRowFence = false;
+  double* b;
+  __device__ __forceinline__ double& operator()(int i, int j) const { return b[i * K + j]; }
+};
+// LDS image: a scheduling fence per matrix row keeps one row live at a time (otherwise the
+// scheduler hoists all K*K reads and the kernel spills)
+template <int K>
+struct LdsB {
+  static constexpr bool kRowFence = true;
+  double* base;  // &lds[tid], entries strided by kLdsStride
+  __device__ __forceinline__ double& operator()(int i, int j) const { return base[(i * K + j) * kLdsStride]; }
+};
+#define MMX_ROW_FENCE(BA) \
+  if constexpr (BA::kRowFence) __builtin_amdgcn_sched_barrier(0)
+
+// Mesh<D>::bfgsOptSimplex iteration loop (src/Mesh.cpp:827-856): inverse-BFGS without line
+// search, <= 50 iterations, stop when ||grad||_1 < tol.  Returns the iteration count.
+template <int D, class BA>
+__device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g, const FunctionalConsts<D>& fc,
+                                               double* z, const double* xi, const double* dx, double* G,
+                                               unsigned fixedBits, double tol, bool& bad) {
+  constexpr int K = D * (D + 1);
+  int iter;
+  for (iter = 0; iter < 50; iter++) {
+    double pk[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      MMX_ROW_FENCE(BA);
+      double sacc = (-B(i, 0)) * G[0];
+#pragma unroll
+      for (int j = 1; j < K; ++j) sacc += (-B(i, j)) * G[j];
+      pk[i] = sacc;
+    }
+    MMX_ROW_FENCE(BA);
+#pragma unroll
+    for (int i = 0; i < K; ++i) z[i] += pk[i];
+    double G1[K], Igt;
+    {
+      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G1, Igt);
+      bad |= (e != e);
+    }
+    zeroFixed<D>(G1, fixedBits);
+    double Ix = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) Ix += __builtin_fabs(G1[i]);
+    double yk[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) yk[i] = G1[i] - G[i];
+    double c2 = pk[0] * yk[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) c2 += pk[i] * yk[i];
+    // one pass over B: By_i = sum_j B_ij y_j, yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij
+    double yBy = 0.0, yB[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      MMX_ROW_FENCE(BA);
+      double row[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) row[j] = B(i, j);
+      double by = row[0] * yk[0];
+#pragma unroll
+      for (int j = 1; j < K; ++j) by += row[j] * yk[j];
+      yBy = (i == 0) ? yk[0] * by : yBy + yk[i] * by;
+#pragma unroll
+      for (int j = 0; j < K; ++j) yB[j] = (i == 0) ? yk[0] * row[j] : yB[j] + yk[i] * row[j];
+    }
+    MMX_ROW_FENCE(BA);
+    const double c1 = (c2 + yBy) / cr_pow_2(c2);
+    // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      MMX_ROW_FENCE(BA);
+      double row[K], nrow[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) row[j] = B(i, j);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        double by = row[0] * (yk[0] * pk[j]);
+#pragma unroll
+        for (int q = 1; q < K; ++q) by += row[q] * (yk[q] * pk[j]);
+        nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - by / c2) - (pk[i] * yB[j]) / c2);
+      }
+#pragma unroll
+      for (int j = 0; j < K; ++j) B(i, j) = nrow[j];
+    }
+    MMX_ROW_FENCE(BA);
+#pragma unroll
+    for (int i = 0; i < K; ++i) G[i] = G1[i];
+    if (Ix < tol) break;
+  }
+  return (iter == 50) ? 50 : iter + 1;
+}
+
 // The prox (src/Mesh.cpp:930-994 / 777-872), one lane per simplex.  FIRST = the first prox of
 // the run, which builds the finite-difference Hessian and inverts it.
 template <int D, bool FIRST>
@@ -304,6 +402,7 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
     }
     double G[K], G1[K], Igt;
     bool bad = false;
+    (void)G1;
     {
       const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G, Igt);
       bad |= (e != e);
@@ -331,68 +430,8 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
           for (int c = 0; c < D; c++) B[(D * n + c) * K + D * n + c] = 1.0;
       invertK<K>(B);
     }
-    int iter;
-    for (iter = 0; iter < 50; iter++) {
-      double pk[K];
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        double sacc = (-B[i * K]) * G[0];
-#pragma unroll
-        for (int j = 1; j < K; ++j) sacc += (-B[i * K + j]) * G[j];
-        pk[i] = sacc;
-      }
-#pragma unroll
-      for (int i = 0; i < K; ++i) z[i] += pk[i];
-      {
-        const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G1, Igt);
-        bad |= (e != e);
-      }
-      zeroFixed<D>(G1, fixedBits);
-      double Ix = 0;
-#pragma unroll
-      for (int i = 0; i < K; i++) Ix += __builtin_fabs(G1[i]);
-      double yk[K];
-#pragma unroll
-      for (int i = 0; i < K; ++i) yk[i] = G1[i] - G[i];
-      double c2 = pk[0] * yk[0];
-#pragma unroll
-      for (int i = 1; i < K; ++i) c2 += pk[i] * yk[i];
-      double yBy = 0.0;
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        double by = B[i * K] * yk[0];
-#pragma unroll
-        for (int j = 1; j < K; ++j) by += B[i * K + j] * yk[j];
-        yBy = (i == 0) ? yk[0] * by : yBy + yk[i] * by;
-      }
-      const double c1 = (c2 + yBy) / cr_pow_2(c2);
-      double yB[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        double sacc = yk[0] * B[j];
-#pragma unroll
-        for (int i = 1; i < K; ++i) sacc += yk[i] * B[i * K + j];
-        yB[j] = sacc;
-      }
-      // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        double row[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          double by = B[i * K] * (yk[0] * pk[j]);
-#pragma unroll
-          for (int q = 1; q < K; ++q) by += B[i * K + q] * (yk[q] * pk[j]);
-          row[j] = B[i * K + j] + (((c1 * (pk[i] * pk[j])) - by / c2) - (pk[i] * yB[j]) / c2);
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j) B[i * K + j] = row[j];
-      }
-#pragma unroll
-      for (int i = 0; i < K; ++i) G[i] = G1[i];
-      if (Ix < tol) break;
-    }
-    const int its = (iter == 50) ? 50 : iter + 1;
+    RegB<K> Bacc{B};
+    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad);
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -408,6 +447,91 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
     pv[3] = (double)its;
     pv[4] = bad ? 1.0 : 0.0;
     pv[5] = (double)its;
+  }
+  block_partials<6>(pv, partials);
+}
+
+
+// Steady-state prox (every prox after the first), Bkinv staged through LDS.  The workgroup's
+// 256 simplices own one contiguous Bkinv chunk (256 x K*K doubles): it is read and written
+// back with 16-byte-per-lane fully coalesced accesses and held in LDS as a padded
+// structure-of-arrays image [K*K][257], so each lane's BFGS reads its own matrix
+// conflict-free and the registers it frees give two waves per SIMD.
+template <int D>
+__global__ void __launch_bounds__(kBlock, 2) k_prox_lds(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+                                                        double* __restrict__ zg, double* __restrict__ ug,
+                                                        double* __restrict__ Bg, double* __restrict__ partials) {
+  constexpr int K = D * (D + 1), KK = K * K;
+  __shared__ __attribute__((aligned(16))) double lds[KK * kLdsStride];
+  const int tid = threadIdx.x;
+  const int s0 = blockIdx.x * kBlock;
+  const int nIn = min(kBlock, m.nF - s0);
+  double* chunk = Bg + (size_t)s0 * KK;
+  const int tot = nIn * KK;  // even: K*K is even
+#pragma unroll 4
+  for (int e = tid * 2; e < tot; e += kBlock * 2) {
+    const double2 v = *reinterpret_cast<const double2*>(chunk + e);
+    const int sa = e / KK, ka = e - sa * KK;
+    const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
+    lds[ka * kLdsStride + sa] = v.x;
+    lds[kb * kLdsStride + sb] = v.y;
+  }
+  __syncthreads();
+  double pv[6] = {0, 0, 0, 0, 0, 0};
+  const int s = s0 + tid;
+  if (tid < nIn) {
+    const GridView<D> g = gridOf<D>(m);
+    const FunctionalConsts<D> fc = constsOf<D>(m);
+    int f[D + 1];
+    loadVerts<D>(m, s, f);
+    const unsigned fixedBits = m.sbits[s] & 0xF;
+    double xi[K];
+    loadXi<D>(m, f, xi);
+    double dx[K], z[K];
+    gatherX<D>(x, f, dx);
+    double* zs = zg + (size_t)s * K;
+    double* us = ug + (size_t)s * K;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      dx[i] = dx[i] + us[i];  // DXpU = D x + uBar
+      z[i] = zs[i];
+    }
+    double G[K], Igt;
+    bool bad = false;
+    {
+      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G, Igt);
+      bad |= (e != e);
+    }
+    zeroFixed<D>(G, fixedBits);
+    const double Ihsave = Igt;
+    LdsB<K> Bacc{lds + tid};
+    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad);
+    double dual2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const double d = z[i] - zs[i];
+      dual2 += d * d;
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      zs[i] = z[i];
+      us[i] = dx[i] - z[i];  // uBar = DXpU - z
+    }
+    pv[0] = Ihsave;
+    pv[1] = dual2;
+    pv[3] = (double)its;
+    pv[4] = bad ? 1.0 : 0.0;
+    pv[5] = (double)its;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int e = tid * 2; e < tot; e += kBlock * 2) {
+    const int sa = e / KK, ka = e - sa * KK;
+    const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
+    double2 v;
+    v.x = lds[ka * kLdsStride + sa];
+    v.y = lds[kb * kLdsStride + sb];
+    *reinterpret_cast<double2*>(chunk + e) = v;
   }
   block_partials<6>(pv, partials);
 }
@@ -566,10 +690,14 @@ void launch_prox(const DeviceMesh<D>& m, bool first, double tol, const double* x
                  double* B, double* partials, int* nblocks, hipStream_t st) {
   *nblocks = nblk(m.nF);
   if (m.nF == 0) return;
-  if (first)
+  if (first) {
     hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
-  else
-    hipLaunchKernelGGL((k_prox<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
+  } else {
+    if constexpr (D == 2)
+      hipLaunchKernelGGL((k_prox_lds<D>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
+    else
+      hipLaunchKernelGGL((k_prox<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
+  }
 }
 template <int D>
 void launch_energy(const DeviceMesh<D>& m, const double* x, double* partials, int* nblocks, hipStream_t st) {
