@@ -60,6 +60,16 @@ void orc_destroy(void* h);
 void orc_set_pow_mode(int mode);
 double orc_crpow(double x, double y);
 
+/* ---- LASolver (backward Euler's ILU(0)-preconditioned CG-STAB), oracle/lasolver.cpp ---- */
+int orc_la_pack(int n, int nent, const int* rows, const int* cols, int no_diag, int* ia, int* ja, int cap);
+int orc_la_mesh_pattern(int dim, int nP, int nF, const int* F, int* ia, int* ja, int cap);
+int orc_la_matmult(int n, const int* ia, const int* ja, const double* a, const double* x, double* y);
+int orc_la_ilu0(int n, const int* ia, const int* ja, const double* a, double* af);
+int orc_la_ilu_solve(int n, const int* ia, const int* ja, const double* af, const double* b, double* x);
+int orc_la_solve(int n, const int* ia, const int* ja, const double* a, const double* b, const double* toler,
+                 int nitmax, double resid_reduc, int new_rhat, int initial_guess, double* x, int* nitr,
+                 double* rms_hist);
+
 #ifdef __cplusplus
 }
 #endif
