@@ -42,6 +42,29 @@ int guarded(Fn&& f) {
   }
 }
 
+// Owning device buffer (hipMalloc / hipFree).
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  void alloc(size_t count) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = count;
+    if (count) MMX_HIP(hipMalloc(&p, count * sizeof(T)));
+  }
+  void upload(const T* h, size_t count, hipStream_t st) {
+    alloc(count);
+    if (count) MMX_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
+  }
+};
+
 // Built-in monitors (Experiments/TestMonitors/MEx*.h restated), by MonType
 void builtin_monitor_eval(int dim, int monType, const double* x, double* M);
 

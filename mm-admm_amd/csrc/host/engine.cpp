@@ -21,27 +21,6 @@ thread_local std::string g_last_error;
 }
 void set_last_error(const std::string& msg) { g_last_error = msg; }
 
-template <class T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  DevBuf() = default;
-  DevBuf(const DevBuf&) = delete;
-  DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-  void alloc(size_t count) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = count;
-    if (count) MMX_HIP(hipMalloc(&p, count * sizeof(T)));
-  }
-  void upload(const T* h, size_t count, hipStream_t st) {
-    alloc(count);
-    if (count) MMX_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
-  }
-};
 
 struct EngineBase {
   virtual ~EngineBase() = default;

@@ -1,0 +1,767 @@
+// sparse.cpp -- host side of the LASolver replacement (include/mmx_sparse.h): MatrixStruc
+// packing, the symbolic ILU (level of fill, natural order) and the device-resident MatrixIter
+// whose numeric factor, sweeps, SpMV and CG-STAB run as HIP kernels (kernels/sparse_kernels.hip).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/mmx_sparse.h"
+#include "../kernels/sparse_kernels.h"
+#include "common.h"
+
+namespace mmx {
+namespace {
+
+// MatrixStruc (lib/LASolver/MatrixIter.cpp:88-257): per-row column lists; pack() sorts each row
+// ascending and removes duplicates; the diagonal is present unless no_diag.
+struct Struc {
+  int n = 0;
+  bool packed = false;
+  std::vector<std::vector<int>> rows;
+  std::vector<int> ia, ja;
+
+  void pack() {
+    if (packed) throw Error(MMADMM_ERR_INVALID, "error: data structure already packed");
+    ia.assign(n + 1, 0);
+    for (int i = 0; i < n; ++i) {
+      auto& r = rows[i];
+      std::sort(r.begin(), r.end());
+      r.erase(std::unique(r.begin(), r.end()), r.end());
+      ia[i + 1] = ia[i] + (int)r.size();
+    }
+    ja.resize(ia[n]);
+    for (int i = 0; i < n; ++i) {
+      std::copy(rows[i].begin(), rows[i].end(), ja.begin() + ia[i]);
+      std::vector<int>().swap(rows[i]);
+    }
+    rows.clear();
+    packed = true;
+  }
+};
+
+// Symbolic ILU by level of fill (scaler_ILU::sfac2 + merge2, lib/LASolver/ILU_class.cpp:17-295),
+// natural ordering.  Rows must be duplicate-free and hold their diagonal (as pack() makes them).
+}  // namespace
+void symbolic_ilu(int n, const std::vector<int>& ia, const std::vector<int>& ja, int level, std::vector<int>& iaf,
+                  std::vector<int>& jaf, std::vector<int>& dgRel) {
+  const int END = n + 1, MAXINT = 2 * n;
+  std::vector<int> list(n, END), lrow(n, MAXINT), tmp;
+  std::vector<std::vector<int>> rj(n), rl(n);
+  dgRel.assign(n, -1);
+  for (int i = 0; i < n; ++i) {
+    tmp.assign(ja.begin() + ia[i], ja.begin() + ia[i + 1]);
+    if (tmp.empty()) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " is empty (no diagonal)");
+    std::sort(tmp.begin(), tmp.end());
+    for (size_t q = 1; q < tmp.size(); ++q)
+      if (tmp[q] == tmp[q - 1]) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has duplicate columns");
+    const int first = tmp[0];
+    for (size_t q = 1; q < tmp.size(); ++q) list[tmp[q - 1]] = tmp[q];
+    list[tmp.back()] = END;
+    for (int c : tmp) lrow[c] = 0;
+    // merge2
+    int next = first;
+    while (next < i) {
+      int oldlst = next, nxtlst = list[next];
+      const int row = next, levlow = lrow[oldlst];
+      const std::vector<int>& J = rj[row];
+      const std::vector<int>& Lv = rl[row];
+      for (int ii = dgRel[row] + 1; ii < (int)J.size(); ++ii) {
+        while (J[ii] > nxtlst) {
+          oldlst = nxtlst;
+          nxtlst = list[oldlst];
+        }
+        if (J[ii] < nxtlst) {
+          const int levnew = levlow + Lv[ii] + 1;
+          if (levnew <= level) {
+            list[oldlst] = J[ii];
+            list[J[ii]] = nxtlst;
+            oldlst = J[ii];
+            lrow[oldlst] = levnew;
+          }
+        } else {
+          oldlst = nxtlst;
+          const int levup = Lv[ii];
+          lrow[oldlst] = std::min(levup + levlow + 1, lrow[oldlst]);
+          nxtlst = list[oldlst];
+        }
+      }
+      next = list[next];
+    }
+    for (next = first; next != END; next = list[next]) {
+      if (next == i) dgRel[i] = (int)rj[i].size();
+      rj[i].push_back(next);
+      rl[i].push_back(lrow[next]);
+      lrow[next] = MAXINT;
+    }
+    if (dgRel[i] < 0) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has no diagonal entry");
+    if (level == 0) std::vector<int>().swap(rl[i]), rl[i].assign(rj[i].size(), 0);
+  }
+  iaf.assign(n + 1, 0);
+  for (int i = 0; i < n; ++i) iaf[i + 1] = iaf[i] + (int)rj[i].size();
+  jaf.resize(iaf[n]);
+  for (int i = 0; i < n; ++i) std::copy(rj[i].begin(), rj[i].end(), jaf.begin() + iaf[i]);
+}
+
+namespace {
+
+void check_params(const mmx_param_iter& p) {
+  if (p.order != 0) throw Error(MMADMM_ERR_INVALID, "unsupported ParamIter.order (only natural ordering, 0)");
+  if (p.drop_ilu != 0) throw Error(MMADMM_ERR_INVALID, "unsupported ParamIter.drop_ilu (only level-of-fill ILU, 0)");
+  if (p.iscal != 0) throw Error(MMADMM_ERR_INVALID, "unsupported ParamIter.iscal (only no scaling, 0)");
+  if (p.ipiv != 0) throw Error(MMADMM_ERR_INVALID, "unsupported ParamIter.ipiv (only no pivoting, 0)");
+  if (p.iaccel != 0) throw Error(MMADMM_ERR_INVALID, "unsupported ParamIter.iaccel (only CG-STAB, 0)");
+  if (p.level < 0) throw Error(MMADMM_ERR_INVALID, "ParamIter.level must be >= 0");
+}
+
+struct Timer {
+  hipEvent_t a = nullptr, b = nullptr;
+  bool armed = false;
+  void init() {
+    if (!a) {
+      MMX_HIP(hipEventCreate(&a));
+      MMX_HIP(hipEventCreate(&b));
+    }
+  }
+  ~Timer() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+  }
+};
+
+}  // namespace
+
+struct SparseMatrix {
+  int device = 0;
+  hipStream_t st = nullptr;
+  int n = 0;
+  long long nnz = 0;
+  std::vector<int> ia, ja;
+  DevBuf<int> d_ia, d_ja, d_rowblk;
+  int nblk = 0;
+  DevBuf<double> d_a, d_b, d_tol;
+  bool tolSet = false;
+  // symbolic + numeric ILU
+  bool symbolic = false;
+  int level = -1;
+  std::vector<int> iaf, jaf, dgRel;
+  DevBuf<int> d_iaf, d_jaf, d_dg, d_amap;
+  DevBuf<double> d_af;
+  DevBuf<unsigned> d_flags, d_ctl;  // ctl: 8 tickets, err, pad (16-byte multiple)
+  DevBuf<uint64_t> d_gy, d_gx;
+  unsigned epoch = 0, fepoch = 0;
+  // CG-STAB vectors
+  DevBuf<double> d_res, d_res0, d_p, d_vbar, d_avbar, d_s, d_z, d_t, d_x, d_part, d_tmp;
+  DevBuf<CgsScalars> d_sc;
+  CgsScalars* h_sc = nullptr;
+  bool timing = false;
+  mmx_sparse_stats stats{};
+  Timer tm[4];  // spmv, sweeps, factor, whole solve
+
+  SparseMatrix(int dev, int n_, const int* ia_, const int* ja_) : device(dev), n(n_) {
+    if (n <= 0) throw Error(MMADMM_ERR_INVALID, "matrix size must be positive");
+    if (ia_[0] != 0) throw Error(MMADMM_ERR_INVALID, "ia[0] must be 0");
+    for (int i = 0; i < n; ++i)
+      if (ia_[i + 1] < ia_[i]) throw Error(MMADMM_ERR_INVALID, "ia must be non-decreasing");
+    nnz = ia_[n];
+    for (long long k = 0; k < nnz; ++k)
+      if (ja_[k] < 0 || ja_[k] >= n) throw Error(MMADMM_ERR_INVALID, "column index out of range");
+    ia.assign(ia_, ia_ + n + 1);
+    ja.assign(ja_, ja_ + nnz);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw Error(MMADMM_ERR_HIP, "no HIP device available");
+    MMX_HIP(hipSetDevice(device));
+    MMX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    d_ia.upload(ia.data(), ia.size(), st);
+    d_ja.upload(ja.data(), ja.size(), st);
+    d_a.alloc(std::max<long long>(nnz, 1));
+    MMX_HIP(hipMemsetAsync(d_a.p, 0, sizeof(double) * std::max<long long>(nnz, 1), st));
+    d_b.alloc(n);
+    MMX_HIP(hipMemsetAsync(d_b.p, 0, sizeof(double) * n, st));
+    // SpMV row blocks: greedy runs of rows with <= kSpmvTile nonzeros (a longer row alone)
+    std::vector<int> rb{0};
+    int r0 = 0;
+    while (r0 < n) {
+      int r = r0 + 1;
+      while (r < n && ia[r + 1] - ia[r0] <= kSpmvTile && r - r0 < 4 * kSpmvBlock) ++r;
+      rb.push_back(r);
+      r0 = r;
+    }
+    nblk = (int)rb.size() - 1;
+    d_rowblk.upload(rb.data(), rb.size(), st);
+    for (DevBuf<double>* v : {&d_res, &d_res0, &d_p, &d_vbar, &d_avbar, &d_s, &d_z, &d_t, &d_x, &d_tmp}) v->alloc(n);
+    d_part.alloc((size_t)std::max(nblk, vec_grid(n)) * 3);
+    d_sc.alloc(1);
+    MMX_HIP(hipMemsetAsync(d_sc.p, 0, sizeof(CgsScalars), st));
+    MMX_HIP(hipHostMalloc((void**)&h_sc, sizeof(CgsScalars), hipHostMallocDefault));
+    d_ctl.alloc(16);
+    MMX_HIP(hipMemsetAsync(d_ctl.p, 0, 16 * sizeof(unsigned), st));
+    d_gy.alloc(2 * (size_t)n);
+    d_gx.alloc(2 * (size_t)n);
+    MMX_HIP(hipMemsetAsync(d_gy.p, 0, 16 * (size_t)n, st));
+    MMX_HIP(hipMemsetAsync(d_gx.p, 0, 16 * (size_t)n, st));
+    d_flags.alloc(n);
+    MMX_HIP(hipMemsetAsync(d_flags.p, 0, sizeof(unsigned) * n, st));
+    stats.spmv_bytes = 12.0 * (double)nnz + 4.0 * (n + 1) + 16.0 * n;
+    MMX_HIP(hipStreamSynchronize(st));
+  }
+  ~SparseMatrix() {
+    if (st) (void)hipStreamSynchronize(st);
+    if (h_sc) (void)hipHostFree(h_sc);
+    if (st) (void)hipStreamDestroy(st);
+  }
+
+  unsigned* tickets() { return d_ctl.p; }
+  unsigned* errw() { return d_ctl.p + 8; }
+
+  void sfac(const mmx_param_iter& p) {
+    check_params(p);
+    symbolic_ilu(n, ia, ja, p.level, iaf, jaf, dgRel);
+    level = p.level;
+    std::vector<int> dg(n), amap(nnz);
+    for (int i = 0; i < n; ++i) {
+      dg[i] = iaf[i] + dgRel[i];
+      const int* b = jaf.data() + iaf[i];
+      const int* e = jaf.data() + iaf[i + 1];
+      for (int k = ia[i]; k < ia[i + 1]; ++k) amap[k] = (int)(std::lower_bound(b, e, ja[k]) - jaf.data());
+    }
+    d_iaf.upload(iaf.data(), iaf.size(), st);
+    d_jaf.upload(jaf.data(), jaf.size(), st);
+    d_dg.upload(dg.data(), dg.size(), st);
+    d_amap.upload(amap.data(), std::max<size_t>(amap.size(), 1), st);
+    d_af.alloc(std::max<size_t>(jaf.size(), 1));
+    MMX_HIP(hipStreamSynchronize(st));
+    symbolic = true;
+  }
+
+  void begin(int t) {
+    if (!timing) return;
+    tm[t].init();
+    MMX_HIP(hipEventRecord(tm[t].a, st));
+  }
+  float end(int t) {
+    if (!timing) return 0.f;
+    MMX_HIP(hipEventRecord(tm[t].b, st));
+    MMX_HIP(hipEventSynchronize(tm[t].b));
+    float ms = 0.f;
+    MMX_HIP(hipEventElapsedTime(&ms, tm[t].a, tm[t].b));
+    return ms;
+  }
+
+  void check_err() {
+    unsigned e = 0;
+    MMX_HIP(hipMemcpyAsync(&e, errw(), sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    MMX_HIP(hipStreamSynchronize(st));
+    if (e) {
+      MMX_HIP(hipMemsetAsync(errw(), 0, sizeof(unsigned), st));
+      throw Error(MMADMM_ERR_HIP, "sync-free ILU dependency wait gave up (code " + std::to_string(e) + ")");
+    }
+  }
+
+  void factor() {
+    if (!symbolic) throw Error(MMADMM_ERR_INVALID, "error: solve called with no symbolic ILU");
+    MMX_HIP(hipMemsetAsync(tickets(), 0, 8 * sizeof(unsigned), st));
+    if (++fepoch == 0) {
+      MMX_HIP(hipMemsetAsync(d_flags.p, 0, sizeof(unsigned) * n, st));
+      fepoch = 1;
+    }
+    begin(2);
+    launch_ilu_factor(n, d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_flags.p, fepoch, tickets(),
+                      errw(), st);
+    MMX_HIP(hipGetLastError());
+    const float ms = end(2);
+    stats.factors++;
+    if (timing) {
+      stats.t_factor_ms += ms;
+      stats.n_factor_timed++;
+    }
+  }
+
+  unsigned next_epoch() {
+    if (++epoch == 0) {  // wrapped: clear every granule tag
+      MMX_HIP(hipMemsetAsync(d_gy.p, 0, 16 * (size_t)n, st));
+      MMX_HIP(hipMemsetAsync(d_gx.p, 0, 16 * (size_t)n, st));
+      epoch = 1;
+    }
+    return epoch;
+  }
+
+  // scaler_ILU::solve: out = (LU)^-1 src, or with the CG-STAB prologues (pro 1: p, pro 2: s)
+  void ilu_apply(int pro, const double* src, double* p, double* out, unsigned* tk) {
+    begin(1);
+    const unsigned ey = next_epoch();
+    launch_sweep_fwd(pro, n, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, src, p, d_res.p, d_avbar.p, d_sc.p, d_gy.p, ey, tk,
+                     errw(), st);
+    const unsigned ex = next_epoch();
+    launch_sweep_bwd(n, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_gy.p, out, d_gx.p, ex, tk + 1, errw(), st);
+    MMX_HIP(hipGetLastError());
+    const float ms = end(1);
+    stats.sweeps += 2;
+    if (timing) {
+      stats.t_sweep_ms += ms;
+      stats.n_sweep_timed += 2;
+    }
+  }
+
+  void spmv(int epi, const double* x, double* y, const double* e1) {
+    begin(0);
+    launch_spmv(epi, nblk, d_rowblk.p, d_ia.p, d_ja.p, d_a.p, x, y, e1, d_part.p, st);
+    MMX_HIP(hipGetLastError());
+    const float ms = end(0);
+    stats.spmvs++;
+    if (timing) {
+      stats.t_spmv_ms += ms;
+      stats.n_spmv_timed++;
+    }
+  }
+
+  // MatrixIter::solve (lib/LASolver/MatrixIter.cpp:635-819) with scaler_cgstab.
+  void solve(const mmx_param_iter& p, double* d_xout, int& nitr, int initial_guess) {
+    check_params(p);
+    if (!symbolic) throw Error(MMADMM_ERR_INVALID, "error: solve called with no symbolic ILU");
+    if (p.level != level) throw Error(MMADMM_ERR_INVALID, "ParamIter.level differs from the one given to sfac");
+    hipEvent_t t0 = nullptr;
+    if (timing) {
+      tm[3].init();
+      MMX_HIP(hipEventRecord(tm[3].a, st));
+    }
+    factor();
+    const int gv = vec_grid(n);
+    if (initial_guess == 0) {
+      launch_cgs_init(0, n, d_b.p, d_xout, d_res.p, d_res0.p, d_p.p, d_avbar.p, p.new_rhat == 0, d_part.p, st);
+    } else {
+      spmv(0, d_xout, d_res.p, nullptr);
+      launch_cgs_init(1, n, d_b.p, d_xout, d_res.p, d_res0.p, d_p.p, d_avbar.p, p.new_rhat == 0, d_part.p, st);
+    }
+    if (p.new_rhat != 0) {  // scaler_cgstab(n, res, ilu): res0 = (LU)^-1 res  (accel_class.h:87-94)
+      MMX_HIP(hipMemsetAsync(tickets(), 0, 8 * sizeof(unsigned), st));
+      ilu_apply(0, d_res.p, nullptr, d_res0.p, tickets());
+      launch_dot_into(n, d_res0.p, d_res.p, d_part.p, st);
+    }
+    const double ctol = p.resid_reduc;
+    MMX_HIP(hipMemcpyAsync(&d_sc.p->ctol, &ctol, sizeof(double), hipMemcpyHostToDevice, st));
+    launch_cgs_fin(0, d_part.p, gv, d_sc.p, st);
+    const double* tol = tolSet ? d_tol.p : nullptr;
+    int conv = 0, it = 0;
+    for (int iter = 1; iter <= p.nitmax; ++iter) {
+      ++it;
+      MMX_HIP(hipMemsetAsync(tickets(), 0, 8 * sizeof(unsigned), st));
+      ilu_apply(1, nullptr, d_p.p, d_vbar.p, tickets());          // p update; vbar = (LU)^-1 p
+      spmv(1, d_vbar.p, d_avbar.p, d_res0.p);                      // avbar = A vbar; (res0, avbar)
+      launch_cgs_fin(1, d_part.p, nblk, d_sc.p, st);               // alpha
+      ilu_apply(2, nullptr, d_s.p, d_z.p, tickets() + 2);          // s = res - alpha avbar; z = (LU)^-1 s
+      spmv(2, d_z.p, d_t.p, d_s.p);                                // t = A z; (t, s), (t, t)
+      launch_cgs_fin(2, d_part.p, nblk, d_sc.p, st);               // omega
+      launch_cgs_update(n, d_vbar.p, d_z.p, d_s.p, d_t.p, d_res0.p, tol, d_xout, d_res.p, d_sc.p, d_part.p, st);
+      launch_cgs_fin(3, d_part.p, gv, d_sc.p, st);
+      MMX_HIP(hipGetLastError());
+      MMX_HIP(hipMemcpyAsync(h_sc, d_sc.p, sizeof(CgsScalars), hipMemcpyDeviceToHost, st));
+      MMX_HIP(hipStreamSynchronize(st));
+      stats.iterations++;
+      if (h_sc->conv) {
+        conv = 1;
+        break;
+      }
+    }
+    if (p.nitmax <= 0) {  // the reference's loop body never runs; report non-convergence
+      MMX_HIP(hipMemcpyAsync(h_sc, d_sc.p, sizeof(CgsScalars), hipMemcpyDeviceToHost, st));
+      MMX_HIP(hipStreamSynchronize(st));
+    }
+    check_err();
+    nitr = conv ? it : -1;
+    stats.solves++;
+    stats.last_rms = h_sc->rms;
+    stats.rmsi = h_sc->rmsi;
+    if (timing) {
+      MMX_HIP(hipEventRecord(tm[3].b, st));
+      MMX_HIP(hipEventSynchronize(tm[3].b));
+      float ms = 0.f;
+      MMX_HIP(hipEventElapsedTime(&ms, tm[3].a, tm[3].b));
+      stats.t_solve_ms += ms;
+    }
+    (void)t0;
+  }
+};
+
+struct StrucHandle {
+  Struc s;
+};
+
+}  // namespace mmx
+
+struct mmx_struc_s {
+  mmx::Struc s;
+};
+struct mmx_matrix_s {
+  mmx::SparseMatrix* m;
+};
+
+using mmx::Error;
+using mmx::guarded;
+
+extern "C" {
+
+void mmx_param_iter_default(mmx_param_iter* p) {  // ParamIter() (MatrixIter.h:155-168)
+  if (!p) return;
+  p->order = 1;
+  p->level = 1;
+  p->drop_ilu = 0;
+  p->iscal = 1;
+  p->nitmax = 30;
+  p->resid_reduc = 1.e-6;
+  p->drop_tol = 1.e-3;
+  p->info = 1;
+  p->new_rhat = 0;
+  p->iaccel = 0;
+  p->north = 10;
+  p->ipiv = 0;
+}
+
+void mmx_param_iter_mesh(mmx_param_iter* p) {  // src/Mesh.cpp:264-304
+  if (!p) return;
+  mmx_param_iter_default(p);
+  p->order = 0;
+  p->level = 0;
+  p->drop_ilu = 0;
+  p->iscal = 0;
+  p->nitmax = 10000;
+  p->ipiv = 0;
+  p->resid_reduc = 1.e-6;
+  p->info = 0;
+  p->drop_tol = 1.e-3;
+  p->new_rhat = 0;
+  p->iaccel = 0;
+  p->north = 10;
+}
+
+int mmx_struc_create(int n, int no_diag, mmx_struc* out) {
+  return guarded([&] {
+    if (!out || n <= 0) throw Error(MMADMM_ERR_INVALID, "mmx_struc_create: bad arguments");
+    auto* h = new mmx_struc_s;
+    h->s.n = n;
+    h->s.rows.resize(n);
+    if (no_diag == 0)
+      for (int i = 0; i < n; ++i) h->s.rows[i].push_back(i);
+    *out = h;
+  });
+}
+
+int mmx_struc_set_entry(mmx_struc s, int row, int col) {
+  return guarded([&] {
+    if (!s) throw Error(MMADMM_ERR_INVALID, "null structure");
+    if (s->s.packed) throw Error(MMADMM_ERR_INVALID, "error: data structure already compressed");
+    if (row < 0 || row >= s->s.n) throw Error(MMADMM_ERR_INVALID, "invalid row entry in set_entry");
+    if (col < 0 || col >= s->s.n) throw Error(MMADMM_ERR_INVALID, "invalid column entry in set_entry");
+    s->s.rows[row].push_back(col);
+  });
+}
+
+int mmx_struc_set_entries(mmx_struc s, long long count, const int32_t* rows, const int32_t* cols) {
+  return guarded([&] {
+    if (!s || (count > 0 && (!rows || !cols))) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    if (s->s.packed) throw Error(MMADMM_ERR_INVALID, "error: data structure already compressed");
+    for (long long e = 0; e < count; ++e) {
+      if (rows[e] < 0 || rows[e] >= s->s.n) throw Error(MMADMM_ERR_INVALID, "invalid row entry in set_entry");
+      if (cols[e] < 0 || cols[e] >= s->s.n) throw Error(MMADMM_ERR_INVALID, "invalid column entry in set_entry");
+      s->s.rows[rows[e]].push_back(cols[e]);
+    }
+  });
+}
+
+int mmx_struc_mesh_pattern(mmx_struc s, int dim, int nF, const int32_t* F) {
+  return guarded([&] {
+    if (!s || (dim != 2 && dim != 3) || nF < 0 || (nF > 0 && !F)) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    if (s->s.packed) throw Error(MMADMM_ERR_INVALID, "error: data structure already compressed");
+    const int D = dim, nP = s->s.n / D;
+    if (nP * D != s->s.n) throw Error(MMADMM_ERR_INVALID, "structure size is not dim * nodes");
+    // node adjacency first (every vertex pair of every simplex), then D x D blocks
+    std::vector<std::vector<int>> nb(nP);
+    for (int t = 0; t < nF; ++t)
+      for (int a = 0; a <= D; ++a) {
+        const int va = F[(size_t)t * (D + 1) + a];
+        if (va < 0 || va >= nP) throw Error(MMADMM_ERR_INVALID, "simplex vertex out of range");
+        for (int b = 0; b <= D; ++b) nb[va].push_back(F[(size_t)t * (D + 1) + b]);
+      }
+    for (int v = 0; v < nP; ++v) {
+      auto& l = nb[v];
+      std::sort(l.begin(), l.end());
+      l.erase(std::unique(l.begin(), l.end()), l.end());
+      for (int d = 0; d < D; ++d) {
+        auto& r = s->s.rows[v * D + d];
+        for (int u : l)
+          for (int e = 0; e < D; ++e) r.push_back(u * D + e);
+      }
+      std::vector<int>().swap(l);
+    }
+  });
+}
+
+int mmx_struc_pack(mmx_struc s) {
+  return guarded([&] {
+    if (!s) throw Error(MMADMM_ERR_INVALID, "null structure");
+    s->s.pack();
+  });
+}
+
+int mmx_struc_get(mmx_struc s, int* n, long long* nnz, int32_t* ia, int32_t* ja) {
+  return guarded([&] {
+    if (!s) throw Error(MMADMM_ERR_INVALID, "null structure");
+    if (!s->s.packed) s->s.pack();  // getia/getja pack on demand (MatrixIter.cpp:146-148)
+    if (n) *n = s->s.n;
+    if (nnz) *nnz = s->s.ia[s->s.n];
+    if (ia) std::memcpy(ia, s->s.ia.data(), sizeof(int) * (s->s.n + 1));
+    if (ja) std::memcpy(ja, s->s.ja.data(), sizeof(int) * s->s.ja.size());
+  });
+}
+
+int mmx_struc_destroy(mmx_struc s) {
+  delete s;
+  return MMADMM_OK;
+}
+
+int mmx_matrix_create(int device, int n, const int32_t* ia, const int32_t* ja, mmx_matrix* out) {
+  return guarded([&] {
+    if (!out || !ia || (n > 0 && !ja && ia[n] > 0)) throw Error(MMADMM_ERR_INVALID, "mmx_matrix_create: bad arguments");
+    *out = nullptr;
+    auto* h = new mmx_matrix_s;
+    try {
+      h->m = new mmx::SparseMatrix(device, n, ia, ja);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int mmx_matrix_create_from_struc(int device, mmx_struc s, mmx_matrix* out) {
+  return guarded([&] {
+    if (!s || !out) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    if (!s->s.packed) s->s.pack();
+    *out = nullptr;
+    auto* h = new mmx_matrix_s;
+    try {
+      h->m = new mmx::SparseMatrix(device, s->s.n, s->s.ia.data(), s->s.ja.data());
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+#define MMX_M(m)                                                    \
+  if (!(m) || !(m)->m) throw Error(MMADMM_ERR_INVALID, "null matrix"); \
+  mmx::SparseMatrix& M = *(m)->m;                                   \
+  MMX_HIP(hipSetDevice(M.device))
+
+int mmx_matrix_sizes(mmx_matrix m, int* n, long long* nnz) {
+  return guarded([&] {
+    MMX_M(m);
+    if (n) *n = M.n;
+    if (nnz) *nnz = M.nnz;
+  });
+}
+
+int mmx_matrix_stream(mmx_matrix m, void** s) {
+  return guarded([&] {
+    MMX_M(m);
+    if (s) *s = (void*)M.st;
+  });
+}
+
+int mmx_matrix_set_values(mmx_matrix m, const double* a) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!a && M.nnz) throw Error(MMADMM_ERR_INVALID, "null values");
+    MMX_HIP(hipMemcpyAsync(M.d_a.p, a, sizeof(double) * M.nnz, hipMemcpyHostToDevice, M.st));
+    MMX_HIP(hipStreamSynchronize(M.st));
+  });
+}
+
+int mmx_matrix_set_values_device(mmx_matrix m, const double* d_a) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!d_a && M.nnz) throw Error(MMADMM_ERR_INVALID, "null values");
+    MMX_HIP(hipMemcpyAsync(M.d_a.p, d_a, sizeof(double) * M.nnz, hipMemcpyDeviceToDevice, M.st));
+  });
+}
+
+int mmx_matrix_set_rhs(mmx_matrix m, const double* b) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!b) throw Error(MMADMM_ERR_INVALID, "null rhs");
+    MMX_HIP(hipMemcpyAsync(M.d_b.p, b, sizeof(double) * M.n, hipMemcpyHostToDevice, M.st));
+    MMX_HIP(hipStreamSynchronize(M.st));
+  });
+}
+
+int mmx_matrix_set_rhs_device(mmx_matrix m, const double* d_b) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!d_b) throw Error(MMADMM_ERR_INVALID, "null rhs");
+    MMX_HIP(hipMemcpyAsync(M.d_b.p, d_b, sizeof(double) * M.n, hipMemcpyDeviceToDevice, M.st));
+  });
+}
+
+int mmx_matrix_set_toler(mmx_matrix m, const double* tol) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!tol) throw Error(MMADMM_ERR_INVALID, "null tolerance vector");
+    bool allZero = true;
+    for (int i = 0; i < M.n; ++i) allZero &= (tol[i] == 0.0);
+    if (allZero) {  // the reference's default (MatrixIter.cpp:394-398) and src/Mesh.cpp's setting
+      M.tolSet = false;
+      return;
+    }
+    M.d_tol.upload(tol, M.n, M.st);
+    MMX_HIP(hipStreamSynchronize(M.st));
+    M.tolSet = true;
+  });
+}
+
+int mmx_matrix_sfac(mmx_matrix m, const mmx_param_iter* p) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!p) throw Error(MMADMM_ERR_INVALID, "null parameters");
+    M.sfac(*p);
+  });
+}
+
+int mmx_matrix_solve_device(mmx_matrix m, const mmx_param_iter* p, double* d_x, int* nitr, int initial_guess) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!p || !d_x || !nitr) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    M.solve(*p, d_x, *nitr, initial_guess);
+  });
+}
+
+int mmx_matrix_solve(mmx_matrix m, const mmx_param_iter* p, double* x, int* nitr, int initial_guess) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!p || !x || !nitr) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    if (initial_guess) MMX_HIP(hipMemcpyAsync(M.d_x.p, x, sizeof(double) * M.n, hipMemcpyHostToDevice, M.st));
+    M.solve(*p, M.d_x.p, *nitr, initial_guess);
+    MMX_HIP(hipMemcpyAsync(x, M.d_x.p, sizeof(double) * M.n, hipMemcpyDeviceToHost, M.st));
+    MMX_HIP(hipStreamSynchronize(M.st));
+  });
+}
+
+int mmx_matrix_matmult_device(mmx_matrix m, const double* d_x, double* d_y) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!d_x || !d_y) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    M.spmv(0, d_x, d_y, nullptr);
+  });
+}
+
+int mmx_matrix_matmult(mmx_matrix m, const double* x, double* y) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!x || !y) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    MMX_HIP(hipMemcpyAsync(M.d_tmp.p, x, sizeof(double) * M.n, hipMemcpyHostToDevice, M.st));
+    M.spmv(0, M.d_tmp.p, M.d_t.p, nullptr);
+    MMX_HIP(hipMemcpyAsync(y, M.d_t.p, sizeof(double) * M.n, hipMemcpyDeviceToHost, M.st));
+    MMX_HIP(hipStreamSynchronize(M.st));
+  });
+}
+
+int mmx_matrix_factor(mmx_matrix m) {
+  return guarded([&] {
+    MMX_M(m);
+    M.factor();
+    M.check_err();
+  });
+}
+
+int mmx_matrix_ilu_solve_device(mmx_matrix m, const double* d_b, double* d_x) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!d_b || !d_x) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    if (!M.symbolic || M.fepoch == 0) throw Error(MMADMM_ERR_INVALID, "error: solve called with no factor");
+    MMX_HIP(hipMemsetAsync(M.tickets(), 0, 8 * sizeof(unsigned), M.st));
+    M.ilu_apply(0, d_b, nullptr, d_x, M.tickets());
+  });
+}
+
+int mmx_matrix_ilu_solve(mmx_matrix m, const double* b, double* x) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!b || !x) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    if (!M.symbolic || M.fepoch == 0) throw Error(MMADMM_ERR_INVALID, "error: solve called with no factor");
+    MMX_HIP(hipMemcpyAsync(M.d_tmp.p, b, sizeof(double) * M.n, hipMemcpyHostToDevice, M.st));
+    MMX_HIP(hipMemsetAsync(M.tickets(), 0, 8 * sizeof(unsigned), M.st));
+    M.ilu_apply(0, M.d_tmp.p, nullptr, M.d_t.p, M.tickets());
+    MMX_HIP(hipMemcpyAsync(x, M.d_t.p, sizeof(double) * M.n, hipMemcpyDeviceToHost, M.st));
+    MMX_HIP(hipStreamSynchronize(M.st));
+    M.check_err();
+  });
+}
+
+int mmx_matrix_factor_nnz(mmx_matrix m, long long* nnzf) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!M.symbolic) throw Error(MMADMM_ERR_INVALID, "no symbolic factor (call mmx_matrix_sfac)");
+    if (nnzf) *nnzf = (long long)M.jaf.size();
+  });
+}
+
+int mmx_matrix_get_factor(mmx_matrix m, int32_t* iaf, int32_t* jaf, double* af, int32_t* diag) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!M.symbolic) throw Error(MMADMM_ERR_INVALID, "no symbolic factor (call mmx_matrix_sfac)");
+    if (iaf) std::memcpy(iaf, M.iaf.data(), sizeof(int) * (M.n + 1));
+    if (jaf) std::memcpy(jaf, M.jaf.data(), sizeof(int) * M.jaf.size());
+    if (diag) std::memcpy(diag, M.dgRel.data(), sizeof(int) * M.n);
+    if (af) {
+      MMX_HIP(hipMemcpyAsync(af, M.d_af.p, sizeof(double) * M.jaf.size(), hipMemcpyDeviceToHost, M.st));
+      MMX_HIP(hipStreamSynchronize(M.st));
+    }
+  });
+}
+
+int mmx_matrix_set_timing(mmx_matrix m, int on) {
+  return guarded([&] {
+    MMX_M(m);
+    M.timing = on != 0;
+  });
+}
+
+int mmx_matrix_stats_get(mmx_matrix m, mmx_sparse_stats* out) {
+  return guarded([&] {
+    MMX_M(m);
+    if (out) *out = M.stats;
+  });
+}
+
+int mmx_matrix_stats_reset(mmx_matrix m) {
+  return guarded([&] {
+    MMX_M(m);
+    const double bytes = M.stats.spmv_bytes;
+    M.stats = mmx_sparse_stats{};
+    M.stats.spmv_bytes = bytes;
+  });
+}
+
+int mmx_ilu_symbolic(int n, const int32_t* ia, const int32_t* ja, int level, long long* nnzf, int32_t* iaf,
+                     int32_t* jaf, int32_t* diag) {
+  return guarded([&] {
+    if (n <= 0 || !ia || !ja || level < 0) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    std::vector<int> via(ia, ia + n + 1), vja(ja, ja + ia[n]), fia, fja, dg;
+    mmx::symbolic_ilu(n, via, vja, level, fia, fja, dg);
+    if (nnzf) *nnzf = (long long)fja.size();
+    if (iaf) std::memcpy(iaf, fia.data(), sizeof(int) * (n + 1));
+    if (jaf) std::memcpy(jaf, fja.data(), sizeof(int) * fja.size());
+    if (diag) std::memcpy(diag, dg.data(), sizeof(int) * n);
+  });
+}
+
+int mmx_matrix_destroy(mmx_matrix m) {
+  if (!m) return MMADMM_OK;
+  delete m->m;
+  delete m;
+  return MMADMM_OK;
+}
+
+}  // extern "C"

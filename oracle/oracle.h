@@ -68,7 +68,7 @@ int orc_la_ilu0(int n, const int* ia, const int* ja, const double* a, double* af
 int orc_la_ilu_solve(int n, const int* ia, const int* ja, const double* af, const double* b, double* x);
 int orc_la_solve(int n, const int* ia, const int* ja, const double* a, const double* b, const double* toler,
                  int nitmax, double resid_reduc, int new_rhat, int initial_guess, double* x, int* nitr,
-                 double* rms_hist);
+                 double* rms_hist, int dotMode);
 
 #ifdef __cplusplus
 }

@@ -75,9 +75,29 @@ def make(name, pat, vseed, shift, bseed, rr, nitmax, new_rhat, x0seed):
     return n, len(ja), it
 
 
+def make_levels():
+    """Level-of-fill ILU(k) factors (sfac2 + factor) at levels 1 and 2 on a 2D n=6 and a 3D n=2
+    Jacobian pattern: pins the symbolic restatement and the numeric factor with fill-in."""
+    out = {}
+    for tag, (dim, n) in (("d2", (2, 6)), ("d3", (3, 2))):
+        ia, ja = jac_pattern(dim, n)
+        a = L.random_values(ia, ja, 21, 0.4)
+        b = np.random.default_rng(22).uniform(-1.0, 1.0, len(ia) - 1)
+        out[f"{tag}_ia"], out[f"{tag}_ja"], out[f"{tag}_a"], out[f"{tag}_b"] = ia, ja, a, b
+        for lev in (1, 2):
+            iaf, jaf, af, diag = L.ref_ilu(ia, ja, a, level=lev)
+            out[f"{tag}_l{lev}_iaf"], out[f"{tag}_l{lev}_jaf"] = iaf, jaf
+            out[f"{tag}_l{lev}_af"], out[f"{tag}_l{lev}_diag"] = af, diag
+            x, it, _ = L.solve_ref_level(ia, ja, a, b, lev)
+            out[f"{tag}_l{lev}_x"], out[f"{tag}_l{lev}_nitr"] = x, np.int32(it)
+    np.savez_compressed(os.path.join(OUT, "ilu_levels.npz"), **out)
+
+
 if __name__ == "__main__":
     assert L.ref_available(), "build oracle/_ref first: make -f oracle/Makefile.ref -C oracle"
     os.makedirs(OUT, exist_ok=True)
     for c in CASES:
         n, nnz, it = make(*c)
         print(f"{c[0]}: n={n} nnz={nnz} nitr={it}")
+    make_levels()
+    print("ilu_levels")

@@ -37,7 +37,7 @@ def orc():
         _orc.orc_la_matmult.argtypes = [_i, _ip, _ip, _dp, _dp, _dp]
         _orc.orc_la_ilu0.argtypes = [_i, _ip, _ip, _dp, _dp]
         _orc.orc_la_ilu_solve.argtypes = [_i, _ip, _ip, _dp, _dp, _dp]
-        _orc.orc_la_solve.argtypes = [_i, _ip, _ip, _dp, _dp, _dp, _i, _d, _i, _i, _dp, _ip, _dp]
+        _orc.orc_la_solve.argtypes = [_i, _ip, _ip, _dp, _dp, _dp, _i, _d, _i, _i, _dp, _ip, _dp, _i]
     return _orc
 
 
@@ -151,8 +151,9 @@ def ilu_solve(ia, ja, af, b):
     return x
 
 
-def solve(ia, ja, a, b, nitmax=10000, resid_reduc=1e-6, new_rhat=0, x0=None, toler=None, use_ref=False):
-    """MatrixIter::solve with the src/Mesh.cpp parameters -> (x, nitr, rms history)."""
+def solve(ia, ja, a, b, nitmax=10000, resid_reduc=1e-6, new_rhat=0, x0=None, toler=None, use_ref=False, tree=False):
+    """MatrixIter::solve with the src/Mesh.cpp parameters -> (x, nitr, rms history).
+    tree=True: dot products in the GPU's fixed reduction order instead of sequential sums."""
     n = len(ia) - 1
     ia, ja, a, b = _i32(ia), _i32(ja), _f64(a), _f64(b)
     tol = _f64(toler) if toler is not None else None
@@ -167,10 +168,21 @@ def solve(ia, ja, a, b, nitmax=10000, resid_reduc=1e-6, new_rhat=0, x0=None, tol
     hist = np.zeros(max(nitmax, 1))
     rc = orc().orc_la_solve(n, _ptr(ia, _ip), _ptr(ja, _ip), _ptr(a, _dp), _ptr(b, _dp), _ptr(tol, _dp),
                             nitmax, resid_reduc, new_rhat, 1 if x0 is not None else 0, _ptr(x, _dp),
-                            ctypes.byref(nitr), _ptr(hist, _dp))
+                            ctypes.byref(nitr), _ptr(hist, _dp), 1 if tree else 0)
     assert rc == 0
     k = nitr.value if nitr.value > 0 else nitmax
     return x, nitr.value, hist[:k]
+
+
+def solve_ref_level(ia, ja, a, b, level, nitmax=10000, resid_reduc=1e-6):
+    """The reference's MatrixIter::solve with ILU(level)."""
+    n = len(ia) - 1
+    ia, ja, a, b = _i32(ia), _i32(ja), _f64(a), _f64(b)
+    x = np.zeros(n)
+    nitr = ctypes.c_int(0)
+    assert ref().lsr_solve(n, _ptr(ia, _ip), _ptr(ja, _ip), _ptr(a, _dp), _ptr(b, _dp), None, 0, level, 0, 0,
+                           nitmax, resid_reduc, 0, 0, _ptr(x, _dp), ctypes.byref(nitr)) == 0
+    return x, nitr.value, None
 
 
 def random_values(ia, ja, seed, shift=None, dtau=None):

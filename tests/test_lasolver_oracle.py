@@ -10,7 +10,8 @@ import pytest
 import lasolver_py as L
 import oracle_py
 
-GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "lasolver", "*.npz")))
+GOLD = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "lasolver", "*.npz"))
+              if not p.endswith("ilu_levels.npz"))
 
 
 def _same(x, y):
@@ -76,3 +77,25 @@ def test_restatement_matches_reference_live(seed):
     assert nr == no and _same(xr, xo)
     _, _, afr, _ = L.ref_ilu(ia, ja, a)
     assert _same(afr, L.ilu0(ia, ja, a))
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p)[:-4] for p in GOLD])
+def test_gpu_reduction_order_vs_reference(path):
+    """dotMode 1 (the GPU's tree-shaped dot products) against the reference's sequential sums:
+    the rounding-level bounds tests/test_gpu_lasolver.py relies on."""
+    g = np.load(path)
+    ia, ja, a, b = g["ia"], g["ja"], g["a"], g["b"]
+    x0 = g["x0"] if "x0" in g.files else None
+    rr, nitmax, rhat = float(g["resid_reduc"]), int(g["nitmax"]), int(g["new_rhat"])
+    name = os.path.basename(path)
+    x, it, _ = L.solve(ia, ja, a, b, nitmax=nitmax, resid_reduc=rr, new_rhat=rhat, x0=x0, tree=True)
+    gx, gi = g["x"], int(g["nitr"])
+    rel = np.linalg.norm(x - gx) / np.linalg.norm(gx)
+    if "zero_rhs" in name:
+        assert it == gi == 1 and np.all(np.isnan(x))
+    elif "noconv" in name:
+        assert it == gi == -1
+    elif "hard" in name:
+        assert abs(it - gi) <= 0.05 * gi and rel <= 1e-5
+    else:
+        assert it == gi and rel <= 1e-14
