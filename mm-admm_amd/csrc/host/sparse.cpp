@@ -146,7 +146,8 @@ struct SparseMatrix {
   bool symbolic = false;
   int level = -1;
   std::vector<int> iaf, jaf, dgRel;
-  DevBuf<int> d_iaf, d_jaf, d_dg, d_amap;
+  DevBuf<int> d_iaf, d_jaf, d_dg, d_amap, d_permf, d_permb;
+  int nchf = 0, nchb = 0, nlevf = 0, nlevb = 0;
   DevBuf<double> d_af;
   DevBuf<unsigned> d_flags, d_ctl;  // ctl: 8 tickets, err, pad (16-byte multiple)
   DevBuf<uint64_t> d_gy, d_gx;
@@ -231,6 +232,34 @@ struct SparseMatrix {
     d_dg.upload(dg.data(), dg.size(), st);
     d_amap.upload(amap.data(), std::max<size_t>(amap.size(), 1), st);
     d_af.alloc(std::max<size_t>(jaf.size(), 1));
+    // level schedules of the lower (forward sweep, factor) and upper (backward sweep) factor
+    std::vector<int> lev(n);
+    auto schedule = [&](bool fwd, DevBuf<int>& out, int& nch, int& nlev) {
+      int maxl = 0;
+      for (int t = 0; t < n; ++t) {
+        const int i = fwd ? t : n - 1 - t;
+        int l = 0;
+        const int kb = fwd ? iaf[i] : dg[i] + 1, ke = fwd ? dg[i] : iaf[i + 1];
+        for (int k = kb; k < ke; ++k) l = std::max(l, lev[jaf[k]] + 1);
+        lev[i] = l;
+        maxl = std::max(maxl, l);
+      }
+      nlev = maxl + 1;
+      std::vector<int> cnt(nlev + 1, 0);
+      for (int i = 0; i < n; ++i) cnt[lev[i] + 1]++;
+      std::vector<int> start(nlev + 1, 0);  // padded chunk offsets
+      for (int l = 0; l < nlev; ++l) start[l + 1] = start[l] + (cnt[l + 1] + kSweepRows - 1) / kSweepRows * kSweepRows;
+      std::vector<int> perm(start[nlev], -1), fill(start.begin(), start.end() - 1);
+      for (int t = 0; t < n; ++t) {
+        const int i = fwd ? t : n - 1 - t;
+        perm[fill[lev[i]]++] = i;
+      }
+      nch = start[nlev] / kSweepRows;
+      out.upload(perm.data(), perm.size(), st);
+    };
+    schedule(true, d_permf, nchf, nlevf);
+    schedule(false, d_permb, nchb, nlevb);
+    MMX_HIP(hipStreamSynchronize(st));
     MMX_HIP(hipStreamSynchronize(st));
     symbolic = true;
   }
@@ -267,8 +296,8 @@ struct SparseMatrix {
       fepoch = 1;
     }
     begin(2);
-    launch_ilu_factor(n, d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_flags.p, fepoch, tickets(),
-                      errw(), st);
+    launch_ilu_factor(d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_permf.p, nchf, d_af.p, d_flags.p,
+                      fepoch, tickets(), errw(), st);
     MMX_HIP(hipGetLastError());
     const float ms = end(2);
     stats.factors++;
@@ -291,10 +320,11 @@ struct SparseMatrix {
   void ilu_apply(int pro, const double* src, double* p, double* out, unsigned* tk) {
     begin(1);
     const unsigned ey = next_epoch();
-    launch_sweep_fwd(pro, n, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, src, p, d_res.p, d_avbar.p, d_sc.p, d_gy.p, ey, tk,
-                     errw(), st);
+    launch_sweep(true, pro, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permf.p, nchf, src, p, d_res.p, d_avbar.p, d_sc.p,
+                 nullptr, d_gy.p, nullptr, ey, tk, errw(), st);
     const unsigned ex = next_epoch();
-    launch_sweep_bwd(n, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_gy.p, out, d_gx.p, ex, tk + 1, errw(), st);
+    launch_sweep(false, 0, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permb.p, nchb, nullptr, nullptr, nullptr, nullptr, nullptr,
+                 d_gy.p, d_gx.p, out, ex, tk + 1, errw(), st);
     MMX_HIP(hipGetLastError());
     const float ms = end(1);
     stats.sweeps += 2;

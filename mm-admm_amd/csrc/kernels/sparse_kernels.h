@@ -10,8 +10,10 @@ namespace mmx {
 // Products staged in LDS per SpMV workgroup (16 KB of fp64).
 constexpr int kSpmvTile = 2048;
 constexpr int kSpmvBlock = 256;
-// Rows per sync-free sweep/factor workgroup (one wavefront).
+// Rows per chunk of the level-scheduled factor/sweeps (one wavefront per chunk) and the size of
+// their persistent grid (wavefronts).
 constexpr int kSweepRows = 64;
+constexpr int kSweepGrid = 128;  // measured: 2048 waves of pollers slow the chain 3.7x (profiles/r01/lasolver_tune.txt)
 // Grid of the vector kernels (fixed for a given n, so their partial sums are deterministic).
 constexpr int kVecBlock = 256;
 int vec_grid(int n);
@@ -34,19 +36,19 @@ struct SweepCtl {
 void launch_spmv(int epi, int nblk, const int* rowblk, const int* ia, const int* ja, const double* a,
                  const double* x, double* y, const double* e1, double* partials, hipStream_t st);
 
-// ILU(0) numeric factor in the factor pattern (iaf/jaf/dg); amap maps A's entries into it.
-void launch_ilu_factor(int n, const int* ia, const int* ja, const double* a, const int* amap, const int* iaf,
-                       const int* jaf, const int* dg, double* af, unsigned* flags, unsigned epoch,
+// ILU numeric factor in the factor pattern (iaf/jaf/dg); amap maps A's entries into it.  perm: rows
+// in forward-level order, padded with -1 to whole chunks of kSweepRows.
+void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
+                       const int* dg, const int* perm, int nchunks, double* af, unsigned* flags, unsigned epoch,
                        unsigned* ticket, unsigned* err, hipStream_t st);
 
-// Forward sweep (unit L) into granules gy.  pro 0: b = src; 1: p = res + beta (p - omega avbar),
-// b = p (stored to p); 2: s = res - alpha avbar, b = s (stored to p).
-void launch_sweep_fwd(int pro, int n, const int* iaf, const int* jaf, const int* dg, const double* af,
-                      const double* src, double* p, const double* res, const double* avbar, const CgsScalars* sc,
-                      uint64_t* gy, unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
-// Backward sweep (U with its diagonal) from granules gy (epoch_y) into out and granules gx.
-void launch_sweep_bwd(int n, const int* iaf, const int* jaf, const int* dg, const double* af, const uint64_t* gy,
-                      double* out, uint64_t* gx, unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
+// Sweep over the rows of perm (forward or backward level order).  Forward: unit L into granules
+// gout, right-hand side per pro (0: src; 1: p = res + beta (p - omega avbar); 2: s = res - alpha
+// avbar, stored to p).  Backward: U from the forward granules gin into out and granules gout.
+void launch_sweep(bool fwd, int pro, const int* iaf, const int* jaf, const int* dg, const double* af, const int* perm,
+                  int nchunks, const double* src, double* p, const double* res, const double* avbar, const CgsScalars* sc,
+                  const uint64_t* gin, uint64_t* gout, double* out, unsigned epoch, unsigned* ticket, unsigned* err,
+                  hipStream_t st);
 
 // init: x = 0, res = b (mode 0) or res = b - res (mode 1, res holding A x); res0 = res; p = 0;
 // avbar = 0.  Partials [sum res^2, sum res0.res] per block.

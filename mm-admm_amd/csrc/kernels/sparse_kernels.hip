@@ -16,6 +16,8 @@
 // wavefront are forwarded through LDS.  Every wait is bounded and reports through *err.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "sparse_kernels.h"
 
 namespace mmx {
@@ -23,6 +25,8 @@ namespace mmx {
 namespace {
 
 constexpr unsigned kSpinMax = 1u << 24;  // idle rounds before a dependency wait gives up
+constexpr int kBatch = 4;               // granule loads in flight per lane in a sweep
+constexpr int kFactorBatch = 8;         // pivot-row entries loaded at once in the factor
 
 __device__ __forceinline__ void store_granule(uint64_t* g, unsigned epoch, double v) {
   const uint64_t bits = (uint64_t)__double_as_longlong(v);
@@ -85,6 +89,15 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[NV]) {
 }
 
 }  // namespace
+
+int sweep_grid() {  // persistent wavefronts of the factor/sweeps (MMX_SWEEP_GRID overrides)
+  static int g = [] {
+    const char* e = getenv("MMX_SWEEP_GRID");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : kSweepGrid;
+  }();
+  return g;
+}
 
 int vec_grid(int n) {
   const int g = (n + kVecBlock - 1) / kVecBlock;
@@ -151,191 +164,187 @@ __global__ void __launch_bounds__(kSpmvBlock) k_spmv(const int* __restrict__ row
 }
 
 // ---------------------------------------------------------------------------------------------
-// ILU(0) numeric factor (scaler_ILU::factor, ILU_class.cpp:300-444), one row per lane.  The row's
-// entries are zeroed, A's values loaded, then for every lower entry id in ascending order
-// mult = row[id] / U(id,id) and row[idd] -= mult * U(id, idd) for the entries idd of row id's
-// upper part that row i holds (two sorted lists merged).  Rows publish through agent-scope
-// stores + a drained flag; readers use agent-scope loads only.
-__global__ void __launch_bounds__(kSweepRows) k_ilu_factor(int n, const int* __restrict__ ia, const int* __restrict__ ja,
+// Level-scheduled sync-free factor and sweeps.  At sfac the host assigns every row its level in
+// the dependency DAG of the lower (forward) or upper (backward) factor and lists the rows level by
+// level, each level padded to whole chunks of 64 (padding = -1), so the 64 rows of a chunk never
+// depend on each other.  A persistent grid of wavefronts takes chunks in list order from a ticket
+// counter: every dependency of a chunk lies in a chunk handed out earlier, to a wavefront that is
+// running, so waiting is deadlock-free.  Each lane computes one row; a row publishes its value as
+// two self-validating 8-byte {epoch, half} granules (sweeps) or as agent-scope stores drained
+// before an epoch flag (factor); waits re-poll with up to kBatch loads in flight, bounded.
+__device__ __forceinline__ void backoff(unsigned& spins, bool progressed, unsigned* err, unsigned code, bool& give_up) {
+  if (progressed) {
+    spins = 0;
+    return;
+  }
+  if (++spins > kSpinMax) {
+    atomicOr(err, code);
+    give_up = true;
+    return;
+  }
+  __builtin_amdgcn_s_sleep(2);
+}
+
+// ILU numeric factor (scaler_ILU::factor, ILU_class.cpp:300-444).  Row i is zeroed, A's values
+// loaded (amap, in storage order: a duplicate's last value wins, as the reference's row[] scatter
+// does), then for every lower entry id in ascending order mult = row[id] / U(id,id) and
+// row[idd] -= mult * U(id,idd) for the entries idd of row id's upper part that row i holds (two
+// sorted lists merged).  The lane works on its own row with plain accesses and publishes it
+// with agent-scope stores before the flag.
+__global__ void __launch_bounds__(kSweepRows) k_ilu_factor(const int* __restrict__ ia, const int* __restrict__ ja,
                                                           const double* __restrict__ a, const int* __restrict__ amap,
                                                           const int* __restrict__ iaf, const int* __restrict__ jaf,
-                                                          const int* __restrict__ dg, double* af, unsigned* flags,
-                                                          unsigned epoch, unsigned* ticket, unsigned* err) {
-  const int blk = take_ticket(ticket);
-  const int i = blk * kSweepRows + (int)threadIdx.x;
-  const bool valid = i < n;
-  int kk = 0, kd = 0, ke = 0;
-  if (valid) {
-    kk = iaf[i];
-    kd = dg[i];
-    ke = iaf[i + 1];
-    for (int k = kk; k < ke; ++k) st_agent(&af[k], 0.0);
-    for (int ii = ia[i]; ii < ia[i + 1]; ++ii) st_agent(&af[amap[ii]], a[ii]);
-  }
-  bool done = !valid;
-  unsigned spins = 0;
-  while (true) {
-    bool fin = false;
-    if (!done) {
-      while (kk < kd) {
-        const int id = jaf[kk];
-        if (__hip_atomic_load(&flags[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) break;
-        const double mult = ld_agent(&af[kk]) / ld_agent(&af[dg[id]]);
-        st_agent(&af[kk], mult);
-        int p = kk + 1;
-        const int ue = iaf[id + 1];
-        for (int iii = dg[id] + 1; iii < ue; ++iii) {
-          const int idd = jaf[iii];
-          while (p < ke && jaf[p] < idd) ++p;
-          if (p < ke && jaf[p] == idd) st_agent(&af[p], ld_agent(&af[p]) - mult * ld_agent(&af[iii]));
+                                                          const int* __restrict__ dg, const int* __restrict__ perm,
+                                                          int nchunks, double* af, unsigned* flags, unsigned epoch,
+                                                          unsigned* ticket, unsigned* err) {
+  const int lane = (int)threadIdx.x;
+  bool give_up = false;
+  while (!give_up) {
+    const int t = take_ticket(ticket);
+    if (t >= nchunks) break;
+    const int i = perm[(size_t)t * kSweepRows + lane];
+    const bool valid = i >= 0;
+    int kk = 0, kd = 0, kb = 0, ke = 0;
+    if (valid) {
+      kb = iaf[i];
+      kd = dg[i];
+      ke = iaf[i + 1];
+      for (int k = kb; k < ke; ++k) af[k] = 0.0;
+      for (int ii = ia[i]; ii < ia[i + 1]; ++ii) af[amap[ii]] = a[ii];
+      kk = kb;
+    }
+    bool done = !valid;
+    unsigned spins = 0;
+    while (true) {
+      bool fin = false, prog = false;
+      if (!done) {
+        while (kk < kd) {
+          const int id = jaf[kk];
+          if (__hip_atomic_load(&flags[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) break;
+          prog = true;
+          const int ub = dg[id], uend = iaf[id + 1];
+          const double mult = af[kk] / ld_agent(&af[ub]);
+          af[kk] = mult;
+          int p = kk + 1;
+          for (int c0 = ub + 1; c0 < uend; c0 += kFactorBatch) {
+            int jj[kFactorBatch];
+            double uu[kFactorBatch];
+#pragma unroll
+            for (int q = 0; q < kFactorBatch; ++q)
+              if (c0 + q < uend) {
+                jj[q] = jaf[c0 + q];
+                uu[q] = ld_agent(&af[c0 + q]);
+              }
+#pragma unroll
+            for (int q = 0; q < kFactorBatch; ++q)
+              if (c0 + q < uend) {
+                const int idd = jj[q];
+                while (p < ke && jaf[p] < idd) ++p;
+                if (p < ke && jaf[p] == idd) af[p] = af[p] - mult * uu[q];
+              }
+          }
+          ++kk;
         }
-        ++kk;
+        fin = (kk == kd);
       }
-      fin = (kk == kd);
-    }
-    if (fin) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&flags[i], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      done = true;
-    }
-    if (__all(done)) break;
-    if (__ballot(fin) == 0) {
-      if (++spins > kSpinMax) {
-        atomicOr(err, 1u);
-        break;
+      if (fin) {  // publish: agent-scope (write-through) stores, drained, then the flag
+        for (int k = kb; k < ke; ++k) st_agent(&af[k], af[k]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&flags[i], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        done = true;
       }
-      __builtin_amdgcn_s_sleep(1);
+      if (__all(done)) break;
+      backoff(spins, __ballot(fin || prog) != 0, err, 1u, give_up);
+      if (give_up) break;
     }
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Forward sweep L y = b (unit diagonal; ILU_class.cpp:470-481): y_i = b_i - sum_{k<diag} af_k y_jk,
-// subtracted one term at a time in ascending column order.
-template <int PRO>
-__global__ void __launch_bounds__(kSweepRows) k_sweep_fwd(int n, const int* __restrict__ iaf, const int* __restrict__ jaf,
-                                                         const int* __restrict__ dg, const double* __restrict__ af,
-                                                         const double* __restrict__ src, double* __restrict__ p,
-                                                         const double* __restrict__ res, const double* __restrict__ avbar,
-                                                         const CgsScalars* __restrict__ sc, uint64_t* gy, unsigned epoch,
-                                                         unsigned* ticket, unsigned* err) {
-  __shared__ uint64_t s_val[kSweepRows];  // row values forwarded inside the wavefront
-  const int blk = take_ticket(ticket);
+// Triangular sweeps (scaler_ILU::solve, ILU_class.cpp:470-499).  Forward (unit L):
+// y_i = b_i - sum_{k<diag} af_k y_jk; backward (U): x_i = (y_i - sum_{k>diag} af_k x_jk) / af_diag;
+// the terms are subtracted one at a time in ascending column order.  The forward sweep fuses the
+// CG-STAB prologue: pro 0 b = src; pro 1 pvec = res + beta*(pvec - omega*avbar)
+// (accel_class.cpp:339-341); pro 2 svec = res - alpha*avbar (361-363), stored to p.
+template <bool FWD, int PRO>
+__global__ void __launch_bounds__(kSweepRows) k_sweep(const int* __restrict__ iaf, const int* __restrict__ jaf,
+                                                     const int* __restrict__ dg, const double* __restrict__ af,
+                                                     const int* __restrict__ perm, int nchunks,
+                                                     const double* __restrict__ src, double* __restrict__ p,
+                                                     const double* __restrict__ res, const double* __restrict__ avbar,
+                                                     const CgsScalars* __restrict__ sc, const uint64_t* __restrict__ gin,
+                                                     uint64_t* gout, double* __restrict__ out, unsigned epoch,
+                                                     unsigned* ticket, unsigned* err) {
   const int lane = (int)threadIdx.x;
-  const int w0 = blk * kSweepRows;
-  const int i = w0 + lane;
-  const bool valid = i < n;
-  double acc = 0.0;
-  int k = 0, ke = 0;
-  if (valid) {
-    double b;
-    if (PRO == 0) {
-      b = src[i];
-    } else if (PRO == 1) {  // pvec = res + beta*(pvec - omega*avbar)   (accel_class.cpp:339-341)
-      b = res[i] + sc->beta * (p[i] - sc->omega * avbar[i]);
-      p[i] = b;
-    } else {  // svec = res - alpha*avbar   (accel_class.cpp:361-363)
-      b = res[i] - sc->alpha * avbar[i];
-      p[i] = b;
-    }
-    acc = b;
-    k = iaf[i];
-    ke = dg[i];
-  }
-  bool done = !valid;
-  uint64_t ready = 0;
-  unsigned spins = 0;
-  while (true) {
-    bool fin = false;
-    if (!done) {
-      while (k < ke) {
-        const int j = jaf[k];
-        double v;
-        if (j >= w0) {
-          if (!((ready >> (j - w0)) & 1ull)) break;
-          v = lds_get(&s_val[j - w0]);
-        } else if (!load_granule(gy + 2 * (size_t)j, epoch, v)) {
-          break;
+  bool give_up = false;
+  while (!give_up) {
+    const int t = take_ticket(ticket);
+    if (t >= nchunks) break;
+    const int i = perm[(size_t)t * kSweepRows + lane];
+    const bool valid = i >= 0;
+    double acc = 0.0;
+    int k = 0, ke = 0, kd = 0;
+    if (valid) {
+      if (FWD) {
+        if (PRO == 0) {
+          acc = src[i];
+        } else if (PRO == 1) {
+          acc = res[i] + sc->beta * (p[i] - sc->omega * avbar[i]);
+          p[i] = acc;
+        } else {
+          acc = res[i] - sc->alpha * avbar[i];
+          p[i] = acc;
         }
-        acc -= af[k] * v;
-        ++k;
+      } else {
+        acc = granule_value(gin + 2 * (size_t)i);
       }
-      fin = (k == ke);
+      kd = dg[i];
+      k = FWD ? iaf[i] : kd + 1;
+      ke = FWD ? kd : iaf[i + 1];
     }
-    if (fin) {
-      lds_put(&s_val[lane], acc);
-      store_granule(gy + 2 * (size_t)i, epoch, acc);
-      done = true;
-    }
-    const uint64_t fm = __ballot(fin);
-    ready |= fm;
-    if (__all(done)) break;
-    if (fm == 0) {
-      if (++spins > kSpinMax) {
-        atomicOr(err, 2u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-}
-
-// Backward sweep U x = y (ILU_class.cpp:485-499): x_i = (y_i - sum_{k>diag} af_k x_jk) / af_diag,
-// rows handed out from the last one down.
-__global__ void __launch_bounds__(kSweepRows) k_sweep_bwd(int n, const int* __restrict__ iaf, const int* __restrict__ jaf,
-                                                         const int* __restrict__ dg, const double* __restrict__ af,
-                                                         const uint64_t* __restrict__ gy, double* __restrict__ out,
-                                                         uint64_t* gx, unsigned epoch, unsigned* ticket, unsigned* err) {
-  __shared__ uint64_t s_val[kSweepRows];  // row values forwarded inside the wavefront
-  const int blk = take_ticket(ticket);
-  const int lane = (int)threadIdx.x;
-  const int whi = n - 1 - blk * kSweepRows;  // row of lane 0; lane l owns row whi - l
-  const int i = whi - lane;
-  const bool valid = i >= 0;
-  double acc = 0.0;
-  int k = 0, ke = 0, kd = 0;
-  if (valid) {
-    acc = granule_value(gy + 2 * (size_t)i);
-    kd = dg[i];
-    k = kd + 1;
-    ke = iaf[i + 1];
-  }
-  bool done = !valid;
-  uint64_t ready = 0;
-  unsigned spins = 0;
-  while (true) {
-    bool fin = false;
-    if (!done) {
-      while (k < ke) {
-        const int j = jaf[k];
-        double v;
-        if (j <= whi) {
-          if (!((ready >> (whi - j)) & 1ull)) break;
-          v = lds_get(&s_val[whi - j]);
-        } else if (!load_granule(gx + 2 * (size_t)j, epoch, v)) {
-          break;
+    bool done = !valid;
+    unsigned spins = 0;
+    while (true) {
+      bool fin = false, prog = false;
+      if (!done) {
+        while (k < ke) {
+          int jb[kBatch];
+          const int m = (ke - k < kBatch) ? ke - k : kBatch;
+#pragma unroll
+          for (int q = 0; q < kBatch; ++q) jb[q] = (q < m) ? jaf[k + q] : 0;
+          uint64_t lo[kBatch], hi[kBatch];
+#pragma unroll
+          for (int q = 0; q < kBatch; ++q)
+            if (q < m) {
+              lo[q] = __hip_atomic_load(gout + 2 * (size_t)jb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              hi[q] = __hip_atomic_load(gout + 2 * (size_t)jb[q] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          int c = 0;
+          bool blocked = false;
+#pragma unroll
+          for (int q = 0; q < kBatch; ++q)
+            if (q < m && !blocked) {
+              if ((unsigned)(lo[q] >> 32) != epoch || (unsigned)(hi[q] >> 32) != epoch) {
+                blocked = true;
+              } else {
+                acc -= af[k + q] * __longlong_as_double((long long)((hi[q] << 32) | (lo[q] & 0xffffffffull)));
+                ++c;
+              }
+            }
+          k += c;
+          prog |= (c > 0);
+          if (blocked) break;
         }
-        acc -= af[k] * v;
-        ++k;
+        fin = (k == ke);
       }
-      fin = (k == ke);
-    }
-    if (fin) {
-      acc = acc / af[kd];
-      lds_put(&s_val[lane], acc);
-      out[i] = acc;
-      store_granule(gx + 2 * (size_t)i, epoch, acc);
-      done = true;
-    }
-    const uint64_t fm = __ballot(fin);
-    ready |= fm;
-    if (__all(done)) break;
-    if (fm == 0) {
-      if (++spins > kSpinMax) {
-        atomicOr(err, 4u);
-        break;
+      if (fin) {
+        if (!FWD) acc = acc / af[kd];
+        if (!FWD) out[i] = acc;
+        store_granule(gout + 2 * (size_t)i, epoch, acc);
+        done = true;
       }
-      __builtin_amdgcn_s_sleep(1);
+      if (__all(done)) break;
+      backoff(spins, __ballot(fin || prog) != 0, err, FWD ? 2u : 4u, give_up);
+      if (give_up) break;
     }
   }
 }
@@ -464,32 +473,33 @@ void launch_spmv(int epi, int nblk, const int* rowblk, const int* ia, const int*
     hipLaunchKernelGGL(k_spmv<2>, dim3(nblk), dim3(kSpmvBlock), 0, st, rowblk, ia, ja, a, x, y, e1, partials);
 }
 
-void launch_ilu_factor(int n, const int* ia, const int* ja, const double* a, const int* amap, const int* iaf,
-                       const int* jaf, const int* dg, double* af, unsigned* flags, unsigned epoch, unsigned* ticket,
-                       unsigned* err, hipStream_t st) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_ilu_factor, dim3((n + kSweepRows - 1) / kSweepRows), dim3(kSweepRows), 0, st, n, ia, ja, a, amap,
-                     iaf, jaf, dg, af, flags, epoch, ticket, err);
+void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
+                       const int* dg, const int* perm, int nchunks, double* af, unsigned* flags, unsigned epoch,
+                       unsigned* ticket, unsigned* err, hipStream_t st) {
+  if (nchunks <= 0) return;
+  const int grid = nchunks < sweep_grid() ? nchunks : sweep_grid();
+  hipLaunchKernelGGL(k_ilu_factor, dim3(grid), dim3(kSweepRows), 0, st, ia, ja, a, amap, iaf, jaf, dg, perm, nchunks, af,
+                     flags, epoch, ticket, err);
 }
 
-void launch_sweep_fwd(int pro, int n, const int* iaf, const int* jaf, const int* dg, const double* af, const double* src,
-                      double* p, const double* res, const double* avbar, const CgsScalars* sc, uint64_t* gy,
-                      unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st) {
-  if (n <= 0) return;
-  const dim3 g((n + kSweepRows - 1) / kSweepRows), b(kSweepRows);
-  if (pro == 0)
-    hipLaunchKernelGGL(k_sweep_fwd<0>, g, b, 0, st, n, iaf, jaf, dg, af, src, p, res, avbar, sc, gy, epoch, ticket, err);
+void launch_sweep(bool fwd, int pro, const int* iaf, const int* jaf, const int* dg, const double* af, const int* perm,
+                  int nchunks, const double* src, double* p, const double* res, const double* avbar, const CgsScalars* sc,
+                  const uint64_t* gin, uint64_t* gout, double* out, unsigned epoch, unsigned* ticket, unsigned* err,
+                  hipStream_t st) {
+  if (nchunks <= 0) return;
+  const dim3 g(nchunks < sweep_grid() ? nchunks : sweep_grid()), b(kSweepRows);
+#define MMX_SWEEP(F, P)                                                                                              \
+  hipLaunchKernelGGL((k_sweep<F, P>), g, b, 0, st, iaf, jaf, dg, af, perm, nchunks, src, p, res, avbar, sc, gin, gout, \
+                     out, epoch, ticket, err)
+  if (!fwd)
+    MMX_SWEEP(false, 0);
+  else if (pro == 0)
+    MMX_SWEEP(true, 0);
   else if (pro == 1)
-    hipLaunchKernelGGL(k_sweep_fwd<1>, g, b, 0, st, n, iaf, jaf, dg, af, src, p, res, avbar, sc, gy, epoch, ticket, err);
+    MMX_SWEEP(true, 1);
   else
-    hipLaunchKernelGGL(k_sweep_fwd<2>, g, b, 0, st, n, iaf, jaf, dg, af, src, p, res, avbar, sc, gy, epoch, ticket, err);
-}
-
-void launch_sweep_bwd(int n, const int* iaf, const int* jaf, const int* dg, const double* af, const uint64_t* gy,
-                      double* out, uint64_t* gx, unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_sweep_bwd, dim3((n + kSweepRows - 1) / kSweepRows), dim3(kSweepRows), 0, st, n, iaf, jaf, dg, af,
-                     gy, out, gx, epoch, ticket, err);
+    MMX_SWEEP(true, 2);
+#undef MMX_SWEEP
 }
 
 void launch_cgs_init(int mode, int n, const double* b, double* x, double* res, double* res0, double* p, double* avbar,
