@@ -129,6 +129,35 @@ int mmadmm_write_simplices(const char* path, int dim, int nF, const int32_t* F);
 int mmadmm_debug_blockgrad(mmadmm_handle h, int s, const double* z, const double* dxpu, int flags,
                            double* out);
 
+/* ---- element partition across ranks (one process per GPU)
+ * Rank r owns simplices [r*nF/nranks, (r+1)*nF/nranks) and the nodes they touch; interface
+ * nodes are replicated and their x-update / predictor sums take the other ranks' slot values
+ * from an all-gather, summed in ascending global simplex order: node positions are bit-identical
+ * to a single-GPU run.  No reference counterpart (the reference is single-process OpenMP). */
+#define MMADMM_UNIQUE_ID_BYTES 128
+typedef struct mmadmm_comm_s* mmadmm_comm;
+typedef struct mmadmm_plan_s* mmadmm_plan;
+/* RCCL: rank 0 makes the id, every rank creates its communicator with it (collective) */
+int mmadmm_comm_unique_id(void* out, int len);
+int mmadmm_comm_create_rccl(int nranks, int rank, const void* uid, int device, mmadmm_comm* out);
+/* one communicator shared by nranks engines driven from threads of one process (tests) */
+int mmadmm_comm_create_loopback(int nranks, mmadmm_comm* out);
+int mmadmm_comm_destroy(mmadmm_comm c);
+/* like mmadmm_create, given the GLOBAL mesh on every rank; p->rank / p->nranks select the
+ * share.  mmadmm_get / mmadmm_get_simplices then return this rank's nodes / simplices (in
+ * global ids); mmadmm_local_nodes lists the global ids of the local nodes. */
+int mmadmm_create_partitioned(int dim, int nP, const double* Xp, const double* Xc, int nF, const int32_t* F,
+                              const int32_t* mask, const mmadmm_params* p, mmadmm_monitor_fn fn, void* user,
+                              mmadmm_comm comm, mmadmm_handle* out);
+int mmadmm_local_nodes(mmadmm_handle h, int* n_local, int32_t* global_ids);
+/* the partition plan alone (host only): local nodes, per-node slot sources (>= 0 local slot
+ * offset s*K+n*D, < 0 row -1-src of the gathered buffer), exported slot offsets */
+int mmadmm_plan_create(int dim, int nP, int nF, const int32_t* F, int nranks, int rank, mmadmm_plan* out);
+int mmadmm_plan_sizes(mmadmm_plan h, int* nLocalNodes, int* nLocalSimplices, int* simplexBegin, int* nSources,
+                      int* nExport, int* maxExport);
+int mmadmm_plan_get(mmadmm_plan h, int32_t* localNodes, int32_t* incPtr, int32_t* incSrc, int32_t* exportOff);
+int mmadmm_plan_destroy(mmadmm_plan h);
+
 /* device math self-test (correctly rounded powers): op 0 sqrt, 1 x^1.5, 2 x^-0.5, 3 x^2.25,
  * 4 x^1.25 */
 int mmadmm_devmath(int op, int n, const double* in, double* out);

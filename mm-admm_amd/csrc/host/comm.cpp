@@ -1,0 +1,132 @@
+// comm.cpp -- see comm.h.
+#include "comm.h"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+namespace mmx {
+namespace {
+
+#define MMX_NCCL(expr)                                                                              \
+  do {                                                                                              \
+    ncclResult_t r_ = (expr);                                                                       \
+    if (r_ != ncclSuccess)                                                                          \
+      throw ::mmx::Error(MMADMM_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));      \
+  } while (0)
+
+struct RcclComm final : Comm {
+  ncclComm_t comm = nullptr;
+  RcclComm(int n, int rank, const void* uid, int device) {
+    nranks = n;
+    MMX_HIP(hipSetDevice(device));
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    MMX_NCCL(ncclCommInitRank(&comm, n, id, rank));
+  }
+  ~RcclComm() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  void allgather(int, const double* dsend, double* drecv, size_t count, hipStream_t st) override {
+    MMX_NCCL(ncclAllGather(dsend, drecv, count, ncclDouble, comm, st));
+  }
+};
+
+// Threads of one process, one per rank, all on the same or on different devices.
+struct LoopbackComm final : Comm {
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  long long generation = 0;
+  std::vector<std::vector<double>> slots;
+  explicit LoopbackComm(int n) : slots(n) { nranks = n; }
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const long long g = generation;
+    if (++arrived == nranks) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != g; });
+    }
+  }
+  void allgather(int rank, const double* dsend, double* drecv, size_t count, hipStream_t st) override {
+    slots[rank].resize(count);
+    if (count) MMX_HIP(hipMemcpyAsync(slots[rank].data(), dsend, count * sizeof(double), hipMemcpyDeviceToHost, st));
+    MMX_HIP(hipStreamSynchronize(st));
+    barrier();
+    for (int q = 0; q < nranks; ++q)
+      if (count)
+        MMX_HIP(hipMemcpyAsync(drecv + (size_t)q * count, slots[q].data(), count * sizeof(double),
+                               hipMemcpyHostToDevice, st));
+    MMX_HIP(hipStreamSynchronize(st));
+    barrier();
+  }
+};
+
+}  // namespace
+
+Comm* make_rccl_comm(int nranks, int rank, const void* uid, int device) {
+  return new RcclComm(nranks, rank, uid, device);
+}
+Comm* make_loopback_comm(int nranks) { return new LoopbackComm(nranks); }
+void rccl_unique_id(void* out128) {
+  ncclUniqueId id;
+  MMX_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(out128, &id, sizeof(id));
+}
+
+}  // namespace mmx
+
+struct mmadmm_comm_s {
+  mmx::Comm* c;
+};
+
+extern "C" {
+
+int mmadmm_comm_unique_id(void* out, int len) {
+  return mmx::guarded([&] {
+    if (!out || len < MMADMM_UNIQUE_ID_BYTES) throw mmx::Error(MMADMM_ERR_INVALID, "unique id buffer too small");
+    mmx::rccl_unique_id(out);
+  });
+}
+
+int mmadmm_comm_create_rccl(int nranks, int rank, const void* uid, int device, mmadmm_comm* out) {
+  return mmx::guarded([&] {
+    if (!out || !uid || nranks < 1 || rank < 0 || rank >= nranks)
+      throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_comm_create_rccl: bad arguments");
+    *out = nullptr;
+    auto* h = new mmadmm_comm_s{nullptr};
+    try {
+      h->c = mmx::make_rccl_comm(nranks, rank, uid, device);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int mmadmm_comm_create_loopback(int nranks, mmadmm_comm* out) {
+  return mmx::guarded([&] {
+    if (!out || nranks < 1) throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_comm_create_loopback: bad arguments");
+    *out = new mmadmm_comm_s{mmx::make_loopback_comm(nranks)};
+  });
+}
+
+int mmadmm_comm_destroy(mmadmm_comm c) {
+  if (!c) return MMADMM_OK;
+  delete c->c;
+  delete c;
+  return MMADMM_OK;
+}
+
+}  // extern "C"
+
+namespace mmx {
+Comm* comm_of(mmadmm_comm c) { return c ? c->c : nullptr; }
+}  // namespace mmx

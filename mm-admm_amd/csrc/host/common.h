@@ -87,4 +87,7 @@ struct HostGrid {
 void build_monitor_grid(int dim, const double* X, int nP, mmadmm_monitor_fn fn, void* user,
                         HostGrid& g);
 
+struct Comm;
+Comm* comm_of(mmadmm_comm c);
+
 }  // namespace mmx

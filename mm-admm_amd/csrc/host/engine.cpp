@@ -12,7 +12,9 @@
 #include <vector>
 
 #include "../kernels/admm_kernels.h"
+#include "comm.h"
 #include "common.h"
+#include "partition.h"
 
 namespace mmx {
 
@@ -31,6 +33,7 @@ struct EngineBase {
   virtual void done() = 0;
   virtual void get(const std::string& what, double* out) = 0;
   virtual void getSimplices(int32_t* F) = 0;
+  virtual void localNodes(int* n, int32_t* ids) = 0;
   virtual void sizes(int* nP, int* nF, int* gridRows) = 0;
   virtual void setTiming(bool on) = 0;
   virtual void stats(mmadmm_stats* s) = 0;
@@ -45,11 +48,13 @@ class Engine final : public EngineBase {
   static constexpr int K = D * (D + 1);
 
   Engine(int nP, const double* Xp, const double* Xc, int nF, const int32_t* F, const int32_t* mask,
-         const mmadmm_params& p, mmadmm_monitor_fn fn, void* user) {
+         const mmadmm_params& p, mmadmm_monitor_fn fn, void* user, Comm* comm) {
     dim = D;
-    nP_ = nP;
-    nF_ = nF;
     prm_ = p;
+    nranks_ = std::max(1, p.nranks);
+    rank_ = nranks_ > 1 ? p.rank : 0;
+    comm_ = comm;
+    if (nranks_ > 1 && !comm_) throw Error(MMADMM_ERR_INVALID, "partitioned engine needs a communicator");
     if (p.device >= 0) MMX_HIP(hipSetDevice(p.device));
     MMX_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     compMesh_ = (Xc != nullptr);
@@ -93,62 +98,71 @@ class Engine final : public EngineBase {
       for (int c = 0; c < D; ++c) EhatH_[r * D + c] = Ehat[r][c];
     const double d = (double)D, pp = 1.5;
     powd_ = pow(d, d * pp / 2.0);
-    // node -> incident simplex slots, ascending simplex id (column-major D^T order)
-    std::vector<int> ptr(nP + 1, 0), off((size_t)nF * (D + 1));
-    for (int s = 0; s < nF; ++s)
-      for (int n = 0; n < D + 1; ++n) ptr[Fh_[(size_t)s * (D + 1) + n] + 1]++;
-    for (int v = 0; v < nP; ++v) ptr[v + 1] += ptr[v];
-    {
-      std::vector<int> fill(ptr.begin(), ptr.end() - 1);
-      for (int s = 0; s < nF; ++s)
-        for (int n = 0; n < D + 1; ++n) off[fill[Fh_[(size_t)s * (D + 1) + n]]++] = s * K + n * D;
-    }
+    // element partition (a single rank owns everything); node -> incident slots in ascending
+    // global simplex id (column-major D^T order), other ranks' slots from the gathered buffer
+    plan_ = make_partition_plan(D, nP, nF, Fh_.data(), nranks_, rank_);
+    nP_ = (int)plan_.localNodes.size();
+    nF_ = plan_.s1 - plan_.s0;
+    const int nl = nP_;
     // t = M + dt^2 WD_T W D is block diagonal: t_vv = tau + dt^2 * (w*w summed valence times)
-    std::vector<double> invdiag(nP);
+    std::vector<double> invdiag(nl);
     const double dtsq = p.dt * p.dt;
-    for (int v = 0; v < nP; ++v) {
+    for (int v = 0; v < nl; ++v) {
       double S = 0.0;
-      for (int c = 0; c < ptr[v + 1] - ptr[v]; ++c) S = (c == 0) ? (w * w) * 1.0 : S + (w * w) * 1.0;
+      for (int c = 0; c < plan_.valence[v]; ++c) S = (c == 0) ? (w * w) * 1.0 : S + (w * w) * 1.0;
       invdiag[v] = 1.0 / (p.tau + dtsq * S);
     }
-    std::vector<uint8_t> sbits(nF), interior(nP);
-    for (int v = 0; v < nP; ++v) interior[v] = maskH_[v] == MMADMM_INTERIOR ? 1 : 0;
-    for (int s = 0; s < nF; ++s) {
+    std::vector<uint8_t> sbits(nF_), interior(nl);
+    for (int v = 0; v < nl; ++v) interior[v] = maskH_[plan_.localNodes[v]] == MMADMM_INTERIOR ? 1 : 0;
+    for (int s = 0; s < nF_; ++s) {
       unsigned b = 0;
       for (int n = 0; n < D + 1; ++n) {
-        const int t = maskH_[Fh_[(size_t)s * (D + 1) + n]];
+        const int t = maskH_[plan_.localNodes[plan_.Flocal[(size_t)s * (D + 1) + n]]];
         if (t == MMADMM_BOUNDARY_FIXED) b |= 1u << n;
         if (t != MMADMM_INTERIOR) b |= 1u << (4 + n);
       }
       sbits[s] = (uint8_t)b;
     }
+    std::vector<double> Vl((size_t)nl * D), Vcl;
+    for (int v = 0; v < nl; ++v)
+      for (int c = 0; c < D; ++c) Vl[(size_t)v * D + c] = Vp[(size_t)plan_.localNodes[v] * D + c];
+    if (compMesh_) {
+      Vcl.resize((size_t)nl * D);
+      for (int v = 0; v < nl; ++v)
+        for (int c = 0; c < D; ++c) Vcl[(size_t)v * D + c] = Xc[(size_t)plan_.localNodes[v] * D + c];
+    }
     // device state
-    F_.upload(Fh_.data(), Fh_.size(), st_);
+    F_.upload(plan_.Flocal.data(), plan_.Flocal.size(), st_);
     sbits_.upload(sbits.data(), sbits.size(), st_);
     interior_.upload(interior.data(), interior.size(), st_);
-    incPtr_.upload(ptr.data(), ptr.size(), st_);
-    incOff_.upload(off.data(), off.size(), st_);
+    incPtr_.upload(plan_.incPtr.data(), plan_.incPtr.size(), st_);
+    incOff_.upload(plan_.incSrc.data(), plan_.incSrc.size(), st_);
     invdiag_.upload(invdiag.data(), invdiag.size(), st_);
-    if (compMesh_) Vc_.upload(Xc, (size_t)nP * D, st_);
+    if (compMesh_) Vc_.upload(Vcl.data(), Vcl.size(), st_);
     gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
     gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
     if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
     gvals_.upload(grid_.vals.data(), grid_.vals.size(), st_);
-    Vp_.upload(Vp.data(), Vp.size(), st_);  // Mesh::Vp
-    x_.upload(Vp.data(), Vp.size(), st_);   // MeshIntegrator ctor: x = xPrev = xBar = copyX(Vp)
-    xPrev_.upload(Vp.data(), Vp.size(), st_);
-    xBar_.upload(Vp.data(), Vp.size(), st_);
-    z_.alloc((size_t)nF * K);
-    u_.alloc((size_t)nF * K);
-    gs_.alloc((size_t)nF * K);
+    Vp_.upload(Vl.data(), Vl.size(), st_);  // Mesh::Vp
+    x_.upload(Vl.data(), Vl.size(), st_);   // MeshIntegrator ctor: x = xPrev = xBar = copyX(Vp)
+    xPrev_.upload(Vl.data(), Vl.size(), st_);
+    xBar_.upload(Vl.data(), Vl.size(), st_);
+    if (nranks_ > 1) {
+      expOff_.upload(plan_.exportOff.data(), std::max<size_t>(plan_.exportOff.size(), 1), st_);
+      export_.alloc((size_t)std::max(plan_.maxExport, 1) * D);
+      remote_.alloc((size_t)nranks_ * std::max(plan_.maxExport, 1) * D);
+    }
+    z_.alloc((size_t)nF_ * K);
+    u_.alloc((size_t)nF_ * K);
+    gs_.alloc((size_t)nF_ * K);
     MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
     {
-      std::vector<double> eye((size_t)nF * K * K, 0.0);  // hessInvs = I (src/Mesh.cpp:456-464)
-      for (int s = 0; s < nF; ++s)
+      std::vector<double> eye((size_t)nF_ * K * K, 0.0);  // hessInvs = I (src/Mesh.cpp:456-464)
+      for (int s = 0; s < nF_; ++s)
         for (int i = 0; i < K; ++i) eye[(size_t)s * K * K + i * K + i] = 1.0;
       B_.upload(eye.data(), eye.size(), st_);
     }
-    const size_t maxBlocks = std::max<size_t>(1, std::max((nF + 255) / 256, (nP + 255) / 256));
+    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 255) / 256, (nP_ + 255) / 256));
     partA_.alloc(maxBlocks * kNumPartials);
     partB_.alloc(maxBlocks * kNumPartials);
     resultsCap_ = 0;
@@ -180,6 +194,7 @@ class Engine final : public EngineBase {
     if (prm_.grad_use || stepsTaken_ <= 2) {
       int nb = 0;
       launch_grad_simplex<D>(m_, x_.p, gs_.p, true, partA_.p, &nb, st_);
+      exchange(1);
       launch_predict<D>(m_, 0, gs_.p, x_.p, xPrev_.p, xBar_.p, dtOverTau, st_);
     } else {
       launch_predict<D>(m_, 1, nullptr, x_.p, xPrev_.p, xBar_.p, dtOverTau, st_);
@@ -189,6 +204,7 @@ class Engine final : public EngineBase {
     if (!stepTaken_) MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
     StepScalars sc{prm_.tau, prm_.dt * prm_.dt, w_, dtOverTau};
     int nbx = 0, nbp = 0;
+    exchange(0);
     launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, false, st_);
     const bool early = tol >= 0;
     int done = 0;
@@ -207,6 +223,7 @@ class Engine final : public EngineBase {
       }
       hessComputed_ = true;
       stepTaken_ = true;
+      exchange(0);
       launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, true, st_);
       if (timing) {
         b1 = nextEvent();
@@ -217,9 +234,9 @@ class Engine final : public EngineBase {
       launch_reduce_partials(partB_.p, nbx, results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
       done = i + 1;
       if (early) {
-        double r[2 * kNumPartials];
-        MMX_HIP(hipMemcpyAsync(r, results_.p + (size_t)i * 2 * kNumPartials, sizeof(r), hipMemcpyDeviceToHost, st_));
-        MMX_HIP(hipStreamSynchronize(st_));
+        std::vector<double> rv;
+        fetchResults(results_.p + (size_t)i * 2 * kNumPartials, 1, rv);
+        const double* r = rv.data();
         primal = sqrt(r[kNumPartials + 2]);
         dual = sqrt(r[1]);
         if (r[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element in prox (reference: assert(Edet > 0))");
@@ -232,9 +249,7 @@ class Engine final : public EngineBase {
       eStep1 = nextEvent();
       MMX_HIP(hipEventRecord(eStep1, st_));
     }
-    hostRes_.resize((size_t)done * 2 * kNumPartials);
-    MMX_HIP(hipMemcpyAsync(hostRes_.data(), results_.p, hostRes_.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    fetchResults(results_.p, done, hostRes_);
     MMX_HIP(hipGetLastError());
     bool bad = false;
     long long bf = 0;
@@ -281,10 +296,11 @@ class Engine final : public EngineBase {
     int nb = 0;
     launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
     launch_reduce_partials(partA_.p, nb, results_.p, st_);
+    exchange(1);
     launch_euler_apply<D>(m_, gs_.p, x_.p, prm_.dt / prm_.tau, st_);
-    double r[kNumPartials];
-    MMX_HIP(hipMemcpyAsync(r, results_.p, sizeof(r), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    std::vector<double> rv;
+    fetchResults(results_.p, 1, rv);
+    const double* r = rv.data();
     if (r[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element (reference: assert(Edet > 0))");
     return r[0];
   }
@@ -294,10 +310,9 @@ class Engine final : public EngineBase {
     int nb = 0;
     launch_energy<D>(m_, Vp_.p, partA_.p, &nb, st_);
     launch_reduce_partials(partA_.p, nb, results_.p, st_);
-    double r[kNumPartials];
-    MMX_HIP(hipMemcpyAsync(r, results_.p, sizeof(r), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
-    return r[0];
+    std::vector<double> rv;
+    fetchResults(results_.p, 1, rv);
+    return rv[0];
   }
 
   void done() override {
@@ -328,7 +343,14 @@ class Engine final : public EngineBase {
     MMX_HIP(hipStreamSynchronize(st_));
   }
 
-  void getSimplices(int32_t* F) override { std::memcpy(F, Fh_.data(), Fh_.size() * sizeof(int32_t)); }
+  void getSimplices(int32_t* F) override {  // this rank's simplices, global node ids, re-oriented
+    for (size_t i = 0; i < plan_.Flocal.size(); ++i) F[i] = plan_.localNodes[plan_.Flocal[i]];
+  }
+
+  void localNodes(int* n, int32_t* ids) override {
+    if (n) *n = nP_;
+    if (ids) std::memcpy(ids, plan_.localNodes.data(), plan_.localNodes.size() * sizeof(int32_t));
+  }
 
   void sizes(int* nP, int* nF, int* gridRows) override {
     if (nP) *nP = nP_;
@@ -379,6 +401,36 @@ class Engine final : public EngineBase {
     return h0 - h1 + h2;
   }
 
+  // all-gather of this rank's interface-slot values: mode 0 x-update terms, 1 simplex gradients
+  void exchange(int mode) {
+    if (nranks_ == 1) return;
+    launch_pack_export<D>(mode, (int)plan_.exportOff.size(), expOff_.p, z_.p, u_.p, gs_.p, w_, export_.p, st_);
+    comm_->allgather(rank_, export_.p, remote_.p, (size_t)std::max(plan_.maxExport, 1) * D, st_);
+  }
+
+  // rows x 2*kNumPartials scalar records on the device -> combined over ranks on the host
+  // (sums in rank order; the max-BFGS entry by max)
+  void fetchResults(const double* dev, int rows, std::vector<double>& out) {
+    const size_t cnt = (size_t)rows * 2 * kNumPartials;
+    out.resize(cnt);
+    if (nranks_ == 1) {
+      MMX_HIP(hipMemcpyAsync(out.data(), dev, cnt * sizeof(double), hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+      return;
+    }
+    if (resAll_.n < cnt * nranks_) resAll_.alloc(cnt * nranks_);
+    comm_->allgather(rank_, dev, resAll_.p, cnt, st_);
+    std::vector<double> all(cnt * nranks_);
+    MMX_HIP(hipMemcpyAsync(all.data(), resAll_.p, all.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    for (size_t i = 0; i < cnt; ++i) {
+      const bool isMax = (i % kNumPartials) == 5;
+      double v = all[i];
+      for (int q = 1; q < nranks_; ++q) v = isMax ? std::max(v, all[(size_t)q * cnt + i]) : v + all[(size_t)q * cnt + i];
+      out[i] = v;
+    }
+  }
+
   DeviceMesh<D> makeView() const {
     DeviceMesh<D> m{};
     m.nP = nP_;
@@ -388,6 +440,7 @@ class Engine final : public EngineBase {
     m.nodeInterior = interior_.p;
     m.inc_ptr = incPtr_.p;
     m.inc_off = incOff_.p;
+    m.remote = nranks_ > 1 ? remote_.p : nullptr;
     m.invdiag = invdiag_.p;
     m.Vc = compMesh_ ? Vc_.p : nullptr;
     m.gx = gx_.p;
@@ -430,7 +483,11 @@ class Engine final : public EngineBase {
   DevBuf<int32_t> F_, incPtr_, incOff_;
   DevBuf<uint8_t> sbits_, interior_;
   DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_;
-  DevBuf<double> partA_, partB_, results_;
+  DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
+  DevBuf<int32_t> expOff_;
+  PartitionPlan plan_;
+  Comm* comm_ = nullptr;
+  int rank_ = 0, nranks_ = 1;
   int resultsCap_ = 0;
   std::vector<double> hostRes_;
   DeviceMesh<D> m_{};
@@ -472,22 +529,58 @@ int mmadmm_create(int dim, int nP, const double* Xp, const double* Xc, int nF, c
       throw Error(MMADMM_ERR_INVALID, "mmadmm_create: bad arguments");
     if (!(p->dt > 0) || !(p->tau > 0) || !(p->rho > 0))
       throw Error(MMADMM_ERR_INVALID, "mmadmm_create: dt, tau, rho must be positive");
-    if (p->nranks > 1) throw Error(MMADMM_ERR_INVALID, "mmadmm_create: use mmadmm_create_partition for nranks > 1");
+    if (p->nranks > 1) throw Error(MMADMM_ERR_INVALID, "mmadmm_create: use mmadmm_create_partitioned for nranks > 1");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
       throw Error(MMADMM_ERR_HIP, "mmadmm_create: no HIP device (the engine has no CPU fallback)");
     auto* h = new mmadmm_engine();
     try {
       if (dim == 2)
-        h->e.reset(new mmx::Engine<2>(nP, Xp, Xc, nF, F, mask, *p, fn, user));
+        h->e.reset(new mmx::Engine<2>(nP, Xp, Xc, nF, F, mask, *p, fn, user, nullptr));
       else
-        h->e.reset(new mmx::Engine<3>(nP, Xp, Xc, nF, F, mask, *p, fn, user));
+        h->e.reset(new mmx::Engine<3>(nP, Xp, Xc, nF, F, mask, *p, fn, user, nullptr));
     } catch (...) {
       delete h;
       throw;
     }
     *out = h;
   });
+}
+
+int mmadmm_create_partitioned(int dim, int nP, const double* Xp, const double* Xc, int nF, const int32_t* F,
+                              const int32_t* mask, const mmadmm_params* p, mmadmm_monitor_fn fn, void* user,
+                              mmadmm_comm comm, mmadmm_handle* out) {
+  return guarded([&] {
+    if (!out) throw Error(MMADMM_ERR_INVALID, "mmadmm_create_partitioned: out is NULL");
+    *out = nullptr;
+    if ((dim != 2 && dim != 3) || nP < dim + 1 || nF < 1 || !Xp || !F || !mask || !p || !fn)
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_create_partitioned: bad arguments");
+    if (!(p->dt > 0) || !(p->tau > 0) || !(p->rho > 0))
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_create_partitioned: dt, tau, rho must be positive");
+    if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks)
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_create_partitioned: bad rank / nranks");
+    mmx::Comm* c = mmx::comm_of(comm);
+    if (p->nranks > 1 && (!c || c->nranks != p->nranks))
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_create_partitioned: communicator missing or of another size");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+      throw Error(MMADMM_ERR_HIP, "mmadmm_create_partitioned: no HIP device (the engine has no CPU fallback)");
+    auto* h = new mmadmm_engine();
+    try {
+      if (dim == 2)
+        h->e.reset(new mmx::Engine<2>(nP, Xp, Xc, nF, F, mask, *p, fn, user, c));
+      else
+        h->e.reset(new mmx::Engine<3>(nP, Xp, Xc, nF, F, mask, *p, fn, user, c));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int mmadmm_local_nodes(mmadmm_handle h, int* n_local, int32_t* global_ids) {
+  return guarded([&] { eng(h).localNodes(n_local, global_ids); });
 }
 
 int mmadmm_step(mmadmm_handle h, int n_iters, double tol, double* Ih, int* admm_iters) {

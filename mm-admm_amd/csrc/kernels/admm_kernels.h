@@ -16,8 +16,10 @@ struct DeviceMesh {
   const int* F;           // nF x (D+1)
   const uint8_t* sbits;   // per simplex: bit n = vertex n FIXED, bit 4+n = vertex n not INTERIOR
   const uint8_t* nodeInterior;  // per node 1 if INTERIOR
-  const int* inc_ptr;     // nP+1, node -> incident slots, ascending simplex id
-  const int* inc_off;     // offset s*K + n*D of each incident slot
+  const int* inc_ptr;     // nP+1, node -> incident slots, ascending (global) simplex id
+  const int* inc_off;     // offset s*K + n*D of each local incident slot; -1-r for a slot of another
+                          // rank: its D values are row r of `remote` (element partition)
+  const double* remote;   // gathered interface-slot values of the other ranks (or nullptr)
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)
   const double* Vc;       // nP x D reference positions (CompMesh) or nullptr
   // monitor grid
@@ -58,6 +60,11 @@ template <int D>
 void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
                         hipStream_t st);
 void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st);
+// interface-slot values a rank contributes to the exchange: mode 0 the x-update term
+// w (w (z - u)) per slot, mode 1 the simplex gradient gs per slot (D values each)
+template <int D>
+void launch_pack_export(int mode, int nExp, const int* expOff, const double* z, const double* u, const double* gs,
+                        double w, double* out, hipStream_t st);
 
 template <int D>
 void launch_debug_blockgrad(const DeviceMesh<D>& m, int s, const double* z, const double* dx, double* out,

@@ -160,8 +160,9 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
     const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
     for (int t = b; t < e; ++t) {
       const int off = m.inc_off[t];
+      const double* src = (off >= 0) ? gs + off : m.remote + (size_t)(-1 - off) * D;
 #pragma unroll
-      for (int c = 0; c < D; ++c) g[c] += gs[(size_t)off + c];
+      for (int c = 0; c < D; ++c) g[c] += src[c];
     }
 #pragma unroll
     for (int c = 0; c < D; ++c) xb[c] = xv[c] - dt_over_tau * g[c];
@@ -192,9 +193,15 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
     for (int c = 0; c < D; ++c) acc[c] = 0.0;
     const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
     for (int t = b; t < e; ++t) {
-      const size_t off = (size_t)m.inc_off[t];
+      const int off = m.inc_off[t];
+      if (off >= 0) {
 #pragma unroll
-      for (int c = 0; c < D; ++c) acc[c] += sc.w * (sc.w * (z[off + c] - u[off + c]));
+        for (int c = 0; c < D; ++c) acc[c] += sc.w * (sc.w * (z[(size_t)off + c] - u[(size_t)off + c]));
+      } else {  // another rank's slot: the same term, formed there (launch_pack_export mode 0)
+        const double* r = m.remote + (size_t)(-1 - off) * D;
+#pragma unroll
+        for (int c = 0; c < D; ++c) acc[c] += r[c];
+      }
     }
     const double inv = m.invdiag[v];
     double xn[D];
@@ -206,10 +213,11 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
     if constexpr (RESID) {
       double r2 = 0.0;
       for (int t = b; t < e; ++t) {
-        const size_t off = (size_t)m.inc_off[t];
+        const int off = m.inc_off[t];
+        if (off < 0) continue;  // counted by the rank that owns the slot
 #pragma unroll
         for (int c = 0; c < D; ++c) {
-          const double d = xn[c] - z[off + c];
+          const double d = xn[c] - z[(size_t)off + c];
           r2 += d * d;
         }
       }
@@ -569,12 +577,26 @@ __global__ void __launch_bounds__(kBlock) k_euler_apply(DeviceMesh<D> m, const d
     const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
     for (int t = b; t < e; ++t) {
       const int off = m.inc_off[t];
+      const double* src = (off >= 0) ? gs + off : m.remote + (size_t)(-1 - off) * D;
 #pragma unroll
-      for (int c = 0; c < D; ++c) g[c] += gs[(size_t)off + c];
+      for (int c = 0; c < D; ++c) g[c] += src[c];
     }
   }
 #pragma unroll
   for (int c = 0; c < D; ++c) x[(size_t)v * D + c] -= dt_over_tau * g[c];
+}
+
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_pack_export(int mode, int nExp, const int* __restrict__ expOff,
+                                                         const double* __restrict__ z, const double* __restrict__ u,
+                                                         const double* __restrict__ gs, double w,
+                                                         double* __restrict__ out) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= nExp) return;
+  const size_t off = (size_t)expOff[e];
+#pragma unroll
+  for (int c = 0; c < D; ++c)
+    out[(size_t)e * D + c] = (mode == 0) ? w * (w * (z[off + c] - u[off + c])) : gs[off + c];
 }
 
 __global__ void __launch_bounds__(kBlock) k_reduce_partials(const double* __restrict__ partials, int nblocks,
@@ -723,6 +745,18 @@ template void launch_debug_blockgrad<2>(const DeviceMesh<2>&, int, const double*
                                         hipStream_t);
 template void launch_debug_blockgrad<3>(const DeviceMesh<3>&, int, const double*, const double*, double*, int,
                                         hipStream_t);
+template <int D>
+void launch_pack_export(int mode, int nExp, const int* expOff, const double* z, const double* u, const double* gs,
+                        double w, double* out, hipStream_t st) {
+  if (nExp <= 0) return;
+  hipLaunchKernelGGL(k_pack_export<D>, dim3((nExp + kBlock - 1) / kBlock), dim3(kBlock), 0, st, mode, nExp, expOff, z, u,
+                     gs, w, out);
+}
+template void launch_pack_export<2>(int, int, const int*, const double*, const double*, const double*, double, double*,
+                                    hipStream_t);
+template void launch_pack_export<3>(int, int, const int*, const double*, const double*, const double*, double, double*,
+                                    hipStream_t);
+
 void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st) {
   if (n == 0) return;
   hipLaunchKernelGGL(k_devmath, dim3((n + 255) / 256), dim3(256), 0, st, op, n, in, out);

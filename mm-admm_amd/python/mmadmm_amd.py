@@ -100,6 +100,19 @@ def lib():
     L.mmadmm_debug_blockgrad.argtypes = [ctypes.c_void_p, ctypes.c_int, c_double_p, c_double_p, ctypes.c_int,
                                          c_double_p]
     L.mmadmm_devmath.argtypes = [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p]
+    vp = ctypes.c_void_p
+    L.mmadmm_comm_unique_id.argtypes = [vp, ctypes.c_int]
+    L.mmadmm_comm_create_rccl.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.mmadmm_comm_create_loopback.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.mmadmm_comm_destroy.argtypes = [vp]
+    L.mmadmm_create_partitioned.argtypes = [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, ctypes.c_int, c_int_p,
+                                            c_int_p, ctypes.POINTER(mmadmm_params), MONITOR_FN, vp, vp,
+                                            ctypes.POINTER(vp)]
+    L.mmadmm_local_nodes.argtypes = [vp, ctypes.POINTER(ctypes.c_int), c_int_p]
+    L.mmadmm_plan_create.argtypes = [ctypes.c_int] * 3 + [c_int_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.mmadmm_plan_sizes.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int)] * 6
+    L.mmadmm_plan_get.argtypes = [vp, c_int_p, c_int_p, c_int_p, c_int_p]
+    L.mmadmm_plan_destroy.argtypes = [vp]
     _lib = L
     return L
 
@@ -241,25 +254,96 @@ class Mesh:
         self.device = device
 
 
+UNIQUE_ID_BYTES = 128
+
+
+class Comm:
+    """Communicator of an element-partitioned run: RCCL between processes (one per GPU) or a
+    loopback shared by the engines of one process (driven from threads; tests)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+        _check(lib().mmadmm_comm_unique_id(buf, UNIQUE_ID_BYTES))
+        return buf.raw
+
+    @staticmethod
+    def rccl(nranks, rank, uid, device):
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), UNIQUE_ID_BYTES)
+        _check(lib().mmadmm_comm_create_rccl(int(nranks), int(rank), buf, int(device), ctypes.byref(h)))
+        return Comm(h)
+
+    @staticmethod
+    def loopback(nranks):
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_comm_create_loopback(int(nranks), ctypes.byref(h)))
+        return Comm(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mmadmm_comm_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+
+def partition_plan(dim, nP, F, nranks, rank):
+    """The element partition of rank `rank` (host only) -> dict of numpy arrays."""
+    L = lib()
+    F = np.ascontiguousarray(F, dtype=np.int32)
+    h = ctypes.c_void_p()
+    _check(L.mmadmm_plan_create(int(dim), int(nP), len(F), _ip(F), int(nranks), int(rank), ctypes.byref(h)))
+    try:
+        v = [ctypes.c_int() for _ in range(6)]
+        _check(L.mmadmm_plan_sizes(h, *[ctypes.byref(x) for x in v]))
+        nl, nfl, s0, ns, ne, mx = [x.value for x in v]
+        out = dict(localNodes=np.zeros(nl, np.int32), incPtr=np.zeros(nl + 1, np.int32),
+                   incSrc=np.zeros(ns, np.int32), exportOff=np.zeros(ne, np.int32))
+        _check(L.mmadmm_plan_get(h, _ip(out["localNodes"]), _ip(out["incPtr"]), _ip(out["incSrc"]),
+                                 _ip(out["exportOff"])))
+        out.update(nLocalSimplices=nfl, simplexBegin=s0, maxExport=mx)
+        return out
+    finally:
+        L.mmadmm_plan_destroy(h)
+
+
 class Engine:
     """Direct handle on one libmmadmm integrator (what MeshIntegrator wraps)."""
 
-    def __init__(self, mesh, dt):
+    def __init__(self, mesh, dt, rank=0, nranks=1, comm=None):
+        """rank/nranks/comm: element-partitioned run (include/mmadmm.h); `mesh` is the global mesh
+        on every rank and this engine owns simplices [rank*nF/nranks, (rank+1)*nF/nranks)."""
         L = lib()
         p = mmadmm_params(dt=float(dt), tau=mesh.tau, rho=mesh.rho, grad_use=int(mesh.gradUse),
-                          device=mesh.device, rank=0, nranks=1)
+                          device=mesh.device, rank=int(rank), nranks=int(nranks))
         fn, user = mesh.Mon._cfunc()
         self._fn = fn
         h = ctypes.c_void_p()
         Xc = _dp(mesh.Xc) if mesh.Xc is not None else None
-        _check(L.mmadmm_create(mesh.dim, mesh.Xp.shape[0], _dp(mesh.Xp), Xc, mesh.F.shape[0], _ip(mesh.F),
-                               _ip(mesh.mask), ctypes.byref(p), fn, user, ctypes.byref(h)))
+        if nranks == 1 and comm is None:
+            _check(L.mmadmm_create(mesh.dim, mesh.Xp.shape[0], _dp(mesh.Xp), Xc, mesh.F.shape[0], _ip(mesh.F),
+                                   _ip(mesh.mask), ctypes.byref(p), fn, user, ctypes.byref(h)))
+        else:
+            _check(L.mmadmm_create_partitioned(mesh.dim, mesh.Xp.shape[0], _dp(mesh.Xp), Xc, mesh.F.shape[0],
+                                               _ip(mesh.F), _ip(mesh.mask), ctypes.byref(p), fn, user,
+                                               comm.h if comm is not None else None, ctypes.byref(h)))
         self.h = h
+        self.comm = comm
         self.dim = mesh.dim
         nP, nF, gr = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(L.mmadmm_sizes(h, ctypes.byref(nP), ctypes.byref(nF), ctypes.byref(gr)))
         self.nP, self.nF, self.gridRows = nP.value, nF.value, gr.value
         self.K = self.dim * (self.dim + 1)
+
+    def local_nodes(self):
+        """Global ids of this engine's nodes (all nodes for a single-GPU engine)."""
+        ids = np.zeros(self.nP, dtype=np.int32)
+        _check(lib().mmadmm_local_nodes(self.h, None, _ip(ids)))
+        return ids
 
     def close(self):
         if getattr(self, "h", None):
