@@ -9,8 +9,16 @@ disabled, SURVEY §8d protocol); value = ADMM iterations per second over the tim
 first warm-up step (finite-difference Hessians) is reported separately.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-For N > 1 launch with torch.distributed.run: each rank runs its own element-partitioned share
-(weak scaling).
+For N > 1 launch with torch.distributed.run: the global mesh grows with N (hexagonal disc of
+N_disc = 577*sqrt(N), ~N million nodes) and is element-partitioned across the ranks, one per GPU,
+exchanging interface-slot values with RCCL all-gathers (weak scaling).
+value = ADMM iterations per second x (global nodes / 1,000,519): whole-job throughput in units of
+C3-sized meshes.
+
+The second half of the metric, achieved HBM GB/s in SpMV, is measured on the backward-Euler
+Jacobian CSR of the 2D SquareGrid n=707 mesh (n = 2,002,226 rows, nnz = 28,008,516, SURVEY §8d
+microbenchmark ii) with the LASolver replacement's matmult, and reported under "spmv" together
+with one ILU(0)-preconditioned CG-STAB solve of that matrix.
 """
 import argparse
 import json
@@ -33,20 +41,95 @@ def parse():
     ap.add_argument("--disc-n", type=int, default=577)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-spmv", action="store_true")
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix):
-    """Per-launch HBM bytes of a kernel from the committed rocprofv3 PMC summary, or None."""
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def spmv_bench(torch, la, mx, with_cpu):
+    """matmult on the n=707 Jacobian (28.0 M nonzeros) + one ILU(0)-CG-STAB solve."""
+    import numpy as np
+    mesh = mx.MeshData.rect(2, 707)
+    s = la.MatrixStruc(2 * mesh.nP)
+    s.mesh_pattern(2, mesh.F)
+    s.pack()
+    ia, ja = s.getia(), s.getja()
+    n = len(ia) - 1
+    rng = np.random.default_rng(20221015)
+    a = rng.uniform(-1.0, 1.0, len(ja))
+    x = rng.uniform(-1.0, 1.0, n)
+    A = la.MatrixIter(s)
+    A.a[:] = a
+    A.upload()
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty(n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(5):
+        A.matmult_device(xd.data_ptr(), yd.data_ptr())
+    A.set_timing(True)
+    A.reset_stats()
+    reps = 50
+    for _ in range(reps):
+        A.matmult_device(xd.data_ptr(), yd.data_ptr())
+    st = A.stats()
+    ms = st["t_spmv_ms"] / st["n_spmv_timed"]
+    gbs = st["spmv_bytes"] / (ms * 1e-3) / 1e9
+    out = {"matrix": "SquareGrid n=707 backward-Euler Jacobian pattern (src/Mesh.cpp:309-345), values U(-1,1)",
+           "rows": n, "nnz": int(len(ja)), "bytes_per_spmv": st["spmv_bytes"], "avg_ms": round(ms, 5),
+           "achieved_GBs": round(gbs, 1), "peak_GBs": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "kernel": "k_spmv<0>", "reps": reps}
+    tr, trr = pmc_traffic("k_spmv<0>")
+    out["traffic"], out["traffic_fetch_uncorrected"] = tr, trr
+    # one solve: diagonally dominant values (SURVEY §8d), src/Mesh.cpp parameters
+    rows = np.repeat(np.arange(n), np.diff(ia))
+    d = np.nonzero(ja == rows)[0]
+    a2 = a.copy()
+    a2[d] = np.add.reduceat(np.abs(a2), ia[:-1]) * 0.5 + 1.0
+    b = rng.uniform(-1.0, 1.0, n)
+    A.a[:] = a2
+    A.b[:] = b
+    p = la.ParamIter.mesh()
+    A.sfac(p)
+    A.reset_stats()
+    xs = np.zeros(n)
+    nitr = A.solve(p, xs)
+    st = A.stats()
+    out["cgstab"] = {"nitr": nitr, "solve_ms": round(st["t_solve_ms"], 2), "factor_ms": round(st["t_factor_ms"], 2),
+                     "sweep_ms": round(st["t_sweep_ms"] / max(st["n_sweep_timed"], 1), 3),
+                     "ms_per_iter": round((st["t_solve_ms"] - st["t_factor_ms"]) / max(nitr, 1), 2)}
+    if with_cpu:
+        import time as _t
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import lasolver_py as L
+        t0 = _t.perf_counter()
+        for _ in range(3):
+            L.matmult(ia, ja, a, x)
+        cms = (_t.perf_counter() - t0) / 3 * 1e3
+        t0 = _t.perf_counter()
+        _, cit, _ = L.solve(ia, ja, a2, b)
+        csolve = (_t.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"matmult_ms": round(cms, 2), "solve_ms": round(csolve, 1), "nitr": cit, "cores": 1,
+                               "kind": "port", "sample": "oracle/lasolver.cpp (bit-identical restatement of "
+                               "lib/LASolver, itself pinned to the reference build): 3 matmults + 1 solve"}
+    A.close()
+    return out
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes of a kernel from the committed rocprofv3 PMC passes
+    (profiles/pmc_summary.json: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE; and raw)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
+            d = json.load(f).get(kernel, {})
+        return d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_raw_per_launch")
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def cpu_baseline(mesh, admm_iter, threads):
@@ -79,12 +162,33 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     import mmadmm_amd as mx
+    import lasolver_amd as la
 
-    mesh = mx.MeshData.hexdisc(args.disc_n, 0.5, 0.5, 0.5)
+    c3_nodes = 1000519
+    disc_n = args.disc_n if world == 1 else int(round(args.disc_n * world ** 0.5))
+    log(f"rank {rank}/{world}: hexdisc N={disc_n}")
+    mesh = mx.MeshData.hexdisc(disc_n, 0.5, 0.5, 0.5)
     M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5, device=local)
     t_setup = time.perf_counter()
-    eng = mx.Engine(M, 0.055)
+    parallelism = "single"
+    comm = None
+    if world > 1:
+        try:
+            uid = [mx.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = mx.Comm.rccl(world, rank, uid[0], local)
+            eng = mx.Engine(M, 0.055, rank=rank, nranks=world, comm=comm)
+            parallelism = f"element-partition x{world} (RCCL all-gather of interface slots)"
+        except mx.MMADMMError as e:  # report, and measure independent replicas instead
+            log(f"partitioned engine unavailable ({e}); running replicas")
+            mesh = mx.MeshData.hexdisc(args.disc_n, 0.5, 0.5, 0.5)
+            M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5, device=local)
+            eng = mx.Engine(M, 0.055)
+            parallelism = f"replicas x{world} (partitioned engine failed: {e})"
+    else:
+        eng = mx.Engine(M, 0.055)
     t_setup = time.perf_counter() - t_setup
+    log(f"rank {rank}: setup {t_setup:.1f}s, local nodes {eng.nP}, local simplices {eng.nF}")
 
     first_ms = None
     for w in range(max(args.warmup, 1)):
@@ -115,15 +219,16 @@ def main():
         elapsed = float(t.item())
 
     st = eng.stats()
-    iters = args.steps * args.admm_iter * world
+    iters = args.steps * args.admm_iter
+    scale = mesh.nP / c3_nodes if parallelism.startswith("element") else (world if world > 1 else mesh.nP / c3_nodes)
     prox_ms = st["t_prox_ms"] / max(st["n_prox"], 1)
     xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
     prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
     xup_gbs = st["xupdate_bytes"] / (xup_ms * 1e-3) / 1e9
-    traffic = pmc_traffic("k_prox")
+    traffic, traffic_raw = pmc_traffic("k_prox_lds<2>")
     result = {
         "metric": "ADMM iterations/sec on 1M-node 2D mesh; achieved HBM GB/s in SpMV",
-        "value": round(iters / elapsed, 3),
+        "value": round(iters / elapsed * scale, 3),
         "unit": "ADMM it/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -136,13 +241,16 @@ def main():
         "data": "synthetic",
         "config": {"workload": "C3: 2D circular mesh (hexagonal disc N=%d), %d nodes, %d triangles, MEx1 "
                                "monitor, dt 0.055 tau 0.5 rho 50, %d ADMM iterations per step"
-                               % (args.disc_n, mesh.nP, mesh.nF, args.admm_iter),
-                   "nodes_per_gpu": mesh.nP, "simplices_per_gpu": mesh.nF, "admm_iter": args.admm_iter,
-                   "parallelism": "replicas" if world > 1 else "single"},
+                               % (disc_n, mesh.nP, mesh.nF, args.admm_iter),
+                   "global_nodes": mesh.nP, "global_simplices": mesh.nF, "nodes_rank0": eng.nP,
+                   "simplices_rank0": eng.nF, "admm_iter": args.admm_iter, "parallelism": parallelism,
+                   "value_unit_note": "ADMM it/s x global nodes / 1,000,519"},
         "roofline": {"bound": "hbm", "kernel": "k_prox_lds<2>",
                      "achieved": round(prox_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "bytes_per_launch": st["prox_bytes"],
+                     "traffic": traffic, "traffic_fetch_uncorrected": traffic_raw,
+                     "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE, WRITE_SIZE passes)",
+                     "bytes_per_launch": st["prox_bytes"],
                      "avg_launch_ms": round(prox_ms, 4)},
         "kernels": {"k_prox_ms": round(prox_ms, 4), "k_xupdate_ms": round(xup_ms, 4),
                     "k_xupdate_GBs": round(xup_gbs, 1), "bfgs_iters_per_prox":
@@ -150,12 +258,18 @@ def main():
         "first_step_ms": round(first_ms, 2),
         "setup_s": round(t_setup, 2),
     }
+    if not args.no_spmv:
+        log("spmv microbenchmark")
+        result["spmv"] = spmv_bench(torch, la, mx, with_cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline")
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
         result["cpu_baseline"] = cpu_baseline(mesh, args.admm_iter, threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 
