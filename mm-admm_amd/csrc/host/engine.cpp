@@ -153,6 +153,7 @@ class Engine final : public EngineBase {
       remote_.alloc((size_t)nranks_ * std::max(plan_.maxExport, 1) * D);
     }
     z_.alloc((size_t)nF_ * K);
+    gcache_.alloc((size_t)nF_ * (K + 1));
     u_.alloc((size_t)nF_ * K);
     gs_.alloc((size_t)nF_ * K);
     MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
@@ -162,7 +163,8 @@ class Engine final : public EngineBase {
         for (int i = 0; i < K; ++i) eye[(size_t)s * K * K + i * K + i] = 1.0;
       B_.upload(eye.data(), eye.size(), st_);
     }
-    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 255) / 256, (nP_ + 255) / 256));
+    // prox workgroups can be 64 lanes; node kernels pad their grid to a multiple of 8 (XCD map)
+    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 63) / 64, (nP_ + 255) / 256 + 8));
     partA_.alloc(maxBlocks * kNumPartials);
     partB_.alloc(maxBlocks * kNumPartials);
     resultsCap_ = 0;
@@ -201,6 +203,7 @@ class Engine final : public EngineBase {
     }
     // x = xBar; z = D x; first step: z = D xPrev
     launch_gather_z<D>(m_, stepsTaken_ == 0 ? xPrev_.p : xBar_.p, z_.p, st_);
+    gcacheValid_ = false;  // z was reset
     if (!stepTaken_) MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
     StepScalars sc{prm_.tau, prm_.dt * prm_.dt, w_, dtOverTau};
     int nbx = 0, nbp = 0;
@@ -215,8 +218,9 @@ class Engine final : public EngineBase {
         a0 = nextEvent();
         MMX_HIP(hipEventRecord(a0, st_));
       }
-      launch_prox<D>(m_, !hessComputed_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p, partA_.p, &nbp,
-                     st_);
+      launch_prox<D>(m_, !hessComputed_, gcacheValid_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p,
+                     partA_.p, &nbp, st_);
+      gcacheValid_ = true;  // the prox's last blockGrad left the gradient at the final z
       if (timing) {
         a1 = nextEvent();
         MMX_HIP(hipEventRecord(a1, st_));
@@ -366,7 +370,8 @@ class Engine final : public EngineBase {
     // writes z, u, Bkinv; x is gathered once per node.  x-update reads the incidence CSR,
     // z and u once each, xBar and invdiag, writes x.
     const double nF = nF_, nP = nP_;
-    s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2) + nP * 8.0 * D;
+    // + the gradient cache: K+1 doubles read at entry and written by the last BFGS iteration
+    s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2 + 8.0 * (K + 1) * 2) + nP * 8.0 * D;
     s->xupdate_bytes = 4.0 * (nP + 1) + 4.0 * (D + 1) * nF + 16.0 * K * nF + 8.0 * D * nP * 2 + 8.0 * nP;
   }
 
@@ -441,6 +446,7 @@ class Engine final : public EngineBase {
     m.inc_ptr = incPtr_.p;
     m.inc_off = incOff_.p;
     m.remote = nranks_ > 1 ? remote_.p : nullptr;
+    m.gcache = gcache_.p;
     m.invdiag = invdiag_.p;
     m.Vc = compMesh_ ? Vc_.p : nullptr;
     m.gx = gx_.p;
@@ -450,6 +456,13 @@ class Engine final : public EngineBase {
     m.gnx = grid_.nx;
     m.gny = grid_.ny;
     m.gnz = grid_.nz;
+    // findLimInfMeshPoint divides by m[1] - m[0] (src/MeshUtils.h:47); the kernels use RN(1/h)
+    m.ghx = grid_.gx[1] - grid_.gx[0];
+    m.ghy = grid_.gy[1] - grid_.gy[0];
+    m.ghz = (D == 3) ? grid_.gz[1] - grid_.gz[0] : 1.0;
+    m.grhx = 1.0 / m.ghx;
+    m.grhy = 1.0 / m.ghy;
+    m.grhz = 1.0 / m.ghz;
     for (int i = 0; i < D * D; ++i) m.Ehat[i] = EhatH_[i];
     m.powd = powd_;
     m.w = w_;
@@ -482,7 +495,7 @@ class Engine final : public EngineBase {
   hipStream_t st_ = nullptr;
   DevBuf<int32_t> F_, incPtr_, incOff_;
   DevBuf<uint8_t> sbits_, interior_;
-  DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_;
+  DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, gcache_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
   DevBuf<int32_t> expOff_;
   PartitionPlan plan_;
@@ -491,7 +504,7 @@ class Engine final : public EngineBase {
   int resultsCap_ = 0;
   std::vector<double> hostRes_;
   DeviceMesh<D> m_{};
-  bool hessComputed_ = false, stepTaken_ = false;
+  bool hessComputed_ = false, stepTaken_ = false, gcacheValid_ = false;
   int stepsTaken_ = 0;
   bool timing_ = false;
   std::vector<hipEvent_t> evPool_;

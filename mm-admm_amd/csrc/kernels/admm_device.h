@@ -24,7 +24,12 @@ struct GridView {  // the smoothed monitor grid, rows of D*D doubles
   const double* gz;
   const double* vals;
   int nx, ny, nz;
+  double hx, hy, hz;     // gx[1]-gx[0] etc., the divisors of findLimInfMeshPoint
+  double rhx, rhy, rhz;  // RN(1/h) (div_by experiments; branchy, slower here: DESIGN.md §3)
 };
+
+template <int D>
+constexpr double kRecipD1 = 1.0 / ((double)D + 1.0);  // RN(1/(D+1))
 
 template <int D>
 struct FunctionalConsts {
@@ -114,8 +119,8 @@ __device__ __forceinline__ double trace(const M<D>& a) {
 }
 
 // utils::findLimInfMeshPoint (src/MeshUtils.h:45-54): (int) cast, then uint32 clamp
-__device__ __forceinline__ int findLimInf(double w, const double* m, int size) {
-  uint32_t guess = (uint32_t)(int)((w - m[0]) / (m[1] - m[0]));
+__device__ __forceinline__ int findLimInf(double w, const double* m, int size, double h, double rh) {
+  uint32_t guess = (uint32_t)(int)((w - m[0]) / h);  // h = m[1] - m[0] (host computed, same double)
   if (guess > (uint32_t)(size - 2)) guess = (uint32_t)(size - 2);
   return (int)guess;
 }
@@ -123,8 +128,8 @@ __device__ __forceinline__ int findLimInf(double w, const double* m, int size) {
 // MeshInterpolator<D>::evalMonitorOnGrid (src/MeshInterpolator.cpp:287-342)
 template <int D>
 __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* pnt, M<D>& mv) {
-  const int xInd = findLimInf(pnt[0], g.gx, g.nx + 1);
-  const int yInd = findLimInf(pnt[1], g.gy, g.ny + 1);
+  const int xInd = findLimInf(pnt[0], g.gx, g.nx + 1, g.hx, g.rhx);
+  const int yInd = findLimInf(pnt[1], g.gy, g.ny + 1, g.hy, g.rhy);
   const int nx = g.nx;
   if constexpr (D == 2) {
     const double xm0 = g.gx[xInd], xm1 = g.gx[xInd + 1], ym0 = g.gy[yInd], ym1 = g.gy[yInd + 1];
@@ -141,7 +146,7 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     mv.m[1][0] = c0 * a1.x + c1 * b1.x + c2 * e1.x + c3 * f1.x;
     mv.m[1][1] = c0 * a1.y + c1 * b1.y + c2 * e1.y + c3 * f1.y;
   } else {
-    const int zInd = findLimInf(pnt[2], g.gz, g.nz + 1);
+    const int zInd = findLimInf(pnt[2], g.gz, g.nz + 1, g.hz, g.rhz);
     const double xd = (pnt[0] - g.gx[xInd]) / (g.gx[xInd + 1] - g.gx[xInd]);
     const double yd = (pnt[1] - g.gy[yInd]) / (g.gy[yInd + 1] - g.gy[yInd]);
     const double zd = (pnt[2] - g.gz[zInd]) / (g.gz[zInd + 1] - g.gz[zInd]);
@@ -182,10 +187,12 @@ __device__ __forceinline__ double pow_dp2m1(double x) {
 // AdaptationFunctional<D>::blockGrad (src/AdaptationFunctional.cpp:102-287).
 // Returns the (regularised if REG) energy, sets Igt = |K| G, grad (if GRAD).
 // An inverted element (assert(Edet > 0), line 174) returns NaN and a NaN gradient.
+// ghuang (optional): receives the unregularised gradient |K| dG (K values) and Igt (entry K) --
+// the part of the result that depends on z alone, reused by the next prox at the same z.
 template <int D, bool GRAD, bool REG>
 __device__ __forceinline__ double blockGrad(const GridView<D>& g, const FunctionalConsts<D>& fc,
                                             const double* z, const double* xi, const double* dxpu,
-                                            double* grad, double& Igt) {
+                                            double* grad, double& Igt, double* ghuang = nullptr) {
   constexpr int K = D * (D + 1);
   const double dFact = (D == 2) ? 2.0 : 6.0;
   M<D> mPre[D + 1], Msum;
@@ -217,6 +224,9 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
     if constexpr (GRAD) {
 #pragma unroll
       for (int i = 0; i < K; ++i) grad[i] = nan;
+      if (ghuang)
+#pragma unroll
+        for (int i = 0; i <= K; ++i) ghuang[i] = nan;
     }
     Igt = nan;
     return nan;
@@ -318,6 +328,11 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
     for (int i = 0; i < K; ++i) grad[i] *= absK;
     double Ih = absK * G;
     Igt = Ih;
+    if (ghuang) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) ghuang[i] = grad[i];
+      ghuang[K] = Igt;
+    }
     if constexpr (REG) {
       Ih += 0.5 * fc.w * fc.w * sq;
 #pragma unroll

@@ -20,6 +20,7 @@ struct DeviceMesh {
   const int* inc_off;     // offset s*K + n*D of each local incident slot; -1-r for a slot of another
                           // rank: its D values are row r of `remote` (element partition)
   const double* remote;   // gathered interface-slot values of the other ranks (or nullptr)
+  double* gcache;         // per simplex K+1: unregularised gradient and energy at the current z
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)
   const double* Vc;       // nP x D reference positions (CompMesh) or nullptr
   // monitor grid
@@ -28,6 +29,7 @@ struct DeviceMesh {
   const double* gz;
   const double* gvals;
   int gnx, gny, gnz;
+  double ghx, ghy, ghz, grhx, grhy, grhz;  // grid spacings of findLimInf and RN(1/h)
   // functional constants
   double Ehat[9];
   double powd, w;
@@ -50,8 +52,10 @@ template <int D>
 void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar,
                     const double* z, const double* u, double* x, double* partials, int* nblocks,
                     bool resid, hipStream_t st);
+// useCache: z is unchanged since the previous prox, whose last blockGrad left the unregularised
+// gradient in m.gcache; the entry blockGrad then reduces to adding the regulariser.
 template <int D>
-void launch_prox(const DeviceMesh<D>& m, bool first, double tol, const double* x, double* z,
+void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z,
                  double* u, double* B, double* partials, int* nblocks, hipStream_t st);
 template <int D>
 void launch_energy(const DeviceMesh<D>& m, const double* x, double* partials, int* nblocks,

@@ -13,6 +13,8 @@
 // Build: -ffp-contract=off (no fused multiply-add unless written), see DESIGN.md.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "admm_device.h"
 #include "admm_kernels.h"
 
@@ -20,6 +22,7 @@ namespace mmx {
 
 constexpr int kBlock = 256;
 constexpr int kLdsStride = kBlock + 1;  // padded SoA stride of the LDS Bkinv image
+constexpr int kProxBlock = 256;         // steady-state 2D prox workgroup (measured)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -34,9 +37,9 @@ __device__ __forceinline__ double wave_max(double v) {
 
 // Workgroup reduction of NV values into partials[blockIdx.x * kNumPartials + i].
 // Values 0..3 are summed, 4 is or-ed (as a sum of flags), 5 is a max.
-template <int NV>
-__device__ __forceinline__ void block_partials(double (&v)[NV], double* partials) {
-  __shared__ double red[kBlock / 64][kNumPartials];
+template <int NV, int BS = kBlock>
+__device__ __forceinline__ void block_partials(double (&v)[NV], double* partials, int slot = -1) {
+  __shared__ double red[BS / 64][kNumPartials];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = (i == 5) ? wave_max(v[i]) : wave_sum(v[i]);
@@ -47,10 +50,14 @@ __device__ __forceinline__ void block_partials(double (&v)[NV], double* partials
   __syncthreads();
   if (threadIdx.x < kNumPartials) {
     double s = red[0][threadIdx.x];
-    for (int w = 1; w < kBlock / 64; ++w)
+    for (int w = 1; w < BS / 64; ++w)
       s = (threadIdx.x == 5) ? fmax(s, red[w][threadIdx.x]) : s + red[w][threadIdx.x];
-    partials[(size_t)blockIdx.x * kNumPartials + threadIdx.x] = s;
+    partials[(size_t)(slot < 0 ? (int)blockIdx.x : slot) * kNumPartials + threadIdx.x] = s;
   }
+}
+
+__device__ __forceinline__ int logical_block(int xcd) {
+  return xcd ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
 }
 
 template <int D>
@@ -63,6 +70,12 @@ __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   g.nx = m.gnx;
   g.ny = m.gny;
   g.nz = m.gnz;
+  g.hx = m.ghx;
+  g.hy = m.ghy;
+  g.hz = m.ghz;
+  g.rhx = m.grhx;
+  g.rhy = m.grhy;
+  g.rhz = m.grhz;
   return g;
 }
 
@@ -147,8 +160,8 @@ __global__ void __launch_bounds__(kBlock) k_grad_simplex(DeviceMesh<D> m, const 
 template <int D>
 __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, const double* __restrict__ gs,
                                                      const double* __restrict__ x, double* __restrict__ xPrev,
-                                                     double* __restrict__ xBar, double dt_over_tau) {
-  const int v = blockIdx.x * kBlock + threadIdx.x;
+                                                     double* __restrict__ xBar, double dt_over_tau, int xcd) {
+  const int v = logical_block(xcd) * kBlock + threadIdx.x;
   if (v >= m.nP) return;
   double xv[D], xb[D];
 #pragma unroll
@@ -184,8 +197,9 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
                                                      const double* __restrict__ xBar,
                                                      const double* __restrict__ z,
                                                      const double* __restrict__ u, double* __restrict__ x,
-                                                     double* __restrict__ partials) {
-  const int v = blockIdx.x * kBlock + threadIdx.x;
+                                                     double* __restrict__ partials, int xcd) {
+  const int lb = logical_block(xcd);
+  const int v = lb * kBlock + threadIdx.x;
   double pv[3] = {0, 0, 0};
   if (v < m.nP) {
     double acc[D];
@@ -224,7 +238,7 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
       pv[2] = r2;
     }
   }
-  if constexpr (RESID) block_partials<3>(pv, partials);
+  if constexpr (RESID) block_partials<3>(pv, partials, lb);
 }
 
 // k x k inverse: unblocked partial-pivot LU + substitution (mirrors the oracle's restatement
@@ -287,11 +301,11 @@ struct RegB {
 };
 // LDS image: a scheduling fence per matrix row keeps one row live at a time (otherwise the
 // scheduler hoists all K*K reads and the kernel spills)
-template <int K>
+template <int K, int STRIDE = kLdsStride>
 struct LdsB {
   static constexpr bool kRowFence = true;
-  double* base;  // &lds[tid], entries strided by kLdsStride
-  __device__ __forceinline__ double& operator()(int i, int j) const { return base[(i * K + j) * kLdsStride]; }
+  double* base;  // &lds[tid], entries strided by STRIDE
+  __device__ __forceinline__ double& operator()(int i, int j) const { return base[(i * K + j) * STRIDE]; }
 };
 #define MMX_ROW_FENCE(BA) \
   if constexpr (BA::kRowFence) __builtin_amdgcn_sched_barrier(0)
@@ -301,7 +315,7 @@ struct LdsB {
 template <int D, class BA>
 __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g, const FunctionalConsts<D>& fc,
                                                double* z, const double* xi, const double* dx, double* G,
-                                               unsigned fixedBits, double tol, bool& bad) {
+                                               unsigned fixedBits, double tol, bool& bad, double* gcache) {
   constexpr int K = D * (D + 1);
   int iter;
   for (iter = 0; iter < 50; iter++) {
@@ -319,7 +333,7 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
     for (int i = 0; i < K; ++i) z[i] += pk[i];
     double G1[K], Igt;
     {
-      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G1, Igt);
+      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G1, Igt, gcache);
       bad |= (e != e);
     }
     zeroFixed<D>(G1, fixedBits);
@@ -349,6 +363,9 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
     }
     MMX_ROW_FENCE(BA);
     const double c1 = (c2 + yBy) / cr_pow_2(c2);
+#ifdef MMX_BFGS_DIVBY
+    const double rc2 = 1.0 / c2;  // the K*K divisions by c2 below: div_by, bit-identical
+#endif
     // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -361,7 +378,11 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
         double by = row[0] * (yk[0] * pk[j]);
 #pragma unroll
         for (int q = 1; q < K; ++q) by += row[q] * (yk[q] * pk[j]);
+#ifdef MMX_BFGS_DIVBY
+        nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - div_by(by, c2, rc2)) - div_by(pk[i] * yB[j], c2, rc2));
+#else
         nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - by / c2) - (pk[i] * yB[j]) / c2);
+#endif
       }
 #pragma unroll
       for (int j = 0; j < K; ++j) B(i, j) = nrow[j];
@@ -374,12 +395,34 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
   return (iter == 50) ? 50 : iter + 1;
 }
 
+// Entry gradient of the prox: the full regularised blockGrad, or -- when z is unchanged since the
+// previous prox -- its cached unregularised part plus the regulariser, added exactly as blockGrad
+// adds it (bit-identical).
+template <int D>
+__device__ __forceinline__ void entry_grad(const GridView<D>& g, const FunctionalConsts<D>& fc, const double* z,
+                                           const double* xi, const double* dx, const double* cache, bool useCache,
+                                           double* G, double& Igt, bool& bad) {
+  constexpr int K = D * (D + 1);
+  if (useCache) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) G[i] = cache[i];
+    Igt = cache[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) G[i] += fc.w * fc.w * (-dx[i] + z[i]);
+    bad |= (Igt != Igt);
+  } else {
+    const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G, Igt);
+    bad |= (e != e);
+  }
+}
+
 // The prox (src/Mesh.cpp:930-994 / 777-872), one lane per simplex.  FIRST = the first prox of
 // the run, which builds the finite-difference Hessian and inverts it.
 template <int D, bool FIRST>
 __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                   double* __restrict__ zg, double* __restrict__ ug,
-                                                  double* __restrict__ Bg, double* __restrict__ partials) {
+                                                  double* __restrict__ Bg, double* __restrict__ partials,
+                                                  int useCache) {
   constexpr int K = D * (D + 1);
   const int s = blockIdx.x * kBlock + threadIdx.x;
   double pv[6] = {0, 0, 0, 0, 0, 0};
@@ -411,10 +454,8 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
     double G[K], G1[K], Igt;
     bool bad = false;
     (void)G1;
-    {
-      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G, Igt);
-      bad |= (e != e);
-    }
+    double* gc = m.gcache + (size_t)s * (K + 1);
+    entry_grad<D>(g, fc, z, xi, dx, gc, !FIRST && useCache, G, Igt, bad);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
     if constexpr (FIRST) {
@@ -439,7 +480,7 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
       invertK<K>(B);
     }
     RegB<K> Bacc{B};
-    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad);
+    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc);
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -465,24 +506,30 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
 // back with 16-byte-per-lane fully coalesced accesses and held in LDS as a padded
 // structure-of-arrays image [K*K][257], so each lane's BFGS reads its own matrix
 // conflict-free and the registers it frees give two waves per SIMD.
-template <int D>
-__global__ void __launch_bounds__(kBlock, 2) k_prox_lds(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+template <int D, int BS>
+__global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                         double* __restrict__ zg, double* __restrict__ ug,
-                                                        double* __restrict__ Bg, double* __restrict__ partials) {
+                                                        double* __restrict__ Bg, double* __restrict__ partials,
+                                                        int useCache) {
   constexpr int K = D * (D + 1), KK = K * K;
-  __shared__ __attribute__((aligned(16))) double lds[KK * kLdsStride];
+  __shared__ __attribute__((aligned(16))) double lds[KK * (BS + 1)];
   const int tid = threadIdx.x;
-  const int s0 = blockIdx.x * kBlock;
-  const int nIn = min(kBlock, m.nF - s0);
+  const int s0 = blockIdx.x * BS;
+  const int nIn = min(BS, m.nF - s0);
   double* chunk = Bg + (size_t)s0 * KK;
   const int tot = nIn * KK;  // even: K*K is even
 #pragma unroll 4
-  for (int e = tid * 2; e < tot; e += kBlock * 2) {
+  for (int e = tid * 2; e < tot; e += BS * 2) {
+#ifdef MMX_EXP_NOB  // experiment: no Bkinv traffic (identity), measures everything else
+    const int ea = e / KK, eb = (e + 1) / KK;
+    const double2 v = make_double2(((e - ea * KK) % (K + 1)) == 0 ? 1.0 : 0.0, ((e + 1 - eb * KK) % (K + 1)) == 0 ? 1.0 : 0.0);
+#else
     const double2 v = *reinterpret_cast<const double2*>(chunk + e);
+#endif
     const int sa = e / KK, ka = e - sa * KK;
     const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
-    lds[ka * kLdsStride + sa] = v.x;
-    lds[kb * kLdsStride + sb] = v.y;
+    lds[ka * (BS + 1) + sa] = v.x;
+    lds[kb * (BS + 1) + sb] = v.y;
   }
   __syncthreads();
   double pv[6] = {0, 0, 0, 0, 0, 0};
@@ -506,14 +553,12 @@ __global__ void __launch_bounds__(kBlock, 2) k_prox_lds(DeviceMesh<D> m, double 
     }
     double G[K], Igt;
     bool bad = false;
-    {
-      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G, Igt);
-      bad |= (e != e);
-    }
+    double* gc = m.gcache + (size_t)s * (K + 1);
+    entry_grad<D>(g, fc, z, xi, dx, gc, useCache != 0, G, Igt, bad);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
-    LdsB<K> Bacc{lds + tid};
-    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad);
+    LdsB<K, BS + 1> Bacc{lds + tid};
+    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc);
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -533,15 +578,19 @@ __global__ void __launch_bounds__(kBlock, 2) k_prox_lds(DeviceMesh<D> m, double 
   }
   __syncthreads();
 #pragma unroll 4
-  for (int e = tid * 2; e < tot; e += kBlock * 2) {
+  for (int e = tid * 2; e < tot; e += BS * 2) {
     const int sa = e / KK, ka = e - sa * KK;
     const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
     double2 v;
-    v.x = lds[ka * kLdsStride + sa];
-    v.y = lds[kb * kLdsStride + sb];
+    v.x = lds[ka * (BS + 1) + sa];
+    v.y = lds[kb * (BS + 1) + sb];
+#ifndef MMX_EXP_NOB
     *reinterpret_cast<double2*>(chunk + e) = v;
+#else
+    if (v.x == 12345.0) chunk[e] = v.y;  // keep the LDS reads alive
+#endif
   }
-  block_partials<6>(pv, partials);
+  block_partials<6, BS>(pv, partials);
 }
 
 // Mesh::computeEnergy (src/Mesh.cpp:496-530) on positions x
@@ -567,8 +616,8 @@ __global__ void __launch_bounds__(kBlock) k_energy(DeviceMesh<D> m, const double
 // Mesh::eulerStepMod scatter (src/Mesh.cpp:566-572): INTERIOR nodes only; x -= (dt/tau) grad
 template <int D>
 __global__ void __launch_bounds__(kBlock) k_euler_apply(DeviceMesh<D> m, const double* __restrict__ gs,
-                                                         double* __restrict__ x, double dt_over_tau) {
-  const int v = blockIdx.x * kBlock + threadIdx.x;
+                                                         double* __restrict__ x, double dt_over_tau, int xcd) {
+  const int v = logical_block(xcd) * kBlock + threadIdx.x;
   if (v >= m.nP) return;
   double g[D];
 #pragma unroll
@@ -660,6 +709,13 @@ __global__ void k_debug_blockgrad(DeviceMesh<D> m, int s, const double* __restri
 __global__ void k_devmath(int op, int n, const double* __restrict__ in, double* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (op == 5) {  // quotient pairs (x, c) -> RN(x/c) by div_by
+    if (2 * i + 1 < n) {
+      const double xx = in[2 * i], c = in[2 * i + 1];
+      out[i] = div_by(xx, c, 1.0 / c);
+    }
+    return;
+  }
   const double x = in[i];
   double r;
   switch (op) {
@@ -674,6 +730,17 @@ __global__ void k_devmath(int op, int n, const double* __restrict__ in, double* 
 
 // ---------------------------------------------------------------------------------------
 static inline int nblk(int n) { return (n + kBlock - 1) / kBlock; }
+// node kernels: grid padded to a multiple of the 8 XCDs, logical blocks dealt in contiguous runs
+// per XCD (blocks b and b+8 share an XCD, MI355X_MICROARCH.md §Workgroup dispatch), so the z/u
+// lines a run of nodes shares stay in one L2.  MMX_XCD_MAP=0 restores the identity mapping.
+static int xcd_map() {
+  static int v = [] {
+    const char* e = getenv("MMX_XCD_MAP");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+static inline int nblk_xcd(int n) { return xcd_map() ? (nblk(n) + 7) / 8 * 8 : nblk(n); }
 
 template <int D>
 void launch_gather_z(const DeviceMesh<D>& m, const double* x, double* z, hipStream_t st) {
@@ -692,33 +759,60 @@ template <int D>
 void launch_predict(const DeviceMesh<D>& m, int mode, const double* gs, double* x, double* xPrev,
                     double* xBar, double dt_over_tau, hipStream_t st) {
   if (m.nP == 0) return;
-  hipLaunchKernelGGL(k_predict<D>, dim3(nblk(m.nP)), dim3(kBlock), 0, st, m, mode, gs, x, xPrev, xBar,
-                     dt_over_tau);
+  hipLaunchKernelGGL(k_predict<D>, dim3(nblk_xcd(m.nP)), dim3(kBlock), 0, st, m, mode, gs, x, xPrev, xBar,
+                     dt_over_tau, xcd_map());
 }
 template <int D>
 void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar, const double* z,
                     const double* u, double* x, double* partials, int* nblocks, bool resid, hipStream_t st) {
-  *nblocks = nblk(m.nP);
+  *nblocks = nblk_xcd(m.nP);
   if (m.nP == 0) return;
   if (resid)
     hipLaunchKernelGGL((k_xupdate<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
-                       partials);
+                       partials, xcd_map());
   else
     hipLaunchKernelGGL((k_xupdate<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
-                       partials);
+                       partials, xcd_map());
 }
+// reuse of the previous prox's last gradient at the prox entry (MMX_GRAD_CACHE=0 disables)
+static int cache_enabled() {
+  static int v = [] {
+    const char* e = getenv("MMX_GRAD_CACHE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+// workgroup size of the steady-state 2D prox (MMX_PROX_BLOCK = 64 | 128 | 256 overrides)
+static int prox_block() {
+  static int b = [] {
+    const char* e = getenv("MMX_PROX_BLOCK");
+    const int v = e ? atoi(e) : 0;
+    return (v == 64 || v == 128 || v == 256) ? v : kProxBlock;
+  }();
+  return b;
+}
+
 template <int D>
-void launch_prox(const DeviceMesh<D>& m, bool first, double tol, const double* x, double* z, double* u,
+void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z, double* u,
                  double* B, double* partials, int* nblocks, hipStream_t st) {
+  const int uc = (useCache && cache_enabled()) ? 1 : 0;
   *nblocks = nblk(m.nF);
   if (m.nF == 0) return;
   if (first) {
-    hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
+    hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials, 0);
   } else {
-    if constexpr (D == 2)
-      hipLaunchKernelGGL((k_prox_lds<D>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
-    else
-      hipLaunchKernelGGL((k_prox<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials);
+    if constexpr (D == 2) {
+      const int bs = prox_block();
+      *nblocks = (m.nF + bs - 1) / bs;
+      if (bs == 64)
+        hipLaunchKernelGGL((k_prox_lds<D, 64>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, B, partials, uc);
+      else if (bs == 128)
+        hipLaunchKernelGGL((k_prox_lds<D, 128>), dim3(*nblocks), dim3(128), 0, st, m, tol, x, z, u, B, partials, uc);
+      else
+        hipLaunchKernelGGL((k_prox_lds<D, 256>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, B, partials, uc);
+    } else {
+      hipLaunchKernelGGL((k_prox<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials, uc);
+    }
   }
 }
 template <int D>
@@ -731,7 +825,7 @@ template <int D>
 void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
                         hipStream_t st) {
   if (m.nP == 0) return;
-  hipLaunchKernelGGL(k_euler_apply<D>, dim3(nblk(m.nP)), dim3(kBlock), 0, st, m, gs, x, dt_over_tau);
+  hipLaunchKernelGGL(k_euler_apply<D>, dim3(nblk_xcd(m.nP)), dim3(kBlock), 0, st, m, gs, x, dt_over_tau, xcd_map());
 }
 void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st) {
   hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, st, partials, nblocks, out);
@@ -770,7 +864,7 @@ void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st
                                   double, hipStream_t);                                                 \
   template void launch_xupdate<D>(const DeviceMesh<D>&, const StepScalars&, const double*, const double*, \
                                   const double*, double*, double*, int*, bool, hipStream_t);            \
-  template void launch_prox<D>(const DeviceMesh<D>&, bool, double, const double*, double*, double*,      \
+  template void launch_prox<D>(const DeviceMesh<D>&, bool, bool, double, const double*, double*, double*,      \
                                double*, double*, int*, hipStream_t);                                    \
   template void launch_energy<D>(const DeviceMesh<D>&, const double*, double*, int*, hipStream_t);       \
   template void launch_euler_apply<D>(const DeviceMesh<D>&, const double*, double*, double, hipStream_t);

@@ -30,6 +30,18 @@ namespace mmx {
 MMX_HD double cr_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 MMX_HD double cr_sqrt(double x) { return __builtin_sqrt(x); }
 
+// RN(x / c) from rc = RN(1 / c) without a division (Markstein: with rc correctly rounded and
+// q = RN(x rc) within one ulp of x/c, the residual r = x - c q is exact (FMA) and RN(q + r rc) is
+// the correctly rounded quotient).  Zero, tiny, huge and non-finite operands take the division.
+MMX_HD double div_by(double x, double c, double rc) {
+  const double q = x * rc;
+  const double aq = std::fabs(q), ac = std::fabs(c);
+  if (!(aq > 0x1p-900 && aq < 0x1p900 && ac > 0x1p-900 && ac < 0x1p900)) return x / c;
+  const double r = cr_fma(-q, c, x);
+  return cr_fma(r, rc, q);
+}
+constexpr double kRecip3 = 1.0 / 3.0;  // RN(1/3), for the divisions by D + 1 = 3
+
 // argument ranges in which the exact fallback (x^p and m^q as expansions) cannot over- or
 // underflow; outside them (never met by the functional) the device libm pow is used.
 MMX_HD bool cr_in(double x, double lo, double hi) { return x > lo && x < hi; }
@@ -272,7 +284,11 @@ MMX_HD double cr_round(double x, int num, int den, double hi, double lo) {
   const double half = std::fabs(nb - h) * 0.5;
   const double dist = half - std::fabs(l);  // distance of the dd value to the midpoint
   if (dist > std::fabs(h) * 0x1p-95) return h;
+#ifdef MMX_CR_NO_RESOLVE  // performance experiments only: skips the exact tie decision
+  return h;
+#else
   return cr_resolve(x, num, den, h, dir);
+#endif
 }
 
 // sqrt(x) = s + e, |error| < 2^-104 |s|

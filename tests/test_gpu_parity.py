@@ -136,3 +136,27 @@ def test_inverted_element_reported():
     with pytest.raises(mx.InvertedElementError):
         for _ in range(3):
             G.step(10, -1.0)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_device_division_by_reciprocal_is_correctly_rounded(seed):
+    """div_by (crmath.h): RN(x/c) from RN(1/c) + one FMA correction, used for the BFGS update's
+    72 divisions by c2 and the divisions by D+1 and by the grid spacing -- bit-identical to IEEE
+    division on random, wide-range and near-midpoint quotients."""
+    import mmadmm_amd as mx
+    rng = np.random.default_rng(seed)
+    n = 1 << 21
+    c = rng.uniform(1, 2, n) * np.exp2(rng.integers(-300, 300, n))
+    c[: n // 4] = rng.uniform(1e-12, 1e-3, n // 4)  # c2 = p.y magnitudes of the prox
+    x = rng.uniform(-2, 2, n) * np.exp2(rng.integers(-300, 300, n))
+    # near-midpoint quotients: x = RN(c * (q + ulp(q)/2 * (1 + tiny)))
+    q = rng.uniform(1, 2, n // 4)
+    half = np.spacing(q) / 2
+    x[n // 2: n // 2 + n // 4] = c[n // 2: n // 2 + n // 4] * (q + half * (1 + rng.uniform(-1e-6, 1e-6, n // 4)))
+    x[-1000:] = 0.0
+    x[-500:] = -0.0
+    pairs = np.empty(2 * n)
+    pairs[0::2], pairs[1::2] = x, c
+    out = mx.devmath(5, pairs)[:n]
+    ref = x / c
+    assert np.array_equal(out.view(np.int64), ref.view(np.int64))
