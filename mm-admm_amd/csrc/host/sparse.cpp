@@ -147,6 +147,7 @@ struct SparseMatrix {
   int level = -1;
   std::vector<int> iaf, jaf, dgRel;
   DevBuf<int> d_iaf, d_jaf, d_dg, d_amap, d_permf, d_permb;
+  DevBuf<int2> d_piv;
   int nchf = 0, nchb = 0, nlevf = 0, nlevb = 0;
   DevBuf<double> d_af;
   DevBuf<unsigned> d_flags, d_ctl;  // ctl: 8 tickets, err, pad (16-byte multiple)
@@ -232,6 +233,12 @@ struct SparseMatrix {
     d_dg.upload(dg.data(), dg.size(), st);
     d_amap.upload(amap.data(), std::max<size_t>(amap.size(), 1), st);
     d_af.alloc(std::max<size_t>(jaf.size(), 1));
+    {  // pivot-row upper ranges of every lower entry (the factor's dependent loads, precomputed)
+      std::vector<int2> pv(std::max<size_t>(jaf.size(), 1), make_int2(0, 0));
+      for (int i = 0; i < n; ++i)
+        for (int k = iaf[i]; k < dg[i]; ++k) pv[k] = make_int2(dg[jaf[k]], iaf[jaf[k] + 1]);
+      d_piv.upload(pv.data(), pv.size(), st);
+    }
     // level schedules of the lower (forward sweep, factor) and upper (backward sweep) factor
     std::vector<int> lev(n);
     auto schedule = [&](bool fwd, DevBuf<int>& out, int& nch, int& nlev) {
@@ -296,8 +303,8 @@ struct SparseMatrix {
       fepoch = 1;
     }
     begin(2);
-    launch_ilu_factor(d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_permf.p, nchf, d_af.p, d_flags.p,
-                      fepoch, tickets(), errw(), st);
+    launch_ilu_factor(d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_permf.p, nchf, d_af.p,
+                      d_flags.p, fepoch, tickets(), errw(), st);
     MMX_HIP(hipGetLastError());
     const float ms = end(2);
     stats.factors++;

@@ -38,9 +38,10 @@ void launch_spmv(int epi, int nblk, const int* rowblk, const int* ia, const int*
 
 // ILU numeric factor in the factor pattern (iaf/jaf/dg); amap maps A's entries into it.  perm: rows
 // in forward-level order, padded with -1 to whole chunks of kSweepRows.
+// piv[k] for a lower entry k of row i: {dg[id], iaf[id+1]} of its pivot row id = jaf[k].
 void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
-                       const int* dg, const int* perm, int nchunks, double* af, unsigned* flags, unsigned epoch,
-                       unsigned* ticket, unsigned* err, hipStream_t st);
+                       const int* dg, const int2* piv, const int* perm, int nchunks, double* af, unsigned* flags,
+                       unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
 
 // Sweep over the rows of perm (forward or backward level order).  Forward: unit L into granules
 // gout, right-hand side per pro (0: src; 1: p = res + beta (p - omega avbar); 2: s = res - alpha

@@ -194,9 +194,10 @@ __device__ __forceinline__ void backoff(unsigned& spins, bool progressed, unsign
 __global__ void __launch_bounds__(kSweepRows) k_ilu_factor(const int* __restrict__ ia, const int* __restrict__ ja,
                                                           const double* __restrict__ a, const int* __restrict__ amap,
                                                           const int* __restrict__ iaf, const int* __restrict__ jaf,
-                                                          const int* __restrict__ dg, const int* __restrict__ perm,
-                                                          int nchunks, double* af, unsigned* flags, unsigned epoch,
-                                                          unsigned* ticket, unsigned* err) {
+                                                          const int* __restrict__ dg, const int2* __restrict__ piv,
+                                                          const int* __restrict__ perm, int nchunks, double* af,
+                                                          unsigned* flags, unsigned epoch, unsigned* ticket,
+                                                          unsigned* err) {
   const int lane = (int)threadIdx.x;
   bool give_up = false;
   while (!give_up) {
@@ -204,15 +205,19 @@ __global__ void __launch_bounds__(kSweepRows) k_ilu_factor(const int* __restrict
     if (t >= nchunks) break;
     const int i = perm[(size_t)t * kSweepRows + lane];
     const bool valid = i >= 0;
-    int kk = 0, kd = 0, kb = 0, ke = 0;
+    int kc = 0, kd = 0, kb = 0, ke = 0;
     if (valid) {
       kb = iaf[i];
       kd = dg[i];
       ke = iaf[i + 1];
       for (int k = kb; k < ke; ++k) af[k] = 0.0;
       for (int ii = ia[i]; ii < ia[i + 1]; ++ii) af[amap[ii]] = a[ii];
-      kk = kb;
+      kc = kb;
     }
+    // eliminate the lower entries in ascending order, each as soon as its pivot row is published
+    // (rows finishing late are usually the last entries, so earlier ones overlap the wait); the
+    // pivot-row range comes from piv (host-built) together with the flag poll
+    int kk = kc;
     bool done = !valid;
     unsigned spins = 0;
     while (true) {
@@ -220,15 +225,31 @@ __global__ void __launch_bounds__(kSweepRows) k_ilu_factor(const int* __restrict
       if (!done) {
         while (kk < kd) {
           const int id = jaf[kk];
+          const int2 pv = piv[kk];
           if (__hip_atomic_load(&flags[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) break;
           prog = true;
-          const int ub = dg[id], uend = iaf[id + 1];
-          const double mult = af[kk] / ld_agent(&af[ub]);
+          const int ub = pv.x, uend = pv.y;
+          const double pivot = ld_agent(&af[ub]);
+          int jj[kFactorBatch];
+          double uu[kFactorBatch];
+          const int m0 = (uend - ub - 1 < kFactorBatch) ? uend - ub - 1 : kFactorBatch;
+#pragma unroll
+          for (int q = 0; q < kFactorBatch; ++q)
+            if (q < m0) {
+              jj[q] = jaf[ub + 1 + q];
+              uu[q] = ld_agent(&af[ub + 1 + q]);
+            }
+          const double mult = af[kk] / pivot;
           af[kk] = mult;
           int p = kk + 1;
-          for (int c0 = ub + 1; c0 < uend; c0 += kFactorBatch) {
-            int jj[kFactorBatch];
-            double uu[kFactorBatch];
+#pragma unroll
+          for (int q = 0; q < kFactorBatch; ++q)
+            if (q < m0) {
+              const int idd = jj[q];
+              while (p < ke && jaf[p] < idd) ++p;
+              if (p < ke && jaf[p] == idd) af[p] = af[p] - mult * uu[q];
+            }
+          for (int c0 = ub + 1 + kFactorBatch; c0 < uend; c0 += kFactorBatch) {  // long pivot rows
 #pragma unroll
             for (int q = 0; q < kFactorBatch; ++q)
               if (c0 + q < uend) {
@@ -474,12 +495,12 @@ void launch_spmv(int epi, int nblk, const int* rowblk, const int* ia, const int*
 }
 
 void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
-                       const int* dg, const int* perm, int nchunks, double* af, unsigned* flags, unsigned epoch,
-                       unsigned* ticket, unsigned* err, hipStream_t st) {
+                       const int* dg, const int2* piv, const int* perm, int nchunks, double* af, unsigned* flags,
+                       unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st) {
   if (nchunks <= 0) return;
   const int grid = nchunks < sweep_grid() ? nchunks : sweep_grid();
-  hipLaunchKernelGGL(k_ilu_factor, dim3(grid), dim3(kSweepRows), 0, st, ia, ja, a, amap, iaf, jaf, dg, perm, nchunks, af,
-                     flags, epoch, ticket, err);
+  hipLaunchKernelGGL(k_ilu_factor, dim3(grid), dim3(kSweepRows), 0, st, ia, ja, a, amap, iaf, jaf, dg, piv, perm, nchunks,
+                     af, flags, epoch, ticket, err);
 }
 
 void launch_sweep(bool fwd, int pro, const int* iaf, const int* jaf, const int* dg, const double* af, const int* perm,

@@ -1,0 +1,100 @@
+"""The experiment driver (mm-admm_amd/bin/mmadmm_run): the reference's command
+line (`mesh.exe <testName> <method> <threads>`), config files and outputs.  Configs are written
+here with the keys and values of the reference's Experiments/InputFiles/*.json (data only); the
+GPU runs are checked against the reference's committed results (tests/golden/)."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from test_oracle_pins import SIX_DIGITS, ih0
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RUN = os.path.join(ROOT, "mm-admm_amd", "bin", "mmadmm_run")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+MONITOR210 = {"TestType": "SquareGrid", "Dim": 2, "MonType": 3, "Method": 0, "CompMesh": False, "BoundaryType": 1,
+              "GradUse": False, "nSteps": 1000, "AdmmIter": 10, "DtTol": 1e-4, "dt": 0.025, "tau": 0.5,
+              "rho": 1000, "w": 3.53553390593, "nx": 10, "ny": 10, "xa": 0, "xb": 1, "ya": 0, "yb": 1}
+MONITOR340 = {"TestType": "FromFile", "MaskFile": "./Experiments/Results/BaseCircle/CircleEx24mask.txt",
+              "PntsFile": "./Experiments/Results/BaseCircle/CircleEx24points.txt",
+              "TrianglesFile": "./Experiments/Results/BaseCircle/CircleEx24triangles.txt", "Dim": 2, "MonType": 5,
+              "Method": 0, "CompMesh": False, "BoundaryType": 1, "GradUse": False, "nSteps": 10000,
+              "AdmmIter": 100, "DtTol": 1e-5, "dt": 0.05, "tau": 1e-1, "rho": 5, "w": 3.53553390593, "nx": 40,
+              "ny": 40, "xa": 0, "xb": 1, "ya": 0, "yb": 1}
+
+
+def _root(tmp_path, name, cfg):
+    inp = tmp_path / "Experiments" / "InputFiles"
+    inp.mkdir(parents=True)
+    (inp / f"{name}.json").write_text(json.dumps(cfg, indent=4))
+    base = tmp_path / "Experiments" / "Results" / "BaseCircle"
+    base.mkdir(parents=True)
+    for f in os.listdir(os.path.join(GOLDEN, "BaseCircle")):
+        shutil.copy(os.path.join(GOLDEN, "BaseCircle", f), base / f)
+    return tmp_path
+
+
+def _run(root, name, *args):
+    return subprocess.run([RUN, name, *args, "--root", str(root)], capture_output=True, text=True, timeout=900)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    if not os.path.exists(RUN):
+        pytest.fail("mmadmm_run not built (make -C mm-admm_amd)")
+
+
+def test_dry_run_square_grid(tmp_path):
+    r = _run(_root(tmp_path, "Monitor210", MONITOR210), "Monitor210", "0", "1", "--dry-run")
+    assert r.returncode == 0, r.stderr
+    assert "size of Vp 221, 2" in r.stdout and "size of F 400, 3" in r.stdout
+
+
+def test_dry_run_from_file(tmp_path):
+    r = _run(_root(tmp_path, "Monitor340", MONITOR340), "Monitor340", "0", "1", "--dry-run")
+    assert r.returncode == 0, r.stderr
+    assert "size of F 4015, 3" in r.stdout
+
+
+def test_unsupported_is_reported(tmp_path):
+    cfg = dict(MONITOR210, TestType="Shoulder")
+    r = _run(_root(tmp_path, "Sh", cfg), "Sh", "0", "1", "--dry-run")
+    assert r.returncode == 2 and "not available" in r.stderr
+    r = _run(_root(tmp_path / "m2", "Monitor210", MONITOR210), "Monitor210", "2", "1", "--dry-run")
+    assert r.returncode == 2 and "backward Euler" in r.stderr
+
+
+def _ih(path):
+    return np.loadtxt(path, delimiter=",")
+
+
+@pytest.mark.gpu
+def test_monitor210_matches_reference_results(tmp_path):
+    root = _root(tmp_path, "Monitor210", MONITOR210)
+    r = _run(root, "Monitor210", "0", "1")
+    assert r.returncode == 0, r.stderr
+    out = root / "Experiments" / "Results" / "Monitor210"
+    ours = _ih(out / "Ih0.txt")[:, 1]
+    ref = ih0("Monitor210")
+    assert len(ours) == len(ref) and (np.abs(ours - ref) / np.abs(ref)).max() < SIX_DIGITS
+    assert os.path.exists(out / "IhPara1.txt")
+    P = np.loadtxt(out / "points.txt", delimiter=",")
+    Pref = np.loadtxt(os.path.join(GOLDEN, "Monitor210", "points.txt"), delimiter=",")
+    assert np.abs(P - Pref).max() < 5e-6 * np.abs(Pref).max()
+    T = np.loadtxt(out / "triangles.txt", delimiter=",").astype(int)
+    Tref = np.loadtxt(os.path.join(GOLDEN, "Monitor210", "triangles.txt"), delimiter=",").astype(int)
+    assert np.array_equal(T, Tref)
+
+
+@pytest.mark.gpu
+def test_monitor340_from_file_matches_reference_trace(tmp_path):
+    root = _root(tmp_path, "Monitor340", MONITOR340)
+    r = _run(root, "Monitor340", "0", "1")
+    assert r.returncode == 0, r.stderr
+    ours = _ih(root / "Experiments" / "Results" / "Monitor340" / "Ih0.txt")[:, 1]
+    ref = ih0("Monitor340")
+    assert len(ours) == len(ref) and (np.abs(ours - ref) / np.abs(ref)).max() < SIX_DIGITS
