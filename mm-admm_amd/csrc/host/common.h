@@ -81,6 +81,7 @@ struct MeshBuf {
 // Smoothed monitor grid (src/MeshInterpolator.cpp:68-130, 166-259, 366-404)
 struct HostGrid {
   int nx = 0, ny = 0, nz = 0;
+  double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};  // linspace end points (bounding box)
   std::vector<double> gx, gy, gz;
   std::vector<double> vals;  // rows x dim*dim
 };

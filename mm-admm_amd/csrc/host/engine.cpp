@@ -234,8 +234,8 @@ class Engine final : public EngineBase {
         MMX_HIP(hipEventRecord(b1, st_));
         timed_.push_back({a0, a1, b1});
       }
-      launch_reduce_partials(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, st_);
-      launch_reduce_partials(partB_.p, nbx, results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
+      launch_reduce_partials2(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, partB_.p, nbx,
+                              results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
       done = i + 1;
       if (early) {
         std::vector<double> rv;
@@ -463,6 +463,19 @@ class Engine final : public EngineBase {
     m.grhx = 1.0 / m.ghx;
     m.grhy = 1.0 / m.ghy;
     m.grhz = 1.0 / m.ghz;
+    // linspace(xa, xb, ns): g[i] = xa + i*(xb - xa)/ns (src/MeshUtils.h:24-29), recomputed in-kernel
+    const int ns[3] = {grid_.nx, grid_.ny, grid_.nz};
+    double* A[3] = {&m.gax, &m.gay, &m.gaz};
+    double* SP[3] = {&m.gspx, &m.gspy, &m.gspz};
+    double* NS[3] = {&m.gnsx, &m.gnsy, &m.gnsz};
+    double* RNS[3] = {&m.grnsx, &m.grnsy, &m.grnsz};
+    for (int d = 0; d < 3; ++d) {
+      const bool on = d < D;
+      *A[d] = on ? grid_.lo[d] : 0.0;
+      *SP[d] = on ? grid_.hi[d] - grid_.lo[d] : 0.0;
+      *NS[d] = on ? (double)ns[d] : 1.0;
+      *RNS[d] = 1.0 / *NS[d];
+    }
     for (int i = 0; i < D * D; ++i) m.Ehat[i] = EhatH_[i];
     m.powd = powd_;
     m.w = w_;

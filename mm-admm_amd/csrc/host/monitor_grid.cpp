@@ -119,6 +119,10 @@ void buildGrid(const double* X, int nP, mmadmm_monitor_fn fn, void* user, HostGr
       mn[d] = (v < mn[d]) ? v : mn[d];
       mx[d] = (v > mx[d]) ? v : mx[d];
     }
+  for (int d = 0; d < D; ++d) {
+    g.lo[d] = mn[d];
+    g.hi[d] = mx[d];
+  }
   linspace(mn[0], mx[0], g.nx, g.gx);
   linspace(mn[1], mx[1], g.ny, g.gy);
   if (D == 3) linspace(mn[2], mx[2], g.nz, g.gz);

@@ -25,8 +25,17 @@ struct GridView {  // the smoothed monitor grid, rows of D*D doubles
   const double* vals;
   int nx, ny, nz;
   double hx, hy, hz;     // gx[1]-gx[0] etc., the divisors of findLimInfMeshPoint
-  double rhx, rhy, rhz;  // RN(1/h) (div_by experiments; branchy, slower here: DESIGN.md §3)
+  double rhx, rhy, rhz;  // RN(1/h)
+  // linspace (src/MeshUtils.h:24-29) parameters: g[i] = a + (i * span) / ns, recomputed on the
+  // device instead of loaded (saves a dependent load before every monitor gather)
+  double ax, ay, az, spx, spy, spz, nsx, nsy, nsz, rnsx, rnsy, rnsz;
 };
+
+// grid coordinate i of an axis, bit-identical to the host linspace (div_nr is exact here:
+// i*span >= 0 and ns >= 1 are normal or zero)
+__device__ __forceinline__ double gridCoord(double a, double span, double ns, double rns, int i) {
+  return a + div_nr(((double)i) * span, ns, rns);
+}
 
 template <int D>
 constexpr double kRecipD1 = 1.0 / ((double)D + 1.0);  // RN(1/(D+1))
@@ -119,8 +128,9 @@ __device__ __forceinline__ double trace(const M<D>& a) {
 }
 
 // utils::findLimInfMeshPoint (src/MeshUtils.h:45-54): (int) cast, then uint32 clamp
-__device__ __forceinline__ int findLimInf(double w, const double* m, int size, double h, double rh) {
-  uint32_t guess = (uint32_t)(int)((w - m[0]) / h);  // h = m[1] - m[0] (host computed, same double)
+__device__ __forceinline__ int findLimInf(double w, double m0, int size, double h, double rh) {
+  // (w - m[0]) / (m[1] - m[0]); operands normal or zero, so div_nr is exact
+  uint32_t guess = (uint32_t)(int)div_nr(w - m0, h, rh);
   if (guess > (uint32_t)(size - 2)) guess = (uint32_t)(size - 2);
   return (int)guess;
 }
@@ -128,10 +138,11 @@ __device__ __forceinline__ int findLimInf(double w, const double* m, int size, d
 // MeshInterpolator<D>::evalMonitorOnGrid (src/MeshInterpolator.cpp:287-342)
 template <int D>
 __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* pnt, M<D>& mv) {
-  const int xInd = findLimInf(pnt[0], g.gx, g.nx + 1, g.hx, g.rhx);
-  const int yInd = findLimInf(pnt[1], g.gy, g.ny + 1, g.hy, g.rhy);
+  const int xInd = findLimInf(pnt[0], g.ax, g.nx + 1, g.hx, g.rhx);
+  const int yInd = findLimInf(pnt[1], g.ay, g.ny + 1, g.hy, g.rhy);
   const int nx = g.nx;
   if constexpr (D == 2) {
+    // loading the coordinates is cheaper here than recomputing them with gridCoord (measured)
     const double xm0 = g.gx[xInd], xm1 = g.gx[xInd + 1], ym0 = g.gy[yInd], ym1 = g.gy[yInd + 1];
     const double x = pnt[0], y = pnt[1];
     const double norm = (1 / ((xm1 - xm0) * (ym1 - ym0)));
@@ -146,10 +157,13 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     mv.m[1][0] = c0 * a1.x + c1 * b1.x + c2 * e1.x + c3 * f1.x;
     mv.m[1][1] = c0 * a1.y + c1 * b1.y + c2 * e1.y + c3 * f1.y;
   } else {
-    const int zInd = findLimInf(pnt[2], g.gz, g.nz + 1, g.hz, g.rhz);
-    const double xd = (pnt[0] - g.gx[xInd]) / (g.gx[xInd + 1] - g.gx[xInd]);
-    const double yd = (pnt[1] - g.gy[yInd]) / (g.gy[yInd + 1] - g.gy[yInd]);
-    const double zd = (pnt[2] - g.gz[zInd]) / (g.gz[zInd + 1] - g.gz[zInd]);
+    const int zInd = findLimInf(pnt[2], g.az, g.nz + 1, g.hz, g.rhz);
+    const double x0 = g.gx[xInd], x1 = g.gx[xInd + 1];
+    const double y0 = g.gy[yInd], y1 = g.gy[yInd + 1];
+    const double z0 = g.gz[zInd], z1 = g.gz[zInd + 1];
+    const double xd = (pnt[0] - x0) / (x1 - x0);
+    const double yd = (pnt[1] - y0) / (y1 - y0);
+    const double zd = (pnt[2] - z0) / (z1 - z0);
     const double c[8] = {(1 - xd) * (1 - yd) * (1 - zd), xd * (1 - yd) * (1 - zd),
                          (1 - xd) * yd * (1 - zd),       xd * yd * (1 - zd),
                          (1 - xd) * (1 - yd) * zd,       xd * (1 - yd) * zd,

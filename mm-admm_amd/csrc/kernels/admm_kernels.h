@@ -30,6 +30,7 @@ struct DeviceMesh {
   const double* gvals;
   int gnx, gny, gnz;
   double ghx, ghy, ghz, grhx, grhy, grhz;  // grid spacings of findLimInf and RN(1/h)
+  double gax, gay, gaz, gspx, gspy, gspz, gnsx, gnsy, gnsz, grnsx, grnsy, grnsz;  // linspace params
   // functional constants
   double Ehat[9];
   double powd, w;
@@ -64,6 +65,9 @@ template <int D>
 void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
                         hipStream_t st);
 void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st);
+// two reductions in one launch (one workgroup each)
+void launch_reduce_partials2(const double* partials, int nblocks, double* out, const double* partials2, int nblocks2,
+                             double* out2, hipStream_t st);
 // interface-slot values a rank contributes to the exchange: mode 0 the x-update term
 // w (w (z - u)) per slot, mode 1 the simplex gradient gs per slot (D values each)
 template <int D>

@@ -76,6 +76,18 @@ __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   g.rhx = m.grhx;
   g.rhy = m.grhy;
   g.rhz = m.grhz;
+  g.ax = m.gax;
+  g.ay = m.gay;
+  g.az = m.gaz;
+  g.spx = m.gspx;
+  g.spy = m.gspy;
+  g.spz = m.gspz;
+  g.nsx = m.gnsx;
+  g.nsy = m.gnsy;
+  g.nsz = m.gnsz;
+  g.rnsx = m.grnsx;
+  g.rnsy = m.grnsy;
+  g.rnsz = m.grnsz;
   return g;
 }
 
@@ -649,7 +661,13 @@ __global__ void __launch_bounds__(kBlock) k_pack_export(int mode, int nExp, cons
 }
 
 __global__ void __launch_bounds__(kBlock) k_reduce_partials(const double* __restrict__ partials, int nblocks,
-                                                             double* __restrict__ out) {
+                                                             double* __restrict__ out, const double* __restrict__ partials2,
+                                                             int nblocks2, double* __restrict__ out2) {
+  if (blockIdx.x == 1) {  // second set in the same launch
+    partials = partials2;
+    nblocks = nblocks2;
+    out = out2;
+  }
   // one workgroup; lane-strided partial sums then a fixed-shape tree
   __shared__ double red[kBlock][kNumPartials];
   double acc[kNumPartials];
@@ -828,7 +846,11 @@ void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, dou
   hipLaunchKernelGGL(k_euler_apply<D>, dim3(nblk_xcd(m.nP)), dim3(kBlock), 0, st, m, gs, x, dt_over_tau, xcd_map());
 }
 void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, st, partials, nblocks, out);
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, st, partials, nblocks, out, partials, nblocks, out);
+}
+void launch_reduce_partials2(const double* partials, int nblocks, double* out, const double* partials2, int nblocks2,
+                             double* out2, hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce_partials, dim3(2), dim3(kBlock), 0, st, partials, nblocks, out, partials2, nblocks2, out2);
 }
 template <int D>
 void launch_debug_blockgrad(const DeviceMesh<D>& m, int s, const double* z, const double* dx, double* out, int flags,

@@ -42,6 +42,14 @@ MMX_HD double div_by(double x, double c, double rc) {
 }
 constexpr double kRecip3 = 1.0 / 3.0;  // RN(1/3), for the divisions by D + 1 = 3
 
+// The same without range guards, for call sites whose operands are known to be normal with a
+// quotient that is zero or normal (grid coordinates): three instructions, no branch.
+MMX_HD double div_nr(double x, double c, double rc) {
+  const double q = x * rc;
+  const double r = cr_fma(-q, c, x);
+  return cr_fma(r, rc, q);
+}
+
 // argument ranges in which the exact fallback (x^p and m^q as expansions) cannot over- or
 // underflow; outside them (never met by the functional) the device libm pow is used.
 MMX_HD bool cr_in(double x, double lo, double hi) { return x > lo && x < hi; }
