@@ -1246,6 +1246,146 @@ struct Integrator : Base {
     return Ihorig;
   }
 
+  // ---- backward Euler (method 2) ------------------------------------------------------------
+  // Mesh<D>::eulerStepMod (Mesh.cpp:532-579): blockGrad (no FIXED zeroing) scattered to INTERIOR
+  // nodes; returns the summed energy.
+  double eulerStepMod(const std::vector<double>& xv, std::vector<double>& grad) {
+    std::fill(grad.begin(), grad.end(), 0.0);
+    double Ihorig = 0.0;
+    double zi[K], xi[K], g[K], Igt;
+    for (int i = 0; i < nF; i++) {
+      simplexXi(i, xi);
+      for (int n = 0; n < D + 1; n++)
+        for (int l = 0; l < D; l++) zi[n * D + l] = xv[D * F[i * (D + 1) + n] + l];
+      Ihorig += blockGrad(i, zi, xi, g, true, false, &Igt, nullptr);
+      for (int n = 0; n < D + 1; n++) {
+        const int off = F[i * (D + 1) + n];
+        if (mask[off] == INTERIOR)
+          for (int l = 0; l < D; ++l) grad[D * off + l] += g[D * n + l];
+      }
+    }
+    return Ihorig;
+  }
+
+  std::vector<int> jia, jja;  // buildMatrix pattern (Mesh.cpp:309-345)
+  std::vector<double> jval;
+  bool beStepTaken = false;
+  int lastNewton = 0;
+
+  // Mesh<D>::buildEulerJac + FSubJac (Mesh.cpp:1112-1261): finite-difference Jacobian of the
+  // gradient, evaluated at Vp (the initial mesh: Vp is only updated by done(), App. A-16).
+  void buildEulerJac(double dtBE) {
+    std::fill(jval.begin(), jval.end(), 0.0);
+    std::vector<std::vector<int>> conn(nP);  // simplexConnects: ascending simplex ids
+    for (int s = 0; s < nF; ++s)
+      for (int n = 0; n < D + 1; ++n) conn[F[s * (D + 1) + n]].push_back(s);
+    const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
+    double xLoc[K], xiLoc[K], Gk[K], Gkp1[K], xPurt[K], derivs[D][K], Igt;
+    for (int pntId = 0; pntId < nP; ++pntId) {
+      auto& sids = conn[pntId];
+      sids.erase(std::unique(sids.begin(), sids.end()), sids.end());
+      for (int sId : sids) {
+        int off = 0;
+        simplexXi(sId, xiLoc);
+        for (int n = 0; n < D + 1; n++) {
+          const int v = F[sId * (D + 1) + n];
+          if (v == pntId) off = n;
+          for (int l = 0; l < D; l++) xLoc[n * D + l] = Vp[(size_t)v * D + l];
+        }
+        blockGrad(sId, xLoc, xiLoc, Gk, true, false, &Igt, nullptr);
+        for (int i = 0; i < K; ++i) xPurt[i] = xLoc[i];
+        if (mask[pntId] == BOUNDARY_FIXED) {
+          for (int r = 0; r < D; r++)
+            for (int c = 0; c < K; c++) derivs[r][c] = 0.0;
+          for (int r = 0; r < D; r++)
+            for (int c = D * off; c < D * (off + 1); c++)
+              if (r == c) derivs[r][c] = 1.0;  // only for off == 0 (App. A-17)
+        } else {
+          for (int i = 0; i < D; i++) {
+            xPurt[D * off + i] += h;
+            blockGrad(sId, xPurt, xiLoc, Gkp1, true, false, &Igt, nullptr);
+            for (int c = 0; c < K; ++c) derivs[i][c] = (Gkp1[c] - Gk[c]) / h;
+            xPurt[D * off + i] = xLoc[D * off + i];
+          }
+        }
+        int sorted[D + 1], rel[D + 1];  // pairsort by node id
+        for (int r = 0; r < D + 1; r++) {
+          sorted[r] = F[sId * (D + 1) + r];
+          rel[r] = r;
+        }
+        for (int a = 1; a < D + 1; ++a)
+          for (int b = a; b > 0 && sorted[b - 1] > sorted[b]; --b) {
+            std::swap(sorted[b - 1], sorted[b]);
+            std::swap(rel[b - 1], rel[b]);
+          }
+        for (int pp = 0; pp < D; pp++) {
+          const int row = D * pntId + pp;
+          for (int i = jia[row]; i < jia[row + 1]; i++) {
+            const int colIndex = jja[i] / D, colOff = jja[i] % D;
+            for (int j = 0; j < D + 1; j++) {
+              if (sorted[j] == colIndex)
+                jval[i] += derivs[pp][D * rel[j] + colOff];
+              else
+                jval[i] += 0.0;
+            }
+          }
+        }
+      }
+    }
+    const int n = D * nP;
+    for (int r = 0; r < n; r++)
+      for (int i = jia[r]; i < jia[r + 1]; i++) {
+        jval[i] *= (dtBE / tau);
+        if (jja[i] == r) jval[i] += 1.0;
+      }
+  }
+
+  // Mesh<D>::backwardsEulerStep (Mesh.cpp:1263-1341): Newton on F(x) = (dt/tau) grad + (x - xn)
+  // with the ILU(0)-CG-STAB solve (lib/LASolver); returns the last eulerStepMod energy.
+  double backwardsEulerStep(double dtBE, double tol, int dotMode) {
+    const int n = D * nP;
+    if (jia.empty()) {  // buildMatrix
+      jia.resize(n + 1);
+      const int nnz = orc_la_mesh_pattern(D, nP, nF, F.data(), jia.data(), nullptr, 0);
+      jja.resize(nnz);
+      orc_la_mesh_pattern(D, nP, nF, F.data(), jia.data(), jja.data(), nnz);
+      jval.assign(nnz, 0.0);
+    }
+    const std::vector<double> xn = x;
+    const double SAFETY_FAC = 1.0 / 10.0;
+    std::vector<double> grad(n, 0.0), rhs(n), dx(n);
+    double Ih = eulerStepMod(x, grad);
+    for (int i = 0; i < n; ++i) x[i] -= (dtBE / tau) * grad[i];
+    const int MAX_ITERS = 1000;
+    int nIter = 0;
+    double gradOneN = 0, gradOneNPrev = INFINITY;
+    if (!beStepTaken) buildEulerJac(dtBE);  // (+ sfac)
+    do {
+      Ih = eulerStepMod(x, grad);
+      for (int i = 0; i < n; ++i) grad[i] *= (dtBE / tau);
+      for (int i = 0; i < n; ++i) grad[i] += (x[i] - xn[i]);
+      gradOneN = sse2_redux(n, [&](long i) { return std::fabs(grad[i]); });
+      if (gradOneN < SAFETY_FAC * tol) break;
+      if (!beStepTaken || std::fabs(gradOneN - gradOneNPrev) / (gradOneN) < 0.25) {
+        buildEulerJac(dtBE);
+        beStepTaken = true;
+      }
+      for (int i = 0; i < n; ++i) rhs[i] = -grad[i];
+      int cgIter = 0;
+      orc_la_solve(n, jia.data(), jja.data(), jval.data(), rhs.data(), nullptr, 10000, 1e-6, 0, 0, dx.data(), &cgIter,
+                   nullptr, dotMode);
+      if (cgIter <= 0) {  // the reference asserts cgIter > 0
+        err = 1;
+        break;
+      }
+      for (int i = 0; i < n; ++i) x[i] += dx[i];
+      nIter++;
+      gradOneNPrev = gradOneN;
+    } while (nIter < MAX_ITERS);
+    lastNewton = nIter;
+    return Ih;
+  }
+
   // Mesh<D>::computeEnergy (Mesh.cpp:496-530) on Vp
   double energy() const {
     double Ih = 0.0;
@@ -1341,6 +1481,26 @@ int orc_euler_step(void* h, double* Ih) {
   DISPATCH(h, r = s->eulerStep(), r = s->eulerStep());
   *Ih = r;
   return 0;
+}
+int orc_backward_euler_step(void* h, double dt, double tol, int dotMode, double* Ih, int* newtonIters) {
+  double r = 0;
+  int e = 0, it = 0;
+  DISPATCH(h, (r = s->backwardsEulerStep(dt, tol, dotMode), e = s->err, it = s->lastNewton),
+           (r = s->backwardsEulerStep(dt, tol, dotMode), e = s->err, it = s->lastNewton));
+  *Ih = r;
+  if (newtonIters) *newtonIters = it;
+  return e;
+}
+void orc_get_jacobian(void* h, int* ia, int* ja, double* a) {
+  DISPATCH(h, (std::copy(s->jia.begin(), s->jia.end(), ia), std::copy(s->jja.begin(), s->jja.end(), ja),
+               std::copy(s->jval.begin(), s->jval.end(), a)),
+           (std::copy(s->jia.begin(), s->jia.end(), ia), std::copy(s->jja.begin(), s->jja.end(), ja),
+            std::copy(s->jval.begin(), s->jval.end(), a)));
+}
+long long orc_jacobian_nnz(void* h) {
+  long long r = 0;
+  DISPATCH(h, r = (long long)s->jja.size(), r = (long long)s->jja.size());
+  return r;
 }
 double orc_energy(void* h) {
   double r = 0;

@@ -43,6 +43,11 @@ void* orc_create(int dim, int nP, const double* Vp, const double* Vc, int nF, co
 int orc_step(void* h, int nIters, double tol, double* Ih, int* admmIters, double* primal,
              double* dual);
 int orc_euler_step(void* h, double* Ih);
+/* MeshIntegrator::backwardsEulerStep (method 2): Newton with the FD Jacobian at the initial mesh
+ * and the LASolver restatement; dotMode 0 reference sums, 1 the GPU's reduction order */
+int orc_backward_euler_step(void* h, double dt, double tol, int dotMode, double* Ih, int* newtonIters);
+long long orc_jacobian_nnz(void* h);
+void orc_get_jacobian(void* h, int* ia, int* ja, double* a);
 double orc_energy(void* h);
 void orc_done(void* h);
 void orc_get(void* h, const char* what, double* out);

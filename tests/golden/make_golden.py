@@ -2,7 +2,7 @@
 
 Run in the build container (where /root/reference exists).  The files are data written by the
 reference's own runs (Experiments/Results/*): input meshes (points/triangles/mask) and energy
-traces Ih0.txt ("t, Ih" rows, 6 significant digits).  Nothing else is copied.
+traces Ih0/Ih1/Ih2.txt ("t, Ih" rows, 6 significant digits).  Nothing else is copied.
 """
 import os
 import shutil
@@ -19,6 +19,8 @@ FILES = [
     "Monitor220/Ih0.txt", "Monitor310/Ih0.txt", "Monitor340/Ih0.txt", "Monitor2160/Ih0.txt",
     "Monitor380/Ih0.txt", "Monitor3160/Ih0.txt",
     "3DMonitor210/Ih0.txt", "3DMonitor310/Ih0.txt", "3DMonitor310/Ih1.txt",
+    # method 2 (backwardsEulerStep) traces
+    "Monitor220/Ih2.txt", "Monitor320/Ih2.txt", "3DMonitor210/Ih2.txt",
 ]
 
 if __name__ == "__main__":

@@ -159,6 +159,31 @@ class Integrator:
         lib().orc_euler_step(self.h, ctypes.byref(Ih))
         return Ih.value
 
+    def backwards_euler_step(self, dt, tol=1e-3, tree=False):
+        """MeshIntegrator::backwardsEulerStep -> (Ih, Newton iterations).  tree: the GPU's
+        reduction order in the CG-STAB dot products."""
+        L = lib()
+        L.orc_backward_euler_step.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                              c_double_p, c_int_p]
+        Ih, it = ctypes.c_double(), ctypes.c_int()
+        e = L.orc_backward_euler_step(self.h, dt, tol, 1 if tree else 0, ctypes.byref(Ih), ctypes.byref(it))
+        if e:
+            raise RuntimeError("oracle: backward Euler failed (inverted element or CG-STAB non-convergence)")
+        return Ih.value, it.value
+
+    def jacobian(self):
+        """The last backward-Euler Jacobian (ia, ja, a)."""
+        L = lib()
+        L.orc_jacobian_nnz.argtypes = [ctypes.c_void_p]
+        L.orc_jacobian_nnz.restype = ctypes.c_longlong
+        L.orc_get_jacobian.argtypes = [ctypes.c_void_p, c_int_p, c_int_p, c_double_p]
+        nnz = L.orc_jacobian_nnz(self.h)
+        ia = np.zeros(self.dim * self.nP + 1, np.int32)
+        ja = np.zeros(nnz, np.int32)
+        a = np.zeros(nnz)
+        L.orc_get_jacobian(self.h, ia.ctypes.data_as(c_int_p), ja.ctypes.data_as(c_int_p), a.ctypes.data_as(c_double_p))
+        return ia, ja, a
+
     def energy(self):
         return lib().orc_energy(self.h)
 

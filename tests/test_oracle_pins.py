@@ -122,3 +122,31 @@ def test_gradient_matches_finite_differences():
         for n in range(3):
             if mask[n] != 1:
                 np.testing.assert_allclose(g[2 * n:2 * n + 2], fd[2 * n:2 * n + 2], rtol=1e-5, atol=1e-7)
+
+
+# Method 2 (Mesh::backwardsEulerStep, Mesh.cpp:1263-1341): (config, mesh, MonType, dt, tau, rho,
+# DtTol, nSteps).  The time loop is runAlgo's with solver.backwardsEulerStep(dt, 1e-3).
+BE_TRACES = [
+    ("Monitor220", ("rect", 2, 20), 3, 0.025, 0.5, 100, 1e-4, 1000),
+    ("Monitor320", ("file", "CircleEx12"), 5, 0.05, 0.1, 5, 1e-5, 10000),
+    ("3DMonitor210", ("rect", 3, 10), 3, 0.025, 0.5, 50, 1e-5, 100),
+]
+
+
+@pytest.mark.parametrize("cfg", BE_TRACES, ids=[t[0] for t in BE_TRACES])
+def test_backward_euler_trace(cfg):
+    name, mesh, mon, dt, tau, rho, dtTol, nSteps = cfg
+    m = oracle_py.Mesh.rect(mesh[1], mesh[2]) if mesh[0] == "rect" else circle_mesh(mesh[1])
+    I = oracle_py.Integrator(m, mon, dt, tau, rho)
+    ours = [I.energy()]
+    prev = np.inf
+    for i in range(nSteps):
+        Ih, _ = I.backwards_euler_step(dt, 1e-3)
+        ours.append(Ih)
+        if i != 0 and abs((Ih - prev) / dt) < dtTol:
+            break
+        prev = Ih
+    ref = np.loadtxt(os.path.join(GOLDEN, name, "Ih2.txt"), delimiter=",")[:, 1]
+    assert len(ours) == len(ref), "number of time steps differs"
+    rel = np.abs(np.array(ours) - ref) / np.abs(ref)
+    assert rel.max() < SIX_DIGITS, rel.max()
