@@ -14,6 +14,9 @@
  *                              src/MeshIntegrator.cpp:15-62)
  *   mmadmm_step              MeshIntegrator<D>::step (src/MeshIntegrator.h:17, .cpp:101-191)
  *   mmadmm_euler_step        MeshIntegrator<D>::eulerStep (src/MeshIntegrator.h:18, .cpp:87-94)
+ *   mmadmm_backward_euler_step MeshIntegrator<D>::backwardsEulerStep (src/MeshIntegrator.h:19,
+ *                            .cpp:68-76) -> Mesh<D>::backwardsEulerStep (src/Mesh.cpp:1263-1341)
+ *   mmadmm_get_jacobian      Mesh<D>::jac after buildEulerJac (src/Mesh.cpp:1112-1136)
  *   mmadmm_energy            MeshIntegrator<D>::getEnergy (src/MeshIntegrator.h:20, .cpp:79-81)
  *   mmadmm_done              MeshIntegrator<D>::done (src/MeshIntegrator.h:23, .cpp:193-196)
  *   mmadmm_get("x"|"z")      MeshIntegrator<D>::outputX / outputZ (src/MeshIntegrator.h:21-22)
@@ -40,6 +43,7 @@ extern "C" {
 #define MMADMM_ERR_INVERTED 3 /* inverted element: the reference's assert(Edet > 0) */
 #define MMADMM_ERR_IO 4       /* file not readable / writable */
 #define MMADMM_ERR_RCCL 5     /* collective failure */
+#define MMADMM_ERR_NOCONV 6   /* linear solve did not converge: the reference's assert(cgIter > 0) */
 
 /* Node types (src/NodeType.h:4-8); mask arrays use these values. */
 #define MMADMM_BOUNDARY_FREE 0
@@ -77,6 +81,8 @@ typedef struct mmadmm_stats {
   long long n_steps_timed;
   double prox_bytes;      /* algorithmic HBM bytes of one prox launch */
   double xupdate_bytes;   /* algorithmic HBM bytes of one x-update launch */
+  long long newton_iters; /* backward Euler: Newton iterations summed over steps */
+  long long jacobians;    /* backward Euler: FD Jacobian builds */
 } mmadmm_stats;
 
 const char* mmadmm_last_error(void);
@@ -96,6 +102,10 @@ int mmadmm_create(int dim, int nP, const double* Xp, const double* Xc, int nF, c
  * *Ih = energy at the first prox of the step (the reference's return value). */
 int mmadmm_step(mmadmm_handle h, int n_iters, double tol, double* Ih, int* admm_iters);
 int mmadmm_euler_step(mmadmm_handle h, double* Ih);
+/* method 2: one backward Euler step (Newton + ILU(0) CG-STAB); single rank only */
+int mmadmm_backward_euler_step(mmadmm_handle h, double dt, double tol, double* Ih, int* newton_iters);
+/* the last assembled backward-Euler Jacobian (CSR over D*nP unknowns); null arrays are skipped */
+int mmadmm_get_jacobian(mmadmm_handle h, long long* nnz, int32_t* ia, int32_t* ja, double* a);
 int mmadmm_energy(mmadmm_handle h, double* E);
 int mmadmm_done(mmadmm_handle h);
 /* what: "x", "xPrev", "xBar", "z", "u", "points", "hess", "grid", "Ehat" */

@@ -6,15 +6,23 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
 
+#include "../../../include/mmx_sparse.h"
 #include "../kernels/admm_kernels.h"
 #include "comm.h"
 #include "common.h"
 #include "partition.h"
+
+#define MMX_SP(expr)                                                                     \
+  do {                                                                                   \
+    const int rc_ = (expr);                                                              \
+    if (rc_ != MMADMM_OK) throw ::mmx::Error(rc_, std::string(#expr) + ": " + mmadmm_last_error()); \
+  } while (0)
 
 namespace mmx {
 
@@ -29,6 +37,8 @@ struct EngineBase {
   int dim = 2;
   virtual void step(int nIters, double tol, double* Ih, int* iters) = 0;
   virtual double eulerStep() = 0;
+  virtual double backwardEulerStep(double dt, double tol, int* newton) = 0;
+  virtual void jacobian(long long* nnz, int32_t* ia, int32_t* ja, double* a) = 0;
   virtual double energy() = 0;
   virtual void done() = 0;
   virtual void get(const std::string& what, double* out) = 0;
@@ -176,6 +186,7 @@ class Engine final : public EngineBase {
   }
 
   ~Engine() override {
+    if (jac_) (void)mmx_matrix_destroy(jac_);
     for (auto& e : evPool_) (void)hipEventDestroy(e);
     if (st_) (void)hipStreamDestroy(st_);
   }
@@ -309,6 +320,68 @@ class Engine final : public EngineBase {
     return r[0];
   }
 
+  // MeshIntegrator::backwardsEulerStep -> Mesh::backwardsEulerStep (src/MeshIntegrator.cpp:68-76,
+  // src/Mesh.cpp:1263-1341): Newton on F(x) = (dt/tau) grad(x) + (x - xn), the explicit Euler
+  // step as initial guess, J dx = -F by the LASolver replacement (ILU(0) CG-STAB, include/
+  // mmx_sparse.h) on the device.  The Jacobian is the FD Jacobian at Vp, built on the first
+  // Newton iteration of the run and again whenever ||F||_1 stagnates (ratio < 0.25).
+  double backwardEulerStep(double dtBE, double tol, int* newtonOut) override {
+    if (nranks_ > 1) throw Error(MMADMM_ERR_INVALID, "backward Euler runs on one rank (no element partition)");
+    const int n = nP_ * D;
+    ensureJacobian();
+    const double dtot = dtBE / prm_.tau;
+    const double SAFETY_FAC = 1.0 / 10.0;
+    const int MAX_ITERS = 1000;
+    MMX_HIP(hipMemcpyAsync(xn_.p, x_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st_));
+    int nb = 0, nb2 = 0;
+    launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);  // initial guess
+    launch_euler_apply<D>(m_, gs_.p, x_.p, dtot, st_);
+    if (!beStepTaken_) buildJacobian(dtBE);
+    int nIter = 0;
+    double Ih = 0.0, normPrev = INFINITY;
+    std::vector<double> rv;
+    void* mst = nullptr;
+    MMX_SP(mmx_matrix_stream(jac_, &mst));
+    do {
+      launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
+      launch_be_residual<D>(m_, gs_.p, x_.p, xn_.p, dtot, rhs_.p, partB_.p, &nb2, st_);
+      launch_reduce_partials2(partA_.p, nb, results_.p, partB_.p, nb2, results_.p + kNumPartials, st_);
+      fetchResults(results_.p, 1, rv);
+      if (rv[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element in backward Euler (reference: assert(Edet > 0))");
+      Ih = rv[0];
+      const double norm = rv[kNumPartials];
+      if (norm < SAFETY_FAC * tol) break;
+      if (!beStepTaken_ || std::fabs(norm - normPrev) / norm < 0.25) {
+        buildJacobian(dtBE);
+        beStepTaken_ = true;
+      }
+      MMX_HIP(hipStreamSynchronize(st_));  // rhs and the Jacobian values are ready for the solver stream
+      MMX_SP(mmx_matrix_set_rhs_device(jac_, rhs_.p));
+      int cgIter = 0;
+      MMX_SP(mmx_matrix_solve_device(jac_, &jprm_, dx_.p, &cgIter, 0));
+      MMX_HIP(hipStreamSynchronize((hipStream_t)mst));
+      if (cgIter <= 0)
+        throw Error(MMADMM_ERR_NOCONV, "backward Euler: CG-STAB did not converge (reference: assert(cgIter > 0))");
+      launch_add_inplace(n, x_.p, dx_.p, st_);
+      nIter++;
+      normPrev = norm;
+    } while (nIter < MAX_ITERS);
+    MMX_HIP(hipStreamSynchronize(st_));
+    st_stats_.steps += 1;
+    st_stats_.newton_iters += nIter;
+    if (newtonOut) *newtonOut = nIter;
+    return Ih;
+  }
+
+  void jacobian(long long* nnz, int32_t* ia, int32_t* ja, double* a) override {
+    if (!jac_) throw Error(MMADMM_ERR_INVALID, "no Jacobian yet: run a backward Euler step first");
+    if (nnz) *nnz = (long long)jja_.n;
+    if (ia) MMX_HIP(hipMemcpyAsync(ia, jia_.p, jia_.n * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
+    if (ja) MMX_HIP(hipMemcpyAsync(ja, jja_.p, jja_.n * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
+    if (a) MMX_HIP(hipMemcpyAsync(a, jval_.p, jval_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+  }
+
   // Mesh::computeEnergy on Vp (src/Mesh.cpp:496-530)
   double energy() override {
     int nb = 0;
@@ -397,6 +470,52 @@ class Engine final : public EngineBase {
   struct Timed {
     hipEvent_t a0, a1, b1;
   };
+
+  // buildMatrix (src/Mesh.cpp:262-382): the Jacobian's pattern over the D*nP unknowns, the
+  // ParamIter of the reference and the symbolic ILU (sfac, done once as the reference does).
+  void ensureJacobian() {
+    if (jac_) return;
+    const int n = nP_ * D;
+    mmx_struc sp = nullptr;
+    MMX_SP(mmx_struc_create(n, 0, &sp));
+    std::vector<int32_t> ia(n + 1), ja;
+    long long nnz = 0;
+    int rc = mmx_struc_mesh_pattern(sp, D, (int)(Fh_.size() / (D + 1)), Fh_.data());
+    if (rc == MMADMM_OK) rc = mmx_struc_pack(sp);
+    if (rc == MMADMM_OK) rc = mmx_struc_get(sp, nullptr, &nnz, nullptr, nullptr);
+    if (rc == MMADMM_OK) {
+      ja.resize(nnz);
+      rc = mmx_struc_get(sp, nullptr, &nnz, ia.data(), ja.data());
+    }
+    int dev = prm_.device;
+    if (dev < 0) MMX_HIP(hipGetDevice(&dev));
+    if (rc == MMADMM_OK) rc = mmx_matrix_create_from_struc(dev, sp, &jac_);
+    (void)mmx_struc_destroy(sp);
+    if (rc != MMADMM_OK) throw Error(rc, std::string("backward Euler Jacobian: ") + mmadmm_last_error());
+    mmx_param_iter_mesh(&jprm_);
+    jia_.upload(ia.data(), ia.size(), st_);
+    jja_.upload(ja.data(), ja.size(), st_);
+    jval_.alloc(std::max<size_t>(nnz, 1));
+    dv_.alloc(std::max<size_t>((size_t)nF_ * (D + 1) * D * K, 1));
+    xn_.alloc((size_t)n);
+    rhs_.alloc((size_t)n);
+    dx_.alloc((size_t)n);
+    MMX_HIP(hipStreamSynchronize(st_));
+  }
+
+  // buildEulerJac (src/Mesh.cpp:1112-1136); sfac after the first build (src/Mesh.cpp:1287-1290)
+  void buildJacobian(double dtBE) {
+    const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
+    launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
+    launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, dtBE / prm_.tau, jval_.p, st_);
+    MMX_HIP(hipStreamSynchronize(st_));
+    MMX_SP(mmx_matrix_set_values_device(jac_, jval_.p));
+    if (!jacFactored_) {
+      MMX_SP(mmx_matrix_sfac(jac_, &jprm_));
+      jacFactored_ = true;
+    }
+    st_stats_.jacobians += 1;
+  }
 
   static double hostDet(const double (&a)[3][3]) {  // Eigen 2x2 / 3x3 determinant
     if (D == 2) return a[0][0] * a[1][1] - a[1][0] * a[0][1];
@@ -518,6 +637,12 @@ class Engine final : public EngineBase {
   std::vector<double> hostRes_;
   DeviceMesh<D> m_{};
   bool hessComputed_ = false, stepTaken_ = false, gcacheValid_ = false;
+  // backward Euler: Jacobian (pattern, values, FD blocks), Newton vectors, the LASolver matrix
+  mmx_matrix jac_ = nullptr;
+  mmx_param_iter jprm_{};
+  bool beStepTaken_ = false, jacFactored_ = false;
+  DevBuf<int32_t> jia_, jja_;
+  DevBuf<double> jval_, dv_, xn_, rhs_, dx_;
   int stepsTaken_ = 0;
   bool timing_ = false;
   std::vector<hipEvent_t> evPool_;
@@ -617,6 +742,16 @@ int mmadmm_euler_step(mmadmm_handle h, double* Ih) {
     const double r = eng(h).eulerStep();
     if (Ih) *Ih = r;
   });
+}
+int mmadmm_backward_euler_step(mmadmm_handle h, double dt, double tol, double* Ih, int* newton_iters) {
+  return guarded([&] {
+    if (!(dt > 0)) throw mmx::Error(MMADMM_ERR_INVALID, "backward Euler: dt must be > 0");
+    const double r = eng(h).backwardEulerStep(dt, tol, newton_iters);
+    if (Ih) *Ih = r;
+  });
+}
+int mmadmm_get_jacobian(mmadmm_handle h, long long* nnz, int32_t* ia, int32_t* ja, double* a) {
+  return guarded([&] { eng(h).jacobian(nnz, ia, ja, a); });
 }
 int mmadmm_energy(mmadmm_handle h, double* E) {
   return guarded([&] {

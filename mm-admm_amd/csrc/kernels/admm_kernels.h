@@ -74,6 +74,25 @@ template <int D>
 void launch_pack_export(int mode, int nExp, const int* expOff, const double* z, const double* u, const double* gs,
                         double w, double* out, hipStream_t st);
 
+// ---- backward Euler (Mesh::backwardsEulerStep, src/Mesh.cpp:1263-1341) ----
+// FD derivative blocks of FSubJac (src/Mesh.cpp:1173-1230) at positions Vp: one D x K block per
+// (simplex s, local vertex n), row-major at dv + ((s*(D+1)+n)*D)*K.
+template <int D>
+void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st);
+// Jacobian values of buildEulerJac (src/Mesh.cpp:1112-1136, 1232-1258) on the buildMatrix CSR
+// pattern (ia, ja over the D*nP unknowns): per entry, the derivative blocks of the node's incident
+// simplices in ascending id (pairsort order, +0.0 adds), scaled by dt/tau, +1 on the diagonal.
+template <int D>
+void launch_jac_assemble(const DeviceMesh<D>& m, const int* ia, const int* ja, const double* dv,
+                         double dt_over_tau, double* a, hipStream_t st);
+// Newton residual F = (dt/tau) grad + (x - xn) with grad the INTERIOR-only scatter of gs
+// (eulerStepMod, src/Mesh.cpp:532-579); rhs = -F; partial record v[0] = sum |F_i|.
+template <int D>
+void launch_be_residual(const DeviceMesh<D>& m, const double* gs, const double* x, const double* xn,
+                        double dt_over_tau, double* rhs, double* partials, int* nblocks, hipStream_t st);
+// x += dx over n doubles
+void launch_add_inplace(int n, double* x, const double* dx, hipStream_t st);
+
 template <int D>
 void launch_debug_blockgrad(const DeviceMesh<D>& m, int s, const double* z, const double* dx, double* out,
                             int flags, hipStream_t st);

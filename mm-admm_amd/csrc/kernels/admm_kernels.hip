@@ -647,6 +647,128 @@ __global__ void __launch_bounds__(kBlock) k_euler_apply(DeviceMesh<D> m, const d
   for (int c = 0; c < D; ++c) x[(size_t)v * D + c] -= dt_over_tau * g[c];
 }
 
+// ---- backward Euler -------------------------------------------------------------------------
+// FSubJac's derivative blocks (src/Mesh.cpp:1173-1230), simplex-centric: thread (s, n) evaluates
+// blockGrad at the vertices Vp (pass -1, the reference's Gk) and with coordinate i of vertex n
+// moved by h (pass i), and writes derivs(i, :) = (Gkp1 - Gk) / h.  A BOUNDARY_FIXED vertex gets
+// the reference's identity pattern, which is nonzero only for n == 0 (r == c in D*n..D*n+D-1).
+// The node-centric reference evaluates Gk once per (node, simplex); the values are the same.
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_fd_jac(DeviceMesh<D> m, const double* __restrict__ Vp, double h,
+                                                    double* __restrict__ dv) {
+  constexpr int K = D * (D + 1);
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (long long)m.nF * (D + 1)) return;
+  const int s = (int)(t / (D + 1)), n = (int)(t % (D + 1));
+  double* out = dv + (size_t)t * D * K;
+  if (m.sbits[s] & (1u << n)) {
+    for (int r = 0; r < D; ++r)
+#pragma unroll
+      for (int c = 0; c < K; ++c) out[r * K + c] = (c == r && c >= D * n && c < D * (n + 1)) ? 1.0 : 0.0;
+    return;
+  }
+  int f[D + 1];
+  loadVerts<D>(m, s, f);
+  double xl[K], xi[K], gk[K], g1[K], xp[K], Igt;
+  gatherX<D>(Vp, f, xl);
+  loadXi<D>(m, f, xi);
+  const GridView<D> g = gridOf<D>(m);
+  const FunctionalConsts<D> fc = constsOf<D>(m);
+#pragma unroll 1
+  for (int it = -1; it < D; ++it) {
+    const int moved = (it < 0) ? -1 : D * n + it;
+#pragma unroll
+    for (int c = 0; c < K; ++c) xp[c] = (c == moved) ? xl[c] + h : xl[c];
+    blockGrad<D, true, false>(g, fc, xp, xi, nullptr, g1, Igt);
+    if (it < 0) {
+#pragma unroll
+      for (int c = 0; c < K; ++c) gk[c] = g1[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < K; ++c) out[it * K + c] = (g1[c] - gk[c]) / h;
+    }
+  }
+}
+
+// buildEulerJac + FSubJac's scatter (src/Mesh.cpp:1112-1136, 1232-1258), row-centric: row
+// r = D*pnt + p, entry (col node ci, offset co).  The reference adds, for each incident simplex
+// in ascending id and each vertex j in pairsort order, derivs(p, D*rel[j]+co) where the sorted id
+// equals ci and +0.0 elsewhere; the +0.0 adds only turn a -0.0 sum into +0.0, so the same value
+// is v + 0.0 before the matching vertex (if it is not first), + d, + 0.0 after (if not last).
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_jac_assemble(DeviceMesh<D> m, const int* __restrict__ ia,
+                                                          const int* __restrict__ ja, const double* __restrict__ dv,
+                                                          double dt_over_tau, double* __restrict__ a) {
+  constexpr int K = D * (D + 1);
+  const int r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= m.nP * D) return;
+  const int pnt = r / D, p = r % D;
+  const int tb = m.inc_ptr[pnt], te = m.inc_ptr[pnt + 1];
+  for (int i = ia[r]; i < ia[r + 1]; ++i) {
+    const int col = ja[i], ci = col / D, co = col % D;
+    double v = 0.0;
+    for (int t = tb; t < te; ++t) {
+      const int off = m.inc_off[t];
+      const int s = off / K, nl = (off % K) / D;
+      int f[D + 1];
+      loadVerts<D>(m, s, f);
+      int hit = -1, rank = 0;
+#pragma unroll
+      for (int k = 0; k < D + 1; ++k) {
+        if (f[k] == ci) hit = k;
+        rank += (f[k] < ci) ? 1 : 0;
+      }
+      if (hit >= 0) {
+        if (rank > 0) v = v + 0.0;
+        v = v + dv[((size_t)(s * (D + 1) + nl) * D + p) * K + D * hit + co];
+        if (rank < D) v = v + 0.0;
+      } else {
+        v = v + 0.0;
+      }
+    }
+    v *= dt_over_tau;
+    if (col == r) v += 1.0;
+    a[i] = v;
+  }
+}
+
+// Newton residual of backwardsEulerStep (src/Mesh.cpp:1301-1306): grad from eulerStepMod's
+// INTERIOR-only scatter (ascending simplex id), F = grad * (dt/tau) + (x - xn), rhs = -F.
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_be_residual(DeviceMesh<D> m, const double* __restrict__ gs,
+                                                         const double* __restrict__ x, const double* __restrict__ xn,
+                                                         double dt_over_tau, double* __restrict__ rhs,
+                                                         double* __restrict__ partials, int xcd) {
+  const int lb = logical_block(xcd);
+  const int v = lb * kBlock + threadIdx.x;
+  double pv[1] = {0.0};
+  if (v < m.nP) {
+    double g[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) g[c] = 0.0;
+    if (m.nodeInterior[v]) {
+      const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
+      for (int t = b; t < e; ++t) {
+        const double* src = gs + m.inc_off[t];
+#pragma unroll
+        for (int c = 0; c < D; ++c) g[c] += src[c];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      const double F = g[c] * dt_over_tau + (x[(size_t)v * D + c] - xn[(size_t)v * D + c]);
+      pv[0] += __builtin_fabs(F);
+      rhs[(size_t)v * D + c] = -F;
+    }
+  }
+  block_partials<1>(pv, partials, lb);
+}
+
+__global__ void __launch_bounds__(kBlock) k_add_inplace(int n, double* __restrict__ x, const double* __restrict__ dx) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) x[i] += dx[i];
+}
+
 template <int D>
 __global__ void __launch_bounds__(kBlock) k_pack_export(int mode, int nExp, const int* __restrict__ expOff,
                                                          const double* __restrict__ z, const double* __restrict__ u,
@@ -878,6 +1000,31 @@ void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st
   hipLaunchKernelGGL(k_devmath, dim3((n + 255) / 256), dim3(256), 0, st, op, n, in, out);
 }
 
+template <int D>
+void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st) {
+  const long long nt = (long long)m.nF * (D + 1);
+  if (nt == 0) return;
+  hipLaunchKernelGGL(k_fd_jac<D>, dim3((unsigned)((nt + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, m, Vp, h, dv);
+}
+template <int D>
+void launch_jac_assemble(const DeviceMesh<D>& m, const int* ia, const int* ja, const double* dv, double dt_over_tau,
+                         double* a, hipStream_t st) {
+  if (m.nP == 0) return;
+  hipLaunchKernelGGL(k_jac_assemble<D>, dim3(nblk(m.nP * D)), dim3(kBlock), 0, st, m, ia, ja, dv, dt_over_tau, a);
+}
+template <int D>
+void launch_be_residual(const DeviceMesh<D>& m, const double* gs, const double* x, const double* xn,
+                        double dt_over_tau, double* rhs, double* partials, int* nblocks, hipStream_t st) {
+  *nblocks = nblk_xcd(m.nP);
+  if (m.nP == 0) return;
+  hipLaunchKernelGGL(k_be_residual<D>, dim3(*nblocks), dim3(kBlock), 0, st, m, gs, x, xn, dt_over_tau, rhs, partials,
+                     xcd_map());
+}
+void launch_add_inplace(int n, double* x, const double* dx, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_add_inplace, dim3(nblk(n)), dim3(kBlock), 0, st, n, x, dx);
+}
+
 #define MMX_INST(D)                                                                                     \
   template void launch_gather_z<D>(const DeviceMesh<D>&, const double*, double*, hipStream_t);          \
   template void launch_grad_simplex<D>(const DeviceMesh<D>&, const double*, double*, bool, double*, int*, \
@@ -889,7 +1036,12 @@ void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st
   template void launch_prox<D>(const DeviceMesh<D>&, bool, bool, double, const double*, double*, double*,      \
                                double*, double*, int*, hipStream_t);                                    \
   template void launch_energy<D>(const DeviceMesh<D>&, const double*, double*, int*, hipStream_t);       \
-  template void launch_euler_apply<D>(const DeviceMesh<D>&, const double*, double*, double, hipStream_t);
+  template void launch_euler_apply<D>(const DeviceMesh<D>&, const double*, double*, double, hipStream_t);     \
+  template void launch_fd_jac<D>(const DeviceMesh<D>&, const double*, double, double*, hipStream_t);          \
+  template void launch_jac_assemble<D>(const DeviceMesh<D>&, const int*, const int*, const double*, double,   \
+                                       double*, hipStream_t);                                                 \
+  template void launch_be_residual<D>(const DeviceMesh<D>&, const double*, const double*, const double*,      \
+                                      double, double*, double*, int*, hipStream_t);
 MMX_INST(2)
 MMX_INST(3)
 

@@ -5,7 +5,7 @@ The classes keep the reference's names and argument meaning:
   Mesh(Xp, F, mask, Mon, numThreads, rho, w, tau, integrationMode, gradUse)
                            src/Mesh.h:22-25 (w is ignored: w = 0.5*sqrt(rho), src/Mesh.cpp:451)
   MeshIntegrator(dt, mesh) src/MeshIntegrator.h:12-51: step(nIters, tol), eulerStep(tol),
-                           getEnergy(), done(), outputX/outputZ(fname), proxTime/predTime
+                           backwardsEulerStep(dt, tol), getEnergy(), done(), outputX/outputZ(fname), proxTime/predTime
 Everything runs through the C-ABI in include/mmadmm.h; there is no CPU fallback: importing
 this module fails loudly when the HIP library is missing.
 """
@@ -39,7 +39,8 @@ class mmadmm_stats(ctypes.Structure):
                 ("t_prox_ms", ctypes.c_double), ("t_xupdate_ms", ctypes.c_double),
                 ("t_step_ms", ctypes.c_double), ("n_prox", ctypes.c_longlong),
                 ("n_xupdate", ctypes.c_longlong), ("n_steps_timed", ctypes.c_longlong),
-                ("prox_bytes", ctypes.c_double), ("xupdate_bytes", ctypes.c_double)]
+                ("prox_bytes", ctypes.c_double), ("xupdate_bytes", ctypes.c_double),
+                ("newton_iters", ctypes.c_longlong), ("jacobians", ctypes.c_longlong)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -75,6 +76,10 @@ def lib():
                               ctypes.POINTER(ctypes.c_int)]
     L.mmadmm_euler_step.argtypes = [ctypes.c_void_p, c_double_p]
     L.mmadmm_energy.argtypes = [ctypes.c_void_p, c_double_p]
+    L.mmadmm_backward_euler_step.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, c_double_p,
+                                             ctypes.POINTER(ctypes.c_int)]
+    L.mmadmm_get_jacobian.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), c_int_p, c_int_p,
+                                      c_double_p]
     L.mmadmm_done.argtypes = [ctypes.c_void_p]
     L.mmadmm_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, c_double_p]
     L.mmadmm_get_simplices.argtypes = [ctypes.c_void_p, c_int_p]
@@ -363,6 +368,23 @@ class Engine:
         _check(lib().mmadmm_euler_step(self.h, ctypes.byref(Ih)))
         return Ih.value
 
+    def backwards_euler_step(self, dt, tol=1e-3):
+        """Mesh::backwardsEulerStep (src/Mesh.cpp:1263-1341) -> (Ih, Newton iterations)."""
+        Ih = ctypes.c_double()
+        it = ctypes.c_int()
+        _check(lib().mmadmm_backward_euler_step(self.h, dt, tol, ctypes.byref(Ih), ctypes.byref(it)))
+        return Ih.value, it.value
+
+    def jacobian(self):
+        """The last backward-Euler Jacobian as CSR (ia, ja, a)."""
+        nnz = ctypes.c_longlong()
+        _check(lib().mmadmm_get_jacobian(self.h, ctypes.byref(nnz), None, None, None))
+        ia = np.zeros(self.nP * self.dim + 1, dtype=np.int32)
+        ja = np.zeros(nnz.value, dtype=np.int32)
+        a = np.zeros(nnz.value)
+        _check(lib().mmadmm_get_jacobian(self.h, None, _ip(ia), _ip(ja), _dp(a)))
+        return ia, ja, a
+
     def energy(self):
         E = ctypes.c_double()
         _check(lib().mmadmm_energy(self.h, ctypes.byref(E)))
@@ -431,8 +453,7 @@ class MeshIntegrator:
         return self.engine.euler_step()
 
     def backwardsEulerStep(self, dt, tol):
-        raise NotImplementedError("method 2 (backward Euler + LASolver) runs through mmx_sparse; "
-                                  "see include/mmx_sparse.h")
+        return self.engine.backwards_euler_step(dt, tol)[0]
 
     def getEnergy(self):
         return self.engine.energy()

@@ -5,9 +5,9 @@
 // exactly as main.cpp's main/runAlgo (main.cpp:132-255, 633-907) do, on the MI355X engine through
 // the C-ABI of include/mmadmm.h.
 //
-// Supported: TestType FromFile, SquareGrid, LevelSet (2D); Method 0 (ADMM) and 1 (explicit
-// Euler).  Shoulder (glibc rand + Eigen Random point clouds) and Method 2 (backward Euler) exit
-// with a message.  Extra options: --root DIR (instead of the current directory), --device N,
+// Supported: TestType FromFile, SquareGrid, LevelSet (2D); Method 0 (ADMM), 1 (explicit Euler)
+// and 2 (backward Euler: Newton + ILU(0) CG-STAB).  Shoulder (glibc rand + Eigen Random point
+// clouds) exits with a message.  Extra options: --root DIR (instead of the current directory), --device N,
 // --dry-run (parse and build the mesh on the host only; no GPU).
 #include <sys/stat.h>
 #include <time.h>
@@ -216,11 +216,7 @@ int main(int argc, char** argv) {
     const double dt = cfg.num("dt"), tau = cfg.num("tau"), rho = cfg.num("rho");
     std::cout << "testName " << testName << " TestType " << testType << " Dim " << D << " Method " << methodType
               << std::endl;
-    if (methodType == 2) {
-      std::cerr << "Method 2 (backward Euler) is not available in this build (DESIGN.md §9)" << std::endl;
-      return 2;
-    }
-    if (methodType != 0 && methodType != 1) {
+    if (methodType < 0 || methodType > 2) {
       std::cerr << "unknown Method " << methodType << std::endl;
       return 2;
     }
@@ -290,8 +286,12 @@ int main(int argc, char** argv) {
       if (methodType == 0) {
         int it = 0;
         check(mmadmm_step(h, admmIter, 1e-3, &Ih, &it), "step");
-      } else {
+      } else if (methodType == 1) {
         check(mmadmm_euler_step(h, &Ih), "eulerStep");
+      } else {
+        int newton = 0;
+        check(mmadmm_backward_euler_step(h, dt, 1e-3, &Ih, &newton), "backwardsEulerStep");
+        std::cout << "Newton in " << newton << " iters" << std::endl;
       }
       Ivals.push_back(Ih);
       tVals.push_back(now() - start);

@@ -19,6 +19,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 MONITOR210 = {"TestType": "SquareGrid", "Dim": 2, "MonType": 3, "Method": 0, "CompMesh": False, "BoundaryType": 1,
               "GradUse": False, "nSteps": 1000, "AdmmIter": 10, "DtTol": 1e-4, "dt": 0.025, "tau": 0.5,
               "rho": 1000, "w": 3.53553390593, "nx": 10, "ny": 10, "xa": 0, "xb": 1, "ya": 0, "yb": 1}
+MONITOR220 = dict(MONITOR210, rho=100, nx=20, ny=20)
 MONITOR340 = {"TestType": "FromFile", "MaskFile": "./Experiments/Results/BaseCircle/CircleEx24mask.txt",
               "PntsFile": "./Experiments/Results/BaseCircle/CircleEx24points.txt",
               "TrianglesFile": "./Experiments/Results/BaseCircle/CircleEx24triangles.txt", "Dim": 2, "MonType": 5,
@@ -64,8 +65,14 @@ def test_unsupported_is_reported(tmp_path):
     cfg = dict(MONITOR210, TestType="Shoulder")
     r = _run(_root(tmp_path, "Sh", cfg), "Sh", "0", "1", "--dry-run")
     assert r.returncode == 2 and "not available" in r.stderr
-    r = _run(_root(tmp_path / "m2", "Monitor210", MONITOR210), "Monitor210", "2", "1", "--dry-run")
-    assert r.returncode == 2 and "backward Euler" in r.stderr
+    r = _run(_root(tmp_path / "m3", "Monitor210", MONITOR210), "Monitor210", "3", "1", "--dry-run")
+    assert r.returncode == 2 and "unknown Method" in r.stderr
+
+
+def test_dry_run_backward_euler(tmp_path):
+    r = _run(_root(tmp_path, "Monitor220", MONITOR220), "Monitor220", "2", "1", "--dry-run")
+    assert r.returncode == 0, r.stderr
+    assert "Method 2" in r.stdout
 
 
 def _ih(path):
@@ -97,4 +104,15 @@ def test_monitor340_from_file_matches_reference_trace(tmp_path):
     assert r.returncode == 0, r.stderr
     ours = _ih(root / "Experiments" / "Results" / "Monitor340" / "Ih0.txt")[:, 1]
     ref = ih0("Monitor340")
+    assert len(ours) == len(ref) and (np.abs(ours - ref) / np.abs(ref)).max() < SIX_DIGITS
+
+
+@pytest.mark.gpu
+def test_monitor220_backward_euler_matches_reference_trace(tmp_path):
+    """Method 2 through the driver against the reference's Experiments/Results/Monitor220/Ih2.txt."""
+    root = _root(tmp_path, "Monitor220", MONITOR220)
+    r = _run(root, "Monitor220", "2", "1")
+    assert r.returncode == 0, r.stderr
+    ours = _ih(root / "Experiments" / "Results" / "Monitor220" / "Ih2.txt")[:, 1]
+    ref = np.loadtxt(os.path.join(GOLDEN, "Monitor220", "Ih2.txt"), delimiter=",")[:, 1]
     assert len(ours) == len(ref) and (np.abs(ours - ref) / np.abs(ref)).max() < SIX_DIGITS
