@@ -83,6 +83,10 @@ typedef struct mmadmm_stats {
   double xupdate_bytes;   /* algorithmic HBM bytes of one x-update launch */
   long long newton_iters; /* backward Euler: Newton iterations summed over steps */
   long long jacobians;    /* backward Euler: FD Jacobian builds */
+  long long cg_iters;     /* backward Euler: CG-STAB iterations summed over Newton iterations */
+  double t_jac_ms;        /* backward Euler: wall time in Jacobian builds (FD + assembly) */
+  double t_solve_ms;      /* backward Euler: wall time in the linear solves (ILU(0) + CG-STAB) */
+  double t_be_ms;         /* backward Euler: wall time of whole steps */
 } mmadmm_stats;
 
 const char* mmadmm_last_error(void);

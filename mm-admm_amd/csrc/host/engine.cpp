@@ -4,6 +4,7 @@
 // All per-step work runs on the device on one HIP stream; the host only launches kernels and,
 // with the early exit enabled, reads back three scalars per ADMM iteration.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -260,6 +261,7 @@ class Engine final : public EngineBase {
     }
     // Mesh::updateAfterStep: Vp = x
     MMX_HIP(hipMemcpyAsync(Vp_.p, x_.p, (size_t)nP_ * D * sizeof(double), hipMemcpyDeviceToDevice, st_));
+    vpVersion_++;
     if (timing) {
       eStep1 = nextEvent();
       MMX_HIP(hipEventRecord(eStep1, st_));
@@ -327,6 +329,7 @@ class Engine final : public EngineBase {
   // Newton iteration of the run and again whenever ||F||_1 stagnates (ratio < 0.25).
   double backwardEulerStep(double dtBE, double tol, int* newtonOut) override {
     if (nranks_ > 1) throw Error(MMADMM_ERR_INVALID, "backward Euler runs on one rank (no element partition)");
+    const auto tStep = Clock::now();
     const int n = nP_ * D;
     ensureJacobian();
     const double dtot = dtBE / prm_.tau;
@@ -356,10 +359,13 @@ class Engine final : public EngineBase {
         beStepTaken_ = true;
       }
       MMX_HIP(hipStreamSynchronize(st_));  // rhs and the Jacobian values are ready for the solver stream
+      const auto tSolve = Clock::now();
       MMX_SP(mmx_matrix_set_rhs_device(jac_, rhs_.p));
       int cgIter = 0;
       MMX_SP(mmx_matrix_solve_device(jac_, &jprm_, dx_.p, &cgIter, 0));
       MMX_HIP(hipStreamSynchronize((hipStream_t)mst));
+      st_stats_.t_solve_ms += msSince(tSolve);
+      if (cgIter > 0) st_stats_.cg_iters += cgIter;
       if (cgIter <= 0)
         throw Error(MMADMM_ERR_NOCONV, "backward Euler: CG-STAB did not converge (reference: assert(cgIter > 0))");
       launch_add_inplace(n, x_.p, dx_.p, st_);
@@ -369,6 +375,7 @@ class Engine final : public EngineBase {
     MMX_HIP(hipStreamSynchronize(st_));
     st_stats_.steps += 1;
     st_stats_.newton_iters += nIter;
+    st_stats_.t_be_ms += msSince(tStep);
     if (newtonOut) *newtonOut = nIter;
     return Ih;
   }
@@ -394,6 +401,7 @@ class Engine final : public EngineBase {
 
   void done() override {
     MMX_HIP(hipMemcpyAsync(Vp_.p, x_.p, (size_t)nP_ * D * sizeof(double), hipMemcpyDeviceToDevice, st_));
+    vpVersion_++;
     MMX_HIP(hipStreamSynchronize(st_));
   }
 
@@ -503,8 +511,15 @@ class Engine final : public EngineBase {
     MMX_HIP(hipStreamSynchronize(st_));
   }
 
-  // buildEulerJac (src/Mesh.cpp:1112-1136); sfac after the first build (src/Mesh.cpp:1287-1290)
+  // buildEulerJac (src/Mesh.cpp:1112-1136); sfac after the first build (src/Mesh.cpp:1287-1290).
+  // The Jacobian is evaluated at Vp, which only step() and done() move: a rebuild with the same
+  // Vp and dt reproduces the current values bit for bit and is skipped (and so is the solver's
+  // re-factorisation of unchanged values).
   void buildJacobian(double dtBE) {
+    if (jacVp_ == vpVersion_ && jacDt_ == dtBE) return;
+    jacVp_ = vpVersion_;
+    jacDt_ = dtBE;
+    const auto t0 = Clock::now();
     const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
     launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
     launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, dtBE / prm_.tau, jval_.p, st_);
@@ -514,7 +529,13 @@ class Engine final : public EngineBase {
       MMX_SP(mmx_matrix_sfac(jac_, &jprm_));
       jacFactored_ = true;
     }
+    MMX_HIP(hipStreamSynchronize(st_));
     st_stats_.jacobians += 1;
+    st_stats_.t_jac_ms += msSince(t0);
+  }
+  using Clock = std::chrono::steady_clock;
+  static double msSince(Clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
   }
 
   static double hostDet(const double (&a)[3][3]) {  // Eigen 2x2 / 3x3 determinant
@@ -641,6 +662,8 @@ class Engine final : public EngineBase {
   mmx_matrix jac_ = nullptr;
   mmx_param_iter jprm_{};
   bool beStepTaken_ = false, jacFactored_ = false;
+  long long vpVersion_ = 0, jacVp_ = -1;  // Vp generation; the one the Jacobian was built at
+  double jacDt_ = 0.0;
   DevBuf<int32_t> jia_, jja_;
   DevBuf<double> jval_, dv_, xn_, rhs_, dx_;
   int stepsTaken_ = 0;

@@ -27,7 +27,7 @@ struct Struc {
     ia.assign(n + 1, 0);
     for (int i = 0; i < n; ++i) {
       auto& r = rows[i];
-      std::sort(r.begin(), r.end());
+      if (!std::is_sorted(r.begin(), r.end())) std::sort(r.begin(), r.end());
       r.erase(std::unique(r.begin(), r.end()), r.end());
       ia[i + 1] = ia[i] + (int)r.size();
     }
@@ -46,6 +46,23 @@ struct Struc {
 }  // namespace
 void symbolic_ilu(int n, const std::vector<int>& ia, const std::vector<int>& ja, int level, std::vector<int>& iaf,
                   std::vector<int>& jaf, std::vector<int>& dgRel) {
+  if (level == 0) {  // no fill can reach level 0 (levnew >= 1): the pattern of A, rows sorted
+    iaf.assign(ia.begin(), ia.begin() + n + 1);
+    jaf.assign(ja.begin(), ja.begin() + ia[n]);
+    dgRel.assign(n, -1);
+    for (int i = 0; i < n; ++i) {
+      int* b = jaf.data() + iaf[i];
+      int* e = jaf.data() + iaf[i + 1];
+      if (b == e) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " is empty (no diagonal)");
+      std::sort(b, e);
+      for (int* q = b + 1; q < e; ++q)
+        if (*q == q[-1]) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has duplicate columns");
+      int* d = std::lower_bound(b, e, i);
+      if (d == e || *d != i) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has no diagonal entry");
+      dgRel[i] = (int)(d - b);
+    }
+    return;
+  }
   const int END = n + 1, MAXINT = 2 * n;
   std::vector<int> list(n, END), lrow(n, MAXINT), tmp;
   std::vector<std::vector<int>> rj(n), rl(n);
@@ -153,6 +170,9 @@ struct SparseMatrix {
   DevBuf<unsigned> d_flags, d_ctl;  // ctl: 8 tickets, err, pad (16-byte multiple)
   DevBuf<uint64_t> d_gy, d_gx;
   unsigned epoch = 0, fepoch = 0;
+  // numeric factor cache: the ILU of unchanged values is the same, so a solve re-factors only
+  // after set_values / sfac (the reference re-factors in every solve, MatrixIter.cpp:684)
+  long long valVersion = 0, factVersion = -1;
   // CG-STAB vectors
   DevBuf<double> d_res, d_res0, d_p, d_vbar, d_avbar, d_s, d_z, d_t, d_x, d_part, d_tmp;
   DevBuf<CgsScalars> d_sc;
@@ -233,6 +253,7 @@ struct SparseMatrix {
     d_dg.upload(dg.data(), dg.size(), st);
     d_amap.upload(amap.data(), std::max<size_t>(amap.size(), 1), st);
     d_af.alloc(std::max<size_t>(jaf.size(), 1));
+    factVersion = -1;
     {  // pivot-row upper ranges of every lower entry (the factor's dependent loads, precomputed)
       std::vector<int2> pv(std::max<size_t>(jaf.size(), 1), make_int2(0, 0));
       for (int i = 0; i < n; ++i)
@@ -290,13 +311,16 @@ struct SparseMatrix {
     MMX_HIP(hipMemcpyAsync(&e, errw(), sizeof(unsigned), hipMemcpyDeviceToHost, st));
     MMX_HIP(hipStreamSynchronize(st));
     if (e) {
+      factVersion = -1;
       MMX_HIP(hipMemsetAsync(errw(), 0, sizeof(unsigned), st));
       throw Error(MMADMM_ERR_HIP, "sync-free ILU dependency wait gave up (code " + std::to_string(e) + ")");
     }
   }
 
-  void factor() {
+  void factor(bool force = true) {
     if (!symbolic) throw Error(MMADMM_ERR_INVALID, "error: solve called with no symbolic ILU");
+    if (!force && factVersion == valVersion) return;
+    factVersion = valVersion;
     MMX_HIP(hipMemsetAsync(tickets(), 0, 8 * sizeof(unsigned), st));
     if (++fepoch == 0) {
       MMX_HIP(hipMemsetAsync(d_flags.p, 0, sizeof(unsigned) * n, st));
@@ -363,7 +387,7 @@ struct SparseMatrix {
       tm[3].init();
       MMX_HIP(hipEventRecord(tm[3].a, st));
     }
-    factor();
+    factor(false);
     const int gv = vec_grid(n);
     if (initial_guess == 0) {
       launch_cgs_init(0, n, d_b.p, d_xout, d_res.p, d_res0.p, d_p.p, d_avbar.p, p.new_rhat == 0, d_part.p, st);
@@ -512,24 +536,29 @@ int mmx_struc_mesh_pattern(mmx_struc s, int dim, int nF, const int32_t* F) {
     if (s->s.packed) throw Error(MMADMM_ERR_INVALID, "error: data structure already compressed");
     const int D = dim, nP = s->s.n / D;
     if (nP * D != s->s.n) throw Error(MMADMM_ERR_INVALID, "structure size is not dim * nodes");
-    // node adjacency first (every vertex pair of every simplex), then D x D blocks
-    std::vector<std::vector<int>> nb(nP);
+    // node adjacency first (every vertex pair of every simplex, flat CSR), then D x D blocks
+    std::vector<int> cnt(nP + 1, 0);
+    for (long long k = 0; k < (long long)nF * (D + 1); ++k) {
+      const int va = F[k];
+      if (va < 0 || va >= nP) throw Error(MMADMM_ERR_INVALID, "simplex vertex out of range");
+      cnt[va + 1] += D + 1;
+    }
+    for (int v = 0; v < nP; ++v) cnt[v + 1] += cnt[v];
+    std::vector<int> nb(cnt[nP]), fill(cnt.begin(), cnt.end() - 1);
     for (int t = 0; t < nF; ++t)
       for (int a = 0; a <= D; ++a) {
         const int va = F[(size_t)t * (D + 1) + a];
-        if (va < 0 || va >= nP) throw Error(MMADMM_ERR_INVALID, "simplex vertex out of range");
-        for (int b = 0; b <= D; ++b) nb[va].push_back(F[(size_t)t * (D + 1) + b]);
+        for (int b = 0; b <= D; ++b) nb[fill[va]++] = F[(size_t)t * (D + 1) + b];
       }
     for (int v = 0; v < nP; ++v) {
-      auto& l = nb[v];
-      std::sort(l.begin(), l.end());
-      l.erase(std::unique(l.begin(), l.end()), l.end());
+      int* b = nb.data() + cnt[v];
+      int* e = std::unique(b, (std::sort(b, nb.data() + cnt[v + 1]), nb.data() + cnt[v + 1]));
       for (int d = 0; d < D; ++d) {
         auto& r = s->s.rows[v * D + d];
-        for (int u : l)
-          for (int e = 0; e < D; ++e) r.push_back(u * D + e);
+        r.reserve(r.size() + (size_t)(e - b) * D);
+        for (const int* u = b; u < e; ++u)
+          for (int c = 0; c < D; ++c) r.push_back(*u * D + c);
       }
-      std::vector<int>().swap(l);
     }
   });
 }
@@ -613,6 +642,7 @@ int mmx_matrix_set_values(mmx_matrix m, const double* a) {
     MMX_M(m);
     if (!a && M.nnz) throw Error(MMADMM_ERR_INVALID, "null values");
     MMX_HIP(hipMemcpyAsync(M.d_a.p, a, sizeof(double) * M.nnz, hipMemcpyHostToDevice, M.st));
+    M.valVersion++;
     MMX_HIP(hipStreamSynchronize(M.st));
   });
 }
@@ -622,6 +652,7 @@ int mmx_matrix_set_values_device(mmx_matrix m, const double* d_a) {
     MMX_M(m);
     if (!d_a && M.nnz) throw Error(MMADMM_ERR_INVALID, "null values");
     MMX_HIP(hipMemcpyAsync(M.d_a.p, d_a, sizeof(double) * M.nnz, hipMemcpyDeviceToDevice, M.st));
+    M.valVersion++;
   });
 }
 

@@ -40,7 +40,9 @@ class mmadmm_stats(ctypes.Structure):
                 ("t_step_ms", ctypes.c_double), ("n_prox", ctypes.c_longlong),
                 ("n_xupdate", ctypes.c_longlong), ("n_steps_timed", ctypes.c_longlong),
                 ("prox_bytes", ctypes.c_double), ("xupdate_bytes", ctypes.c_double),
-                ("newton_iters", ctypes.c_longlong), ("jacobians", ctypes.c_longlong)]
+                ("newton_iters", ctypes.c_longlong), ("jacobians", ctypes.c_longlong),
+                ("cg_iters", ctypes.c_longlong), ("t_jac_ms", ctypes.c_double), ("t_solve_ms", ctypes.c_double),
+                ("t_be_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
