@@ -69,6 +69,8 @@ typedef struct mmx_sparse_stats {
   long long n_spmv_timed, n_sweep_timed, n_factor_timed;
   double spmv_bytes;  /* algorithmic bytes of one SpMV: 12 nnz + 4 (n+1) + 16 n */
   double last_rms, rmsi;
+  int sweep_mode;     /* triangular sweeps: 0 level-scheduled, 1 chain/band-scheduled */
+  int sweep_e;        /* chain sweeps: entry slots per row (8, 16, 32) */
 } mmx_sparse_stats;
 
 void mmx_param_iter_default(mmx_param_iter* p);
@@ -115,6 +117,14 @@ int mmx_matrix_destroy(mmx_matrix m);
  * and diag (n, row-relative). */
 int mmx_ilu_symbolic(int n, const int32_t* ia, const int32_t* ja, int level, long long* nnzf, int32_t* iaf,
                      int32_t* jaf, int32_t* diag);
+
+/* Diagnostics (host only): the chain/band schedule the sweeps would use for the ILU(level) of this
+ * pattern.  info[16]: ok, E, R, RI, bands, chains, max chain length,
+ * max skew, max band iterations, slots, imports, simulated critical iterations, levels. */
+/* Cycle counters of the chain sweeps when MMX_CHAIN_PROF=1 was set before sfac (1024 values:
+ * forward 0..511, backward 512..1023; layout in chain_sweep.hip); reset != 0 zeroes them. */
+int mmx_matrix_chain_prof(mmx_matrix m, unsigned long long* out, int reset);
+int mmx_sweep_schedule_info(int n, const int32_t* ia, const int32_t* ja, int level, int fwd, long long* info);
 
 #ifdef __cplusplus
 }

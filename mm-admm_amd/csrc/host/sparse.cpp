@@ -9,6 +9,7 @@
 
 #include "../../../include/mmx_sparse.h"
 #include "../kernels/sparse_kernels.h"
+#include "chain_sched.h"
 #include "common.h"
 
 namespace mmx {
@@ -170,6 +171,19 @@ struct SparseMatrix {
   DevBuf<unsigned> d_flags, d_ctl;  // ctl: 8 tickets, err, pad (16-byte multiple)
   DevBuf<uint64_t> d_gy, d_gx;
   unsigned epoch = 0, fepoch = 0;
+  // chain/band-scheduled sweeps (host/chain_sched.h); level-scheduled when a schedule is not
+  // possible (a triangle row wider than 32 entries) or MMX_SWEEP=level
+  struct ChainDir {
+    int E = 0;
+    long long nent = 0, nslot = 0;
+    DevBuf<int> bandSlot, bandT, bandImp, bandNImp, bandE, laneStart, laneLen, laneSkew, code, src, dsrc, impRow,
+        impFree, impNeed;
+    DevBuf<double> val, dval;
+    ChainArgs args{};
+  };
+  ChainDir chf, chb;
+  bool useChain = false;
+  DevBuf<unsigned long long> d_cprof;  // MMX_CHAIN_PROF: 2 x 512 counters (forward, backward)
   // numeric factor cache: the ILU of unchanged values is the same, so a solve re-factors only
   // after set_values / sfac (the reference re-factors in every solve, MatrixIter.cpp:684)
   long long valVersion = 0, factVersion = -1;
@@ -287,9 +301,58 @@ struct SparseMatrix {
     };
     schedule(true, d_permf, nchf, nlevf);
     schedule(false, d_permb, nchb, nlevb);
+    useChain = false;
+    const char* mode = getenv("MMX_SWEEP");
+    if (!(mode && std::strcmp(mode, "level") == 0)) {
+      const ChainSchedule F = build_chain_schedule(n, iaf, jaf, dg, true);
+      const ChainSchedule B = F.ok ? build_chain_schedule(n, iaf, jaf, dg, false) : ChainSchedule();
+      if (F.ok && B.ok) {
+        upload_chain(F, chf);
+        upload_chain(B, chb);
+        useChain = true;
+      }
+    }
     MMX_HIP(hipStreamSynchronize(st));
     MMX_HIP(hipStreamSynchronize(st));
     symbolic = true;
+  }
+
+  void upload_chain(const ChainSchedule& S, ChainDir& c) {
+    auto up = [&](DevBuf<int>& d, const std::vector<int>& h) {
+      if (h.empty()) {
+        const int z = 0;
+        d.upload(&z, 1, st);
+      } else {
+        d.upload(h.data(), h.size(), st);
+      }
+    };
+    up(c.bandSlot, S.bandSlot);
+    up(c.bandT, S.bandT);
+    up(c.bandImp, S.bandImp);
+    up(c.bandNImp, S.bandNImp);
+    up(c.laneStart, S.laneStart);
+    up(c.laneLen, S.laneLen);
+    up(c.laneSkew, S.laneSkew);
+    up(c.code, S.code);
+    up(c.src, S.src);
+    up(c.dsrc, S.dsrc);
+    up(c.impRow, S.impRow);
+    up(c.impFree, S.impFree);
+    up(c.impNeed, S.impNeed);
+    up(c.bandE, S.bandE);
+    c.E = S.E;
+    c.nent = (long long)S.code.size();
+    c.nslot = (long long)S.dsrc.size();
+    c.val.alloc(std::max<long long>(c.nent, 1));
+    c.dval.alloc(std::max<long long>(c.nslot, 1));
+    const char* pe = getenv("MMX_CHAIN_PROF");
+    if (pe && atoi(pe) && !d_cprof.p) {
+      d_cprof.alloc(1024);
+      MMX_HIP(hipMemsetAsync(d_cprof.p, 0, 1024 * sizeof(unsigned long long), st));
+    }
+    c.args = ChainArgs{c.bandSlot.p, c.bandT.p, c.bandImp.p, c.bandNImp.p, c.laneStart.p, c.laneLen.p, c.laneSkew.p,
+                       c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impFree.p, c.impNeed.p, S.nbands, S.R, S.RI,
+                       d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr};
   }
 
   void begin(int t) {
@@ -329,6 +392,11 @@ struct SparseMatrix {
     begin(2);
     launch_ilu_factor(d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_permf.p, nchf, d_af.p,
                       d_flags.p, fepoch, tickets(), errw(), st);
+    if (useChain) {  // the sweeps read the factor's entries in schedule order
+      launch_chain_fill(chf.nent, chf.src.p, d_af.p, chf.val.p, 0.0, st);
+      launch_chain_fill(chb.nent, chb.src.p, d_af.p, chb.val.p, 0.0, st);
+      launch_chain_fill(chb.nslot, chb.dsrc.p, d_af.p, chb.dval.p, 1.0, st);
+    }
     MMX_HIP(hipGetLastError());
     const float ms = end(2);
     stats.factors++;
@@ -351,11 +419,19 @@ struct SparseMatrix {
   void ilu_apply(int pro, const double* src, double* p, double* out, unsigned* tk) {
     begin(1);
     const unsigned ey = next_epoch();
-    launch_sweep(true, pro, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permf.p, nchf, src, p, d_res.p, d_avbar.p, d_sc.p,
-                 nullptr, d_gy.p, nullptr, ey, tk, errw(), st);
+    if (useChain)
+      launch_chain_sweep(true, pro, chf.E, chf.args, src, p, d_res.p, d_avbar.p, d_sc.p, nullptr, d_gy.p, nullptr, ey,
+                         tk, errw(), st);
+    else
+      launch_sweep(true, pro, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permf.p, nchf, src, p, d_res.p, d_avbar.p, d_sc.p,
+                   nullptr, d_gy.p, nullptr, ey, tk, errw(), st);
     const unsigned ex = next_epoch();
-    launch_sweep(false, 0, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permb.p, nchb, nullptr, nullptr, nullptr, nullptr, nullptr,
-                 d_gy.p, d_gx.p, out, ex, tk + 1, errw(), st);
+    if (useChain)
+      launch_chain_sweep(false, 0, chb.E, chb.args, nullptr, nullptr, nullptr, nullptr, nullptr, d_gy.p, d_gx.p, out, ex,
+                         tk + 1, errw(), st);
+    else
+      launch_sweep(false, 0, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permb.p, nchb, nullptr, nullptr, nullptr, nullptr,
+                   nullptr, d_gy.p, d_gx.p, out, ex, tk + 1, errw(), st);
     MMX_HIP(hipGetLastError());
     const float ms = end(1);
     stats.sweeps += 2;
@@ -799,7 +875,22 @@ int mmx_matrix_set_timing(mmx_matrix m, int on) {
 int mmx_matrix_stats_get(mmx_matrix m, mmx_sparse_stats* out) {
   return guarded([&] {
     MMX_M(m);
-    if (out) *out = M.stats;
+    if (out) {
+      *out = M.stats;
+      out->sweep_mode = M.useChain ? 1 : 0;
+      out->sweep_e = M.useChain ? M.chf.E : 0;
+    }
+  });
+}
+
+int mmx_matrix_chain_prof(mmx_matrix m, unsigned long long* out, int reset) {
+  return guarded([&] {
+    MMX_M(m);
+    if (!M.d_cprof.p) throw Error(MMADMM_ERR_INVALID, "chain profiling off (set MMX_CHAIN_PROF=1 before sfac)");
+    if (out)
+      MMX_HIP(hipMemcpyAsync(out, M.d_cprof.p, 1024 * sizeof(unsigned long long), hipMemcpyDeviceToHost, M.st));
+    if (reset) MMX_HIP(hipMemsetAsync(M.d_cprof.p, 0, 1024 * sizeof(unsigned long long), M.st));
+    MMX_HIP(hipStreamSynchronize(M.st));
   });
 }
 
@@ -822,6 +913,34 @@ int mmx_ilu_symbolic(int n, const int32_t* ia, const int32_t* ja, int level, lon
     if (iaf) std::memcpy(iaf, fia.data(), sizeof(int) * (n + 1));
     if (jaf) std::memcpy(jaf, fja.data(), sizeof(int) * fja.size());
     if (diag) std::memcpy(diag, dg.data(), sizeof(int) * n);
+  });
+}
+
+int mmx_sweep_schedule_info(int n, const int32_t* ia, const int32_t* ja, int level, int fwd, long long* info) {
+  return guarded([&] {
+    if (n <= 0 || !ia || !ja || level < 0 || !info) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    std::vector<int> via(ia, ia + n + 1), vja(ja, ja + ia[n]), fia, fja, dgRel;
+    mmx::symbolic_ilu(n, via, vja, level, fia, fja, dgRel);
+    std::vector<int> dg(n);
+    for (int i = 0; i < n; ++i) dg[i] = fia[i] + dgRel[i];
+    const mmx::ChainSchedule S = mmx::build_chain_schedule(n, fia, fja, dg, fwd != 0);
+    int nlev = 0;
+    {
+      std::vector<int> lev(n, 0);
+      for (int t = 0; t < n; ++t) {
+        const int i = fwd ? t : n - 1 - t;
+        int l = 0;
+        const int kb = fwd ? fia[i] : dg[i] + 1, ke = fwd ? dg[i] : fia[i + 1];
+        for (int k = kb; k < ke; ++k) l = std::max(l, lev[fja[k]] + 1);
+        lev[i] = l;
+        nlev = std::max(nlev, l + 1);
+      }
+    }
+    const std::string bad = S.ok ? mmx::validate_chain_schedule(S, n, fia, fja, dg) : std::string();
+    if (!bad.empty()) throw Error(MMADMM_ERR_INVALID, "chain schedule invalid: " + bad);
+    const long long v[16] = {S.ok ? 1 : 0, S.E, S.R, S.RI, S.nbands, S.nchains, S.maxLen, S.maxSkew,
+                             S.maxT, S.slots, S.nImports, S.estIters, nlev, 0, 0, 0};
+    std::memcpy(info, v, sizeof(v));
   });
 }
 

@@ -1,0 +1,389 @@
+// chain_sweep.hip -- band/chain-scheduled ILU triangular sweeps (scaler_ILU::solve,
+// lib/LASolver/ILU_class.cpp:470-499) for gfx950.  Schedule: host/chain_sched.h.
+//
+// One workgroup runs one band (64 chains) at a time, four wavefronts:
+//   wave 0  compute: lane l computes position t - skew[l] of its chain at iteration t; every
+//           entry carries the LDS index of its value: the zero cell (pads), a lane's ring slot
+//           (static schedule: written at an earlier iteration, not yet overwritten) or an import
+//           slot (delivered once the importer's counter passes the iteration's impNeed);
+//   wave 1,2 loaders: global -> LDS DMA (global_load_lds) of the matrix entries, their codes and
+//           the right-hand-side operands of iteration t into stage t % DL (even / odd t), each
+//           keeping several stages in flight against its own vmcnt;
+//   wave 3  importer: polls the producers' global granules (agent scope) of the band's imports in
+//           order of first use, stores each into its slot once the slot is free and publishes the
+//           length of the delivered prefix.
+// Every row is x_i = (b_i - sum_k a_k x_jk) [/ d_i] with the terms subtracted in ascending column
+// order, exactly as the level-scheduled k_sweep and the reference.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sparse_kernels.h"
+
+namespace mmx {
+namespace {
+
+#define MMX_LDS __attribute__((address_space(3)))
+
+constexpr int kPad = -2147483647 - 1;
+constexpr int kRingMax = 32;    // = kChainRingMax (host/chain_sched.h)
+constexpr int kImpMax = 1024;   // = kChainImpMax
+constexpr unsigned kChainSpinMax = 1u << 22;
+
+template <typename T>
+__device__ __forceinline__ unsigned lds_off(T* p) {
+  return (unsigned)(size_t)(MMX_LDS T*)p;
+}
+// LDS word access the compiler does not track: the loaders' tag stores must not wait for their
+// own in-flight DMA (the compiler would insert vmcnt(0) before any tracked LDS access).
+__device__ __forceinline__ int lds_read(const int* p) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_off(p)) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_write(int* p, int v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void dma16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (MMX_LDS void*)lds_base, 16, 0, 0);
+}
+__device__ __forceinline__ void dma4(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (MMX_LDS void*)lds_base, 4, 0, 0);
+}
+// s_waitcnt vmcnt(N) through the builtin, so the compiler's waitcnt pass knows the DMA has landed
+// (an inline-asm wait is opaque to it and it would add vmcnt(0) before later LDS reads)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+__device__ __forceinline__ double join_words(uint32_t lo, uint32_t hi) {
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// stage geometry
+template <int E>
+struct Geo {
+  static constexpr int DL = (E <= 16) ? 8 : 4;  // stages in the LDS ring
+};
+template <bool FWD, int PRO>
+struct AuxN {  // DMA instructions for the right-hand-side operands of one stage (+1: impNeed)
+  static constexpr int n = (FWD ? (PRO == 0 ? 2 : PRO == 1 ? 6 : 4) : 2) + 1;  // bwd: y granule + diagonal
+};
+constexpr int kAuxWords = 448;  // per stage: operands (<= 384 words) + impNeed (64 copies)
+constexpr int kDepCells = 1 + 64 * (kRingMax + 1) + kImpMax;
+
+// abort protocol: a bounded wait that gives up sets err; everyone polls err now and then
+__device__ __forceinline__ bool aborted(unsigned* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+__device__ __forceinline__ bool spin(unsigned& spins, unsigned* err, unsigned code) {
+  if ((++spins & 255u) == 0 && aborted(err)) return false;
+  if (spins > kChainSpinMax) {
+    atomicOr(err, code);
+    return false;
+  }
+  __builtin_amdgcn_s_sleep(1);
+  return true;
+}
+
+// profiling counters (ca.prof, s_memtime cycles): 0 compute cycles, 1 compute waiting for stages,
+// 2 compute waiting for imports, 3 compute iterations, 4 loader flush waits, 5 loader slot waits,
+// 6 loader in-flight waits, 7 importer cycles, 8 bands; 16 + 4 i + {0 total, 1 stage wait,
+// 2 import wait, 3 iterations} for the first 32 (i = b) and the last 32 bands (i = 64 + b - nbands)
+__device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ void prof_add(unsigned long long* prof, int i, unsigned long long v) {
+  if (prof) atomicAdd(prof + i, v);
+}
+
+template <bool FWD, int PRO, int E>
+__global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double* __restrict__ src,
+                                                     double* __restrict__ pvec, const double* __restrict__ res,
+                                                     const double* __restrict__ avbar, const CgsScalars* __restrict__ sc,
+                                                     const uint64_t* __restrict__ gin, uint64_t* gout,
+                                                     double* __restrict__ out, unsigned epoch, unsigned* ticket,
+                                                     unsigned* err) {
+  constexpr int DL = Geo<E>::DL;
+  constexpr int NAUX = AuxN<FWD, PRO>::n;
+  constexpr int NI = E / 2 + E / 4 + NAUX;          // DMA instructions per stage
+  constexpr int LAG0 = 63 / NI < 1 ? 1 : 63 / NI;
+  constexpr int LAG = LAG0 < DL / 2 ? LAG0 : DL / 2;  // own stages in flight per loader
+  __shared__ double s_val[DL * E * 64];
+  __shared__ int s_code[DL * E * 64];
+  __shared__ uint32_t s_aux[DL * kAuxWords];
+  __shared__ double s_dep[kDepCells];  // [0] = +0.0, lane rings, import slots
+  __shared__ int s_tag[DL];
+  __shared__ int s_prog, s_band, s_impDone;
+
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int R = ca.R, RI = ca.RI;
+  const int impBase = 1 + 64 * (R + 1);
+  double beta = 0.0, omega = 0.0, alpha = 0.0;
+  if (FWD && PRO == 1) {
+    beta = sc->beta;
+    omega = sc->omega;
+  }
+  if (FWD && PRO == 2) alpha = sc->alpha;
+
+  while (true) {
+    if (tid == 0) {
+      s_band = (int)atomicAdd(ticket, 1u);
+      s_prog = 0;
+      s_impDone = 0;
+      s_dep[0] = 0.0;
+    }
+    if (tid < DL) s_tag[tid] = -1;
+    __syncthreads();
+    const int b = s_band;
+    if (b >= ca.nbands) break;
+    const bool skip = aborted(err);
+    const int sb = ca.bandSlot[b], T = ca.bandT[b];
+    const int g = b * 64 + lane;
+    int cst = ca.laneStart[g], len = ca.laneLen[g], skew = ca.laneSkew[g];
+    // launder the loaded lane values: inside the loops they must not count as pending loads, or the
+    // waitcnt pass waits for every younger store/DMA (vmcnt(0)) at each iteration
+    asm volatile("" : "+v"(cst), "+v"(len), "+v"(skew));
+
+    if (skip) {
+      // nothing: an earlier wait gave up; the host reports it
+    } else if (wave == 0) {
+      // ---------------- compute ----------------
+      const int Eb = ca.bandE[b];
+      wait_vm<0>();  // nothing in flight here; tells the waitcnt pass so the loop needs no vmcnt waits
+      unsigned long long c0 = ca.prof ? clk() : 0, cstage = 0, cimp = 0;
+      for (int t = 0; t < T; ++t) {
+        const int st = t & (DL - 1);
+        unsigned spins = 0;
+        bool ok = true;
+        const unsigned long long w0 = ca.prof ? clk() : 0;
+        while (lds_read(&s_tag[st]) != t)
+          if (!(ok = spin(spins, err, 8u))) break;
+        if (ca.prof) cstage += clk() - w0;
+        if (!ok) break;
+        const uint32_t* sa = s_aux + st * kAuxWords;
+        const int need = __builtin_amdgcn_readfirstlane((int)sa[384 + lane]);
+        if (need >= 0) {  // imports this iteration reads: wait for their delivery
+          const unsigned long long i0 = ca.prof ? clk() : 0;
+          while (lds_read(&s_impDone) <= need)
+            if (!(ok = spin(spins, err, 16u))) break;
+          if (ca.prof) cimp += clk() - i0;
+          if (!ok) break;
+        }
+        const int p = t - skew;
+        if (p >= 0 && p < len) {
+          const int row = FWD ? cst + p : cst - p;
+          const double* sv = s_val + st * E * 64;
+          const int* scd = s_code + st * E * 64;
+          double init;
+          if (FWD) {
+            const double r0 = join_words(sa[lane], sa[64 + lane]);
+            if (PRO == 0) {
+              init = r0;
+            } else if (PRO == 1) {
+              const double pv = join_words(sa[128 + lane], sa[192 + lane]);
+              const double av = join_words(sa[256 + lane], sa[320 + lane]);
+              init = r0 + beta * (pv - omega * av);
+            } else {
+              const double av = join_words(sa[128 + lane], sa[192 + lane]);
+              init = r0 - alpha * av;
+            }
+          } else {
+            init = join_words(sa[4 * lane], sa[4 * lane + 2]);  // granule {tag|lo, tag|hi}
+          }
+          // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
+          double acc = init;
+#pragma unroll
+          for (int e0 = 0; e0 < E; e0 += 4) {
+            if (e0 < Eb) {
+              double a[4], v[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                a[q] = sv[(e0 + q) * 64 + lane];
+                v[q] = s_dep[scd[(e0 + q) * 64 + lane]];
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc -= a[q] * v[q];
+            }
+          }
+          if (!FWD) acc = acc / join_words(sa[256 + 2 * lane], sa[256 + 2 * lane + 1]);
+          s_dep[1 + lane * (R + 1) + (p & (R - 1))] = acc;
+          const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
+          __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!FWD) out[row] = acc;
+          if (FWD && PRO != 0) pvec[row] = init;
+        }
+        if (lane == 0) lds_write(&s_prog, t + 1);
+      }
+      if (ca.prof && lane == 0) {
+        const unsigned long long tot = clk() - c0;
+        prof_add(ca.prof, 0, tot);
+        prof_add(ca.prof, 1, cstage);
+        prof_add(ca.prof, 2, cimp);
+        prof_add(ca.prof, 3, (unsigned long long)T);
+        prof_add(ca.prof, 8, 1ull);
+        const int pi = b < 32 ? b : (b >= ca.nbands - 32 ? 64 + b - ca.nbands : -1);
+        if (pi >= 0) {
+          prof_add(ca.prof, 16 + 4 * pi, tot);
+          prof_add(ca.prof, 16 + 4 * pi + 1, cstage);
+          prof_add(ca.prof, 16 + 4 * pi + 2, cimp);
+          prof_add(ca.prof, 16 + 4 * pi + 3, (unsigned long long)T);
+        }
+      }
+    } else if (wave <= 2) {
+      // ---------------- loaders (stages t = w, w+2, ...) ----------------
+      const int w = wave - 1;
+      int nextPub = w;
+      bool ok = true;
+      unsigned long long cfl = 0, csl = 0, cin = 0;
+      for (int t = w; t < T && ok; t += 2) {
+        const int st = t & (DL - 1);
+        if (lds_read(&s_prog) < t - DL + 1) {  // slot busy: publish what is in flight, then wait
+          const unsigned long long f0 = ca.prof ? clk() : 0;
+          wait_vm<0>();
+          if (ca.prof) cfl += clk() - f0;
+          for (; nextPub < t; nextPub += 2)
+            if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
+          unsigned spins = 0;
+          const unsigned long long s0 = ca.prof ? clk() : 0;
+          while (lds_read(&s_prog) < t - DL + 1)
+            if (!(ok = spin(spins, err, 32u))) break;
+          if (ca.prof) csl += clk() - s0;
+          if (!ok) break;
+        }
+        const size_t slot = (size_t)(sb + t);
+        const double* gv = ca.val + slot * E * 64;
+#pragma unroll
+        for (int i = 0; i < E / 2; ++i) dma16(gv + i * 128 + lane * 2, s_val + st * E * 64 + i * 128);
+        const int* gc = ca.code + slot * E * 64;
+#pragma unroll
+        for (int i = 0; i < E / 4; ++i) dma16(gc + i * 256 + lane * 4, s_code + st * E * 64 + i * 256);
+        const int p = t - skew;
+        const int row = (p >= 0 && p < len) ? (FWD ? cst + p : cst - p) : 0;
+        uint32_t* sa = s_aux + st * kAuxWords;
+        if (FWD) {
+          const double* v0 = (PRO == 0) ? src : res;
+          dma4((const char*)(v0 + row), sa);
+          dma4((const char*)(v0 + row) + 4, sa + 64);
+          if (PRO == 1) {
+            dma4((const char*)(pvec + row), sa + 128);
+            dma4((const char*)(pvec + row) + 4, sa + 192);
+            dma4((const char*)(avbar + row), sa + 256);
+            dma4((const char*)(avbar + row) + 4, sa + 320);
+          } else if (PRO == 2) {
+            dma4((const char*)(avbar + row), sa + 128);
+            dma4((const char*)(avbar + row) + 4, sa + 192);
+          }
+        } else {
+          dma16(gin + 2 * (size_t)row, sa);  // 64 x 16 B: words 0..255
+          if (lane < 32) dma16(ca.dval + slot * 64 + lane * 2, sa + 256);  // 64 diagonals: words 256..383
+        }
+        dma4(ca.impNeed + slot, sa + 384);  // the same word in every lane
+        if ((t - nextPub) / 2 + 1 > LAG) {
+          const unsigned long long l0 = ca.prof ? clk() : 0;
+          wait_vm<NI * LAG>();
+          if (ca.prof) cin += clk() - l0;
+          for (; nextPub <= t - 2 * LAG; nextPub += 2)
+            if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
+        }
+      }
+      wait_vm<0>();
+      if (ok)
+        for (; nextPub < T; nextPub += 2)
+          if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
+      if (ca.prof && lane == 0) {
+        prof_add(ca.prof, 4, cfl);
+        prof_add(ca.prof, 5, csl);
+        prof_add(ca.prof, 6, cin);
+      }
+    } else {
+      // ---------------- importer ----------------
+      const int ib = ca.bandImp[b], ni = ca.bandNImp[b];
+      bool ok = true;
+      const unsigned long long m0 = ca.prof ? clk() : 0;
+      for (int k0 = 0; k0 < ni && ok; k0 += 64) {
+        const int k = k0 + lane;
+        const bool act = k < ni;
+        const int need = (act && k >= RI) ? ca.impFree[ib + k - RI] : -1;
+        const int j = act ? ca.impRow[ib + k] : 0;
+        bool done = !act;
+        int published = k0;
+        unsigned spins = 0;
+        while (true) {
+          if (!done && lds_read(&s_prog) > need) {  // slot free: its previous import is no longer read
+            const uint64_t lo = __hip_atomic_load(gout + 2 * (size_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t hi = __hip_atomic_load(gout + 2 * (size_t)j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(lo >> 32) == epoch && (unsigned)(hi >> 32) == epoch) {
+              s_dep[impBase + (k & (RI - 1))] = join_words((uint32_t)lo, (uint32_t)hi);
+              done = true;
+            }
+          }
+          // publish the delivered prefix (values are written before the count, same wavefront)
+          const unsigned long long mask = __ballot(done);
+          const int prefix = (~mask == 0ull) ? 64 : __builtin_ctzll(~mask);
+          const int upto = k0 + prefix < ni ? k0 + prefix : ni;
+          if (upto > published) {
+            published = upto;
+            if (lane == 0) {
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              lds_write(&s_impDone, upto);
+            }
+          }
+          if (~mask == 0ull) break;
+          if (!(ok = spin(spins, err, 64u))) break;
+        }
+      }
+      if (ca.prof && lane == 0) prof_add(ca.prof, 7, clk() - m0);
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const double* src, double* p, const double* res,
+                        const double* avbar, const CgsScalars* sc, const uint64_t* gin, uint64_t* gout, double* out,
+                        unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st) {
+  if (ca.nbands <= 0) return;
+  const dim3 grid(ca.nbands < 256 ? ca.nbands : 256), block(256);
+#define MMX_CHAIN(F, P, EE)                                                                                    \
+  hipLaunchKernelGGL((k_chain_sweep<F, P, EE>), grid, block, 0, st, ca, src, p, res, avbar, sc, gin, gout, out, \
+                     epoch, ticket, err)
+#define MMX_CHAIN_E(F, P)    \
+  do {                       \
+    if (E == 8)              \
+      MMX_CHAIN(F, P, 8);    \
+    else if (E == 16)        \
+      MMX_CHAIN(F, P, 16);   \
+    else                     \
+      MMX_CHAIN(F, P, 32);   \
+  } while (0)
+  if (!fwd)
+    MMX_CHAIN_E(false, 0);
+  else if (pro == 0)
+    MMX_CHAIN_E(true, 0);
+  else if (pro == 1)
+    MMX_CHAIN_E(true, 1);
+  else
+    MMX_CHAIN_E(true, 2);
+#undef MMX_CHAIN_E
+#undef MMX_CHAIN
+}
+
+__global__ void k_chain_fill(long long n, const int* __restrict__ srcIdx, const double* __restrict__ af,
+                             double* __restrict__ val, double padValue) {
+  const long long x = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (x < n) {
+    const int s = srcIdx[x];
+    val[x] = s >= 0 ? af[s] : padValue;
+  }
+}
+
+void launch_chain_fill(long long n, const int* srcIdx, const double* af, double* val, double padValue,
+                       hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_chain_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, srcIdx, af, val, padValue);
+}
+
+}  // namespace mmx

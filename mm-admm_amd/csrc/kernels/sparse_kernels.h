@@ -51,6 +51,33 @@ void launch_sweep(bool fwd, int pro, const int* iaf, const int* jaf, const int* 
                   const uint64_t* gin, uint64_t* gout, double* out, unsigned epoch, unsigned* ticket, unsigned* err,
                   hipStream_t st);
 
+// Band/chain-scheduled sweeps (chain_sweep.hip, schedule host/chain_sched.h): the same rows and
+// arithmetic as launch_sweep, with intra-band dependencies resolved in LDS.
+struct ChainArgs {
+  const int* bandSlot;
+  const int* bandT;
+  const int* bandImp;
+  const int* bandNImp;
+  const int* laneStart;
+  const int* laneLen;
+  const int* laneSkew;
+  const int* bandE;    // per band: entry slots in use (multiple of 4)
+  const double* val;   // [slot][E][64] entry values (filled from the factor by launch_chain_fill)
+  const int* code;     // [slot][E][64] LDS index of the entry's value (0: the zero cell)
+  const double* dval;  // [slot][64] diagonals (backward)
+  const int* impRow;
+  const int* impFree;
+  const int* impNeed;  // per slot: highest import index read at that iteration (-1: none)
+  int nbands, R, RI;
+  unsigned long long* prof;  // optional cycle counters (MMX_CHAIN_PROF), see chain_sweep.hip
+};
+void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const double* src, double* p, const double* res,
+                        const double* avbar, const CgsScalars* sc, const uint64_t* gin, uint64_t* gout, double* out,
+                        unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
+// val[x] = af[srcIdx[x]] (padValue where srcIdx < 0)
+void launch_chain_fill(long long n, const int* srcIdx, const double* af, double* val, double padValue,
+                       hipStream_t st);
+
 // init: x = 0, res = b (mode 0) or res = b - res (mode 1, res holding A x); res0 = res; p = 0;
 // avbar = 0.  Partials [sum res^2, sum res0.res] per block.
 void launch_cgs_init(int mode, int n, const double* b, double* x, double* res, double* res0, double* p,

@@ -42,7 +42,8 @@ class SparseStats(ctypes.Structure):
                 ("t_sweep_ms", ctypes.c_double), ("t_factor_ms", ctypes.c_double), ("t_vec_ms", ctypes.c_double),
                 ("t_solve_ms", ctypes.c_double), ("n_spmv_timed", ctypes.c_longlong),
                 ("n_sweep_timed", ctypes.c_longlong), ("n_factor_timed", ctypes.c_longlong),
-                ("spmv_bytes", ctypes.c_double), ("last_rms", ctypes.c_double), ("rmsi", ctypes.c_double)]
+                ("spmv_bytes", ctypes.c_double), ("last_rms", ctypes.c_double), ("rmsi", ctypes.c_double),
+                ("sweep_mode", ctypes.c_int), ("sweep_e", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -144,6 +145,8 @@ class MatrixStruc:
         return ja
 
     def __del__(self):
+        if lib is None:  # interpreter shutdown: the library is being torn down
+            return
         if getattr(self, "h", None) and self.h.value:
             lib().mmx_struc_destroy(self.h)
             self.h = ctypes.c_void_p()
@@ -259,6 +262,8 @@ class MatrixIter:
         _check(lib().mmx_matrix_stats_reset(self.h))
 
     def close(self):
+        if lib is None:  # interpreter shutdown
+            return
         if getattr(self, "h", None) and self.h.value:
             lib().mmx_matrix_destroy(self.h)
             self.h = ctypes.c_void_p()

@@ -208,3 +208,48 @@ def test_spmv_full_size_bitwise(la):
     A = la.MatrixIter(s)
     A.a[:] = a
     assert _bit(A.matmult(x), L.matmult(ia, ja, a, x))
+
+
+def _sweep_run(la, ia, ja, a, b, mode, monkeypatch):
+    monkeypatch.setenv("MMX_SWEEP", mode)  # read by sfac
+    A = _matrix(la, ia, ja, a, b)
+    p = la.ParamIter.mesh()
+    A.sfac(p)
+    A.factor()
+    y = A.ilu_solve(b)
+    x = np.zeros(len(b))
+    it = A.solve(p, x)
+    st = A.stats()
+    A.close()
+    return y, x, it, st["sweep_mode"]
+
+
+@pytest.mark.parametrize("mesh", [("rect", 2, 45), ("hexdisc", 40), ("circle", "CircleEx24"), ("rect", 2, 300)])
+def test_chain_sweeps_equal_level_sweeps(la, mesh, monkeypatch):
+    """The chain/band-scheduled sweeps (chain_sweep.hip) and the level-scheduled ones compute every
+    row with the same operations in the same order: ILU solves and CG-STAB iterates are identical."""
+    import mmadmm_amd as mx
+    from conftest import circle_mesh
+    if mesh[0] == "rect":
+        m = oracle_py.Mesh.rect(mesh[1], mesh[2])
+        dim, F, nP = mesh[1], m.F, m.nP
+    elif mesh[0] == "hexdisc":
+        md = mx.MeshData.hexdisc(mesh[1], 0.5, 0.5, 0.5)
+        dim, F, nP = 2, md.F, md.nP
+    else:
+        c = circle_mesh(mesh[1])
+        dim, F, nP = 2, c.F, c.Vp.shape[0]
+    ia, ja = L.mesh_pattern(dim, nP, F)
+    N = len(ia) - 1
+    rng = np.random.default_rng(7)
+    a = rng.uniform(-1, 1, len(ja))
+    rows = np.repeat(np.arange(N), np.diff(ia))
+    d = np.nonzero(ja == rows)[0]
+    a[d] = np.add.reduceat(np.abs(a), ia[:-1]) * 0.3 + 1.0
+    b = rng.uniform(-1, 1, N)
+    yl, xl, il, ml = _sweep_run(la, ia, ja, a, b, "level", monkeypatch)
+    yc, xc, ic, mc = _sweep_run(la, ia, ja, a, b, "auto", monkeypatch)
+    assert ml == 0 and mc == 1
+    assert _bit(yc, yl) and il == ic and _bit(xc, xl)
+    if N < 20000:  # and both equal the restatement
+        assert _bit(yc, L.ilu_solve(ia, ja, L.ilu0(ia, ja, a), b))

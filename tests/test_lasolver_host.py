@@ -69,3 +69,44 @@ def test_param_defaults():
     assert (p.order, p.level, p.iscal, p.nitmax, p.info) == (1, 1, 1, 30, 1)
     q = la.ParamIter.mesh()
     assert (q.order, q.level, q.iscal, q.nitmax, q.resid_reduc, q.new_rhat, q.iaccel) == (0, 0, 0, 10000, 1e-6, 0, 0)
+
+
+def _schedule_info(ia, ja, level, fwd):
+    import ctypes
+    L_ = la.lib()
+    L_.mmx_sweep_schedule_info.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p]
+    ia = np.ascontiguousarray(ia, np.int32)
+    ja = np.ascontiguousarray(ja, np.int32)
+    out = np.zeros(16, np.int64)
+    rc = L_.mmx_sweep_schedule_info(len(ia) - 1, ia.ctypes.data, ja.ctypes.data, level, int(fwd), out.ctypes.data)
+    assert rc == 0, L_.mmx_last_error().decode() if hasattr(L_, "mmx_last_error") else rc
+    keys = "ok E R RI bands chains maxLen maxSkew maxT slots imports estIters levels".split()
+    return dict(zip(keys, out[:13].tolist()))
+
+
+@pytest.mark.parametrize("mesh,level", [(("rect", 2, 20), 0), (("rect", 2, 57), 0), (("rect", 2, 20), 1),
+                                        (("hexdisc", 30), 0), (("circle", "CircleEx24"), 0), (("rect", 3, 6), 0)])
+def test_chain_schedule_is_valid(mesh, level):
+    """The chain/band sweep schedule (host/chain_sched.cpp) replays correctly on the host: every row
+    once with the reference's entry order, ring values live when read, imports right and ordered
+    (validate_chain_schedule, which mmx_sweep_schedule_info runs and fails on)."""
+    import mmadmm_amd as mx
+    from conftest import circle_mesh
+    if mesh[0] == "rect":
+        m = oracle_py.Mesh.rect(mesh[1], mesh[2])
+        dim, F, nP = mesh[1], m.F, m.nP
+    elif mesh[0] == "hexdisc":
+        md = mx.MeshData.hexdisc(mesh[1], 0.5, 0.5, 0.5)
+        dim, F, nP = 2, md.F, md.nP
+    else:
+        c = circle_mesh(mesh[1])
+        dim, F, nP = 2, c.F, c.Vp.shape[0]
+    ia, ja = L.mesh_pattern(dim, nP, F)
+    for fwd in (True, False):
+        info = _schedule_info(ia, ja, level, fwd)
+        if dim == 3 and not fwd:
+            continue  # upper rows wider than 32 entries: the level-scheduled sweep is used
+        assert info["ok"] == 1, info
+        # the critical path stays close to the dependency DAG's depth
+        assert info["estIters"] <= 1.3 * info["levels"] + 64, info
