@@ -352,7 +352,7 @@ struct SparseMatrix {
     }
     c.args = ChainArgs{c.bandSlot.p, c.bandT.p, c.bandImp.p, c.bandNImp.p, c.laneStart.p, c.laneLen.p, c.laneSkew.p,
                        c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impFree.p, c.impNeed.p, S.nbands, S.R, S.RI,
-                       d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr};
+                       d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr, (pe && atoi(pe) >= 2) ? 1 : 0};
   }
 
   void begin(int t) {

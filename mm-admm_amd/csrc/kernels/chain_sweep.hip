@@ -148,73 +148,116 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       // nothing: an earlier wait gave up; the host reports it
     } else if (wave == 0) {
       // ---------------- compute ----------------
+      // iteration t + 1's stage (entries, addresses, operands) is read before iteration t is
+      // computed, so an iteration costs one LDS round trip (its dependency values) plus the chain
       const int Eb = ca.bandE[b];
       wait_vm<0>();  // nothing in flight here; tells the waitcnt pass so the loop needs no vmcnt waits
       unsigned long long c0 = ca.prof ? clk() : 0, cstage = 0, cimp = 0;
-      for (int t = 0; t < T; ++t) {
+      bool ok = true;
+      struct Fetched {
+        double a[E];
+        int c[E];
+        double init, diag;
+        int need;
+      };
+      auto load_stage = [&](int st, Fetched& f) {
+        const uint32_t* sa = s_aux + st * kAuxWords;
+        f.need = (int)sa[384 + lane];  // the same in every lane; made scalar where it is used
+        const double* sv = s_val + st * E * 64;
+        const int* scd = s_code + st * E * 64;
+#pragma unroll
+        for (int e0 = 0; e0 < E; e0 += 4)
+          if (e0 < Eb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              f.a[e0 + q] = sv[(e0 + q) * 64 + lane];
+              f.c[e0 + q] = scd[(e0 + q) * 64 + lane];
+            }
+          }
+        if (FWD) {
+          const double r0 = join_words(sa[lane], sa[64 + lane]);
+          if (PRO == 0) {
+            f.init = r0;
+          } else if (PRO == 1) {
+            const double pv = join_words(sa[128 + lane], sa[192 + lane]);
+            const double av = join_words(sa[256 + lane], sa[320 + lane]);
+            f.init = r0 + beta * (pv - omega * av);
+          } else {
+            const double av = join_words(sa[128 + lane], sa[192 + lane]);
+            f.init = r0 - alpha * av;
+          }
+          f.diag = 1.0;
+        } else {
+          f.init = join_words(sa[4 * lane], sa[4 * lane + 2]);  // granule {tag|lo, tag|hi}
+          f.diag = join_words(sa[256 + 2 * lane], sa[256 + 2 * lane + 1]);
+        }
+      };
+      auto fetch = [&](int t, Fetched& f) {  // blocking: wait for stage t, then read it
         const int st = t & (DL - 1);
         unsigned spins = 0;
-        bool ok = true;
-        const unsigned long long w0 = ca.prof ? clk() : 0;
+        const unsigned long long w0 = ca.profIter ? clk() : 0;
         while (lds_read(&s_tag[st]) != t)
           if (!(ok = spin(spins, err, 8u))) break;
-        if (ca.prof) cstage += clk() - w0;
-        if (!ok) break;
-        const uint32_t* sa = s_aux + st * kAuxWords;
-        const int need = __builtin_amdgcn_readfirstlane((int)sa[384 + lane]);
-        if (need >= 0) {  // imports this iteration reads: wait for their delivery
-          const unsigned long long i0 = ca.prof ? clk() : 0;
-          while (lds_read(&s_impDone) <= need)
+        if (ca.profIter) cstage += clk() - w0;
+        load_stage(st, f);
+      };
+      // one iteration: a single batch of LDS reads -- this iteration's dependency values, the next
+      // stage's tag, the import count, and the next stage's contents (valid when that tag, read
+      // first and served first, says the stage has landed) -- then the chain
+      int seen = 0;  // import count read by the previous batch
+      auto step = [&](int t, const Fetched& f, Fetched& nx) {
+        const int need = __builtin_amdgcn_readfirstlane(f.need);
+        if (need >= 0 && seen <= need) {  // imports this iteration reads: wait for their delivery
+          unsigned spins = 0;
+          const unsigned long long i0 = ca.profIter ? clk() : 0;
+          while ((seen = lds_read(&s_impDone)) <= need)
             if (!(ok = spin(spins, err, 16u))) break;
-          if (ca.prof) cimp += clk() - i0;
-          if (!ok) break;
+          if (ca.profIter) cimp += clk() - i0;
+          if (!ok) return;
         }
+        double v[E];
+#pragma unroll
+        for (int e0 = 0; e0 < E; e0 += 4)
+          if (e0 < Eb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[e0 + q] = s_dep[f.c[e0 + q]];
+          }
+        const bool hasNext = t + 1 < T;
+        const int stn = (t + 1) & (DL - 1);
+        const int tagN = __hip_atomic_load(&s_tag[stn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int doneN = __hip_atomic_load(&s_impDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");  // keep the stage reads behind the tag read (LDS serves them in order)
+        if (hasNext) load_stage(stn, nx);
         const int p = t - skew;
         if (p >= 0 && p < len) {
           const int row = FWD ? cst + p : cst - p;
-          const double* sv = s_val + st * E * 64;
-          const int* scd = s_code + st * E * 64;
-          double init;
-          if (FWD) {
-            const double r0 = join_words(sa[lane], sa[64 + lane]);
-            if (PRO == 0) {
-              init = r0;
-            } else if (PRO == 1) {
-              const double pv = join_words(sa[128 + lane], sa[192 + lane]);
-              const double av = join_words(sa[256 + lane], sa[320 + lane]);
-              init = r0 + beta * (pv - omega * av);
-            } else {
-              const double av = join_words(sa[128 + lane], sa[192 + lane]);
-              init = r0 - alpha * av;
-            }
-          } else {
-            init = join_words(sa[4 * lane], sa[4 * lane + 2]);  // granule {tag|lo, tag|hi}
-          }
           // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
-          double acc = init;
+          double acc = f.init;
 #pragma unroll
-          for (int e0 = 0; e0 < E; e0 += 4) {
+          for (int e0 = 0; e0 < E; e0 += 4)
             if (e0 < Eb) {
-              double a[4], v[4];
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                a[q] = sv[(e0 + q) * 64 + lane];
-                v[q] = s_dep[scd[(e0 + q) * 64 + lane]];
-              }
-#pragma unroll
-              for (int q = 0; q < 4; ++q) acc -= a[q] * v[q];
+              for (int q = 0; q < 4; ++q) acc -= f.a[e0 + q] * v[e0 + q];
             }
-          }
-          if (!FWD) acc = acc / join_words(sa[256 + 2 * lane], sa[256 + 2 * lane + 1]);
+          if (!FWD) acc = acc / f.diag;
           s_dep[1 + lane * (R + 1) + (p & (R - 1))] = acc;
           const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
           __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (!FWD) out[row] = acc;
-          if (FWD && PRO != 0) pvec[row] = init;
+          if (FWD && PRO != 0) pvec[row] = f.init;
         }
         if (lane == 0) lds_write(&s_prog, t + 1);
+        seen = doneN;
+        if (hasNext && __builtin_amdgcn_readfirstlane(tagN) != t + 1) fetch(t + 1, nx);  // not landed yet
+      };
+      Fetched fa, fb;
+      if (T > 0) fetch(0, fa);
+      for (int t = 0; t < T && ok; t += 2) {
+        step(t, fa, fb);
+        if (t + 1 >= T || !ok) break;
+        step(t + 1, fb, fa);
       }
       if (ca.prof && lane == 0) {
         const unsigned long long tot = clk() - c0;
@@ -280,6 +323,11 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           if (lane < 32) dma16(ca.dval + slot * 64 + lane * 2, sa + 256);  // 64 diagonals: words 256..383
         }
         dma4(ca.impNeed + slot, sa + 384);  // the same word in every lane
+#ifdef MMX_CHAIN_EXPT  // timing experiment only: publish before the DMA lands (wrong results)
+        if (lane == 0) lds_write(&s_tag[st], t);
+        nextPub = t + 2;
+        continue;
+#endif
         if ((t - nextPub) / 2 + 1 > LAG) {
           const unsigned long long l0 = ca.prof ? clk() : 0;
           wait_vm<NI * LAG>();
@@ -299,39 +347,45 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       }
     } else {
       // ---------------- importer ----------------
+      // lane l delivers imports l, l + 64, l + 128, ... in order; the published count is the
+      // lowest import still pending over the lanes (all below it are in their slots)
       const int ib = ca.bandImp[b], ni = ca.bandNImp[b];
-      bool ok = true;
       const unsigned long long m0 = ca.prof ? clk() : 0;
-      for (int k0 = 0; k0 < ni && ok; k0 += 64) {
-        const int k = k0 + lane;
-        const bool act = k < ni;
-        const int need = (act && k >= RI) ? ca.impFree[ib + k - RI] : -1;
-        const int j = act ? ca.impRow[ib + k] : 0;
-        bool done = !act;
-        int published = k0;
-        unsigned spins = 0;
-        while (true) {
-          if (!done && lds_read(&s_prog) > need) {  // slot free: its previous import is no longer read
-            const uint64_t lo = __hip_atomic_load(gout + 2 * (size_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t hi = __hip_atomic_load(gout + 2 * (size_t)j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(lo >> 32) == epoch && (unsigned)(hi >> 32) == epoch) {
-              s_dep[impBase + (k & (RI - 1))] = join_words((uint32_t)lo, (uint32_t)hi);
-              done = true;
+      int k = lane;
+      int need = (k < ni && k >= RI) ? ca.impFree[ib + k - RI] : -1;
+      int j = k < ni ? ca.impRow[ib + k] : 0;
+      int published = 0;
+      unsigned spins = 0;
+      while (ni > 0) {
+        bool prog = false;
+        if (k < ni && lds_read(&s_prog) > need) {  // slot free: its previous import is no longer read
+          const uint64_t lo = __hip_atomic_load(gout + 2 * (size_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t hi = __hip_atomic_load(gout + 2 * (size_t)j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(lo >> 32) == epoch && (unsigned)(hi >> 32) == epoch) {
+            s_dep[impBase + (k & (RI - 1))] = join_words((uint32_t)lo, (uint32_t)hi);
+            k += 64;
+            prog = true;
+            if (k < ni) {
+              need = k >= RI ? ca.impFree[ib + k - RI] : -1;
+              j = ca.impRow[ib + k];
             }
           }
-          // publish the delivered prefix (values are written before the count, same wavefront)
-          const unsigned long long mask = __ballot(done);
-          const int prefix = (~mask == 0ull) ? 64 : __builtin_ctzll(~mask);
-          const int upto = k0 + prefix < ni ? k0 + prefix : ni;
-          if (upto > published) {
-            published = upto;
-            if (lane == 0) {
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-              lds_write(&s_impDone, upto);
-            }
+        }
+        int low = k < ni ? k : ni;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) low = min(low, __shfl_xor(low, o));
+        if (low > published) {  // values are written before the count, same wavefront
+          published = low;
+          if (lane == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_write(&s_impDone, low);
           }
-          if (~mask == 0ull) break;
-          if (!(ok = spin(spins, err, 64u))) break;
+        }
+        if (low >= ni) break;
+        if (__any(prog)) {
+          spins = 0;
+        } else if (!spin(spins, err, 64u)) {
+          break;
         }
       }
       if (ca.prof && lane == 0) prof_add(ca.prof, 7, clk() - m0);

@@ -70,6 +70,7 @@ struct ChainArgs {
   const int* impNeed;  // per slot: highest import index read at that iteration (-1: none)
   int nbands, R, RI;
   unsigned long long* prof;  // optional cycle counters (MMX_CHAIN_PROF), see chain_sweep.hip
+  int profIter;              // MMX_CHAIN_PROF=2: also time the waits inside iterations (perturbs them)
 };
 void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const double* src, double* p, const double* res,
                         const double* avbar, const CgsScalars* sc, const uint64_t* gin, uint64_t* gout, double* out,
