@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-spmv", action="store_true")
+    ap.add_argument("--no-be", action="store_true", help="skip the backward-Euler (method 2) section")
     return ap.parse_args()
 
 
@@ -99,6 +100,7 @@ def spmv_bench(torch, la, mx, with_cpu):
     st = A.stats()
     out["cgstab"] = {"nitr": nitr, "solve_ms": round(st["t_solve_ms"], 2), "factor_ms": round(st["t_factor_ms"], 2),
                      "sweep_ms": round(st["t_sweep_ms"] / max(st["n_sweep_timed"], 1), 3),
+                     "sweep_kernel": "k_chain_sweep (E=%d)" % st["sweep_e"] if st["sweep_mode"] else "k_sweep",
                      "ms_per_iter": round((st["t_solve_ms"] - st["t_factor_ms"]) / max(nitr, 1), 2)}
     if with_cpu:
         import time as _t
@@ -115,6 +117,47 @@ def spmv_bench(torch, la, mx, with_cpu):
                                "kind": "port", "sample": "oracle/lasolver.cpp (bit-identical restatement of "
                                "lib/LASolver, itself pinned to the reference build): 3 matmults + 1 solve"}
     A.close()
+    return out
+
+
+def be_bench(mx, with_cpu):
+    """Method 2 (Mesh::backwardsEulerStep, src/Mesh.cpp:1263-1341) on the device: SquareGrid
+    n = 707 (1,001,113 nodes, the SpMV matrix's mesh), MEx3, dt 0.025, tau 0.5, rho 100 (the
+    Monitor220 family).  First step (pattern, symbolic ILU, sweep schedules, FD Jacobian) and the
+    steady steps after it are timed separately."""
+    mesh = mx.MeshData.rect(2, 707)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 3), rho=100.0, tau=0.5)
+    E = mx.Engine(M, 0.025)
+    t0 = time.perf_counter()
+    E.backwards_euler_step(0.025)
+    first = time.perf_counter() - t0
+    E.reset_stats()
+    steps = 3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        E.backwards_euler_step(0.025)
+    dt = (time.perf_counter() - t0) / steps
+    st = E.stats()
+    out = {"workload": "SquareGrid n=707 (%d nodes, %d triangles), MEx3, dt 0.025 tau 0.5 rho 100" % (mesh.nP, mesh.nF),
+           "first_step_s": round(first, 3), "step_ms": round(dt * 1e3, 2),
+           "newton_per_step": st["newton_iters"] / steps, "cg_iters_per_step": st["cg_iters"] / steps,
+           "solve_ms_per_step": round(st["t_solve_ms"] / steps, 2)}
+    E.close()
+    if with_cpu:  # the oracle's restatement, one core, on a bounded sample of the same family
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_py
+        n = 400
+        om = oracle_py.Mesh.rect(2, n)
+        O = oracle_py.Integrator(om, 3, 0.025, 0.5, 100.0, nthreads=1)
+        O.backwards_euler_step(0.025)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            O.backwards_euler_step(0.025)
+        cdt = (time.perf_counter() - t0) / steps
+        out["cpu_baseline"] = {"step_ms": round(cdt * 1e3, 1), "nodes": int(om.nP), "cores": 1, "kind": "port",
+                               "step_ms_per_1M_nodes": round(cdt * 1e3 * 1001113 / om.nP, 1),
+                               "sample": "oracle/oracle.cpp backwards_euler_step (FD Jacobian + LASolver "
+                                         "restatement) on SquareGrid n=%d, 3 steady steps after the first" % n}
     return out
 
 
@@ -261,6 +304,9 @@ def main():
     if not args.no_spmv:
         log("spmv microbenchmark")
         result["spmv"] = spmv_bench(torch, la, mx, with_cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
+    if not args.no_be and world == 1:
+        log("backward Euler")
+        result["backward_euler"] = be_bench(mx, with_cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline")
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
