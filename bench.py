@@ -161,18 +161,28 @@ def be_bench(mx, with_cpu):
     return out
 
 
-def pmc_traffic(kernel):
-    """Per-launch HBM bytes of a kernel from the committed rocprofv3 PMC passes
-    (profiles/pmc_summary.json: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE; and raw)."""
+def pmc_entry(kernel):
+    """The committed rocprofv3 PMC summary of a kernel (profiles/pmc_summary.json); `kernel` is the
+    short name, template arguments included, or a prefix of it ending in ','."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if not os.path.exists(path):
-        return None, None
     try:
         with open(path) as f:
-            d = json.load(f).get(kernel, {})
-        return d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_raw_per_launch")
+            d = json.load(f)
     except (OSError, ValueError):
-        return None, None
+        return {}
+    if kernel in d:
+        return d[kernel]
+    for k, v in d.items():
+        if k.startswith(kernel):
+            return v
+    return {}
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes of a kernel from the PMC passes (FETCH_SIZE x2 per the gfx950
+    correction + WRITE_SIZE; and raw)."""
+    d = pmc_entry(kernel)
+    return d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_raw_per_launch")
 
 
 def cpu_baseline(mesh, admm_iter, threads):
@@ -188,9 +198,40 @@ def cpu_baseline(mesh, admm_iter, threads):
     t0 = time.perf_counter()
     O.step(admm_iter, -1.0)
     dt = time.perf_counter() - t0
+    oracle_py.set_threads(1)  # all cores and 1 thread
+    t0 = time.perf_counter()
+    O.step(1, -1.0)
+    dt1 = time.perf_counter() - t0
     return {"value": round(admm_iter / dt, 3), "unit": "ADMM it/s", "cores": threads, "kind": "port",
+            "value_1thread": round(1.0 / dt1, 3),
             "sample": f"C3 mesh, 1 timed step of {admm_iter} ADMM iterations after set-up and the "
-                      f"FD-Hessian step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, {threads} threads)"}
+                      f"FD-Hessian step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, {threads} threads); "
+                      f"value_1thread: one further step of 1 ADMM iteration on 1 thread"}
+
+
+def stream_copy_ceiling(torch):
+    """Measured HBM ceiling on this box: 1 GiB device-to-device copy (read + write bytes / time)."""
+    n = 1 << 27  # doubles
+    x = torch.ones(n, dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    for _ in range(3):
+        y.copy_(x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    reps = 20
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del x, y
+    return round(2 * 8 * n / (ms * 1e-3) / 1e9, 1)
+
+
+def pmc_flops(kernel):
+    """Executed fp64 flops per launch from the SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 pass."""
+    return pmc_entry(kernel).get("fp64_flops_per_launch")
 
 
 def main():
@@ -262,13 +303,19 @@ def main():
         elapsed = float(t.item())
 
     st = eng.stats()
+    # a second run with the early exit enabled reports the iterations actually executed
+    eng.reset_stats()
+    for _ in range(3):
+        eng.step(args.admm_iter, 1e-3)
+    st_early = eng.stats()
     iters = args.steps * args.admm_iter
     scale = mesh.nP / c3_nodes if parallelism.startswith("element") else (world if world > 1 else mesh.nP / c3_nodes)
     prox_ms = st["t_prox_ms"] / max(st["n_prox"], 1)
     xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
     prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
     xup_gbs = st["xupdate_bytes"] / (xup_ms * 1e-3) / 1e9
-    traffic, traffic_raw = pmc_traffic("k_prox_lds<2>")
+    prox_name = "k_prox_lds<2, %d>" % int(os.environ.get("MMX_PROX_BLOCK", "256"))
+    traffic, traffic_raw = pmc_traffic(prox_name)
     result = {
         "metric": "ADMM iterations/sec on 1M-node 2D mesh; achieved HBM GB/s in SpMV",
         "value": round(iters / elapsed * scale, 3),
@@ -288,19 +335,30 @@ def main():
                    "global_nodes": mesh.nP, "global_simplices": mesh.nF, "nodes_rank0": eng.nP,
                    "simplices_rank0": eng.nF, "admm_iter": args.admm_iter, "parallelism": parallelism,
                    "value_unit_note": "ADMM it/s x global nodes / 1,000,519"},
-        "roofline": {"bound": "hbm", "kernel": "k_prox_lds<2>",
+        "roofline": {"bound": "hbm", "kernel": prox_name,
                      "achieved": round(prox_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_fetch_uncorrected": traffic_raw,
                      "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE, WRITE_SIZE passes)",
                      "bytes_per_launch": st["prox_bytes"],
                      "avg_launch_ms": round(prox_ms, 4)},
+        "prox_fp64": None,
         "kernels": {"k_prox_ms": round(prox_ms, 4), "k_xupdate_ms": round(xup_ms, 4),
                     "k_xupdate_GBs": round(xup_gbs, 1), "bfgs_iters_per_prox":
                         round(st["bfgs_iters"] / max(st["admm_iters"], 1) / mesh.nF, 4)},
+        "early_exit": {"tol": 1e-3, "steps": 3,
+                       "admm_iters_per_step": round(st_early["admm_iters"] / 3, 2)},
         "first_step_ms": round(first_ms, 2),
         "setup_s": round(t_setup, 2),
     }
+    fl = pmc_flops(prox_name)
+    if fl:
+        result["prox_fp64"] = {"executed_flops_per_launch": fl, "achieved_TFLOPs": round(fl / (prox_ms * 1e-3) / 1e12, 2),
+                               "peak_TFLOPs": 78.6, "frac": round(fl / (prox_ms * 1e-3) / 1e12 / 78.6, 4),
+                               "source": "rocprofv3 SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes "
+                                         "(profiles/pmc_summary.json); peak: AMD MI355X fp64 vector spec"}
+    if rank == 0 and world == 1:
+        result["roofline"]["measured_copy_ceiling_GBs"] = stream_copy_ceiling(torch)
     if not args.no_spmv:
         log("spmv microbenchmark")
         result["spmv"] = spmv_bench(torch, la, mx, with_cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))

@@ -1406,6 +1406,11 @@ using namespace orc;
 
 extern "C" {
 
+// OpenMP threads of the prox restatement (process-wide, like the reference's Mesh ctor, Mesh.cpp:428-438)
+void orc_set_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+}
+
 void* orc_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, double ya, double yb,
                     double za, double zb, int btype) {
   auto* m = new MeshData();

@@ -25,6 +25,7 @@ extern "C" {
 #endif
 
 /* ---- meshes (generators + file reader), returned as an opaque handle ---- */
+void orc_set_threads(int n);
 void* orc_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, double ya,
                     double yb, double za, double zb, int btype);
 void* orc_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb,

@@ -7,7 +7,11 @@ fetch side (the prox kernel's bulk read, Bkinv, is such a stream), `hbm_bytes_ra
 not.  Other access widths are uncalibrated, so the truth lies between the two for mixed kernels.
 
   python profiles/make_pmc_summary.py profiles/r01/pmc/fetch_size_counter_collection.csv \
-         profiles/r01/pmc/write_size_counter_collection.csv
+         profiles/r01/pmc/write_size_counter_collection.csv [profiles/r01/pmc/f64_counter_collection.csv]
+
+The optional third pass (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, wave instructions) gives
+`fp64_flops_per_launch` = 64 lanes x (ADD + MUL + 2 FMA + TRANS): executed fp64 work, including
+the correctly rounded powers' double-double arithmetic.
 """
 import collections
 import csv
@@ -25,13 +29,27 @@ def load(path):
 
 
 def short(name):
-    m = re.match(r"(?:void )?mmx::(\w+(?:<[^>]*>)?)", name)
+    m = re.match(r"(?:void )?mmx::(?:\(anonymous namespace\)::)?(\w+(?:<[^>]*>)?)", name)
     return m.group(1) if m else name
 
 
-def main(fetch, write):
+def load_f64(path):
+    d = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        d[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k, c in d.items():
+        n = max(len(v) for v in c.values())
+        mean = {name: sum(v) / len(v) for name, v in c.items()}
+        out[k] = round(64 * (mean.get("SQ_INSTS_VALU_ADD_F64", 0) + mean.get("SQ_INSTS_VALU_MUL_F64", 0) +
+                             2 * mean.get("SQ_INSTS_VALU_FMA_F64", 0) + mean.get("SQ_INSTS_VALU_TRANS_F64", 0)))
+    return out
+
+
+def main(fetch, write, f64=None):
     f, w = load(fetch), load(write)
-    out = {"source": [os.path.relpath(fetch), os.path.relpath(write)], "units": "bytes per launch"}
+    fl = load_f64(f64) if f64 else {}
+    out = {"source": [os.path.relpath(p) for p in (fetch, write, f64) if p], "units": "bytes per launch"}
     for k in f:
         if not k.startswith(("void mmx::", "mmx::")):
             continue
@@ -40,10 +58,12 @@ def main(fetch, write):
         out[short(k)] = {"launches": len(f[k]), "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
                          "hbm_bytes_per_launch": round((2 * fk + wk) * 1024),
                          "hbm_bytes_raw_per_launch": round((fk + wk) * 1024)}
+        if k in fl:
+            out[short(k)]["fp64_flops_per_launch"] = fl[k]
     here = os.path.dirname(os.path.abspath(__file__))
     with open(os.path.join(here, "pmc_summary.json"), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])

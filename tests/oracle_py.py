@@ -121,6 +121,12 @@ class Mesh:
         return Mesh._from_handle(dim, h)
 
 
+def set_threads(n):
+    """OpenMP threads of the restatement's prox (process-wide)."""
+    lib().orc_set_threads.argtypes = [ctypes.c_int]
+    lib().orc_set_threads(int(n))
+
+
 class Integrator:
     """Mesh<D> + MeshIntegrator<D> of the reference, restated on the CPU."""
 
