@@ -124,6 +124,15 @@ void symbolic_ilu(int n, const std::vector<int>& ia, const std::vector<int>& ja,
 
 namespace {
 
+// SpMV kernel: 2 = k_spmv2 (default), 1 = k_spmv (MMX_SPMV=1; kept for A/B measurements)
+int spmv_version() {
+  static int v = [] {
+    const char* e = getenv("MMX_SPMV");
+    return (e && atoi(e) == 1) ? 1 : 2;
+  }();
+  return v;
+}
+
 void check_params(const mmx_param_iter& p) {
   if (p.order != 0) throw Error(MMADMM_ERR_INVALID, "unsupported ParamIter.order (only natural ordering, 0)");
   if (p.drop_ilu != 0) throw Error(MMADMM_ERR_INVALID, "unsupported ParamIter.drop_ilu (only level-of-fill ILU, 0)");
@@ -157,6 +166,7 @@ struct SparseMatrix {
   long long nnz = 0;
   std::vector<int> ia, ja;
   DevBuf<int> d_ia, d_ja, d_rowblk;
+  DevBuf<int4> d_desc;  // SpMV block descriptors {r0, r1, k0, k1}
   int nblk = 0;
   DevBuf<double> d_a, d_b, d_tol;
   bool tolSet = false;
@@ -210,9 +220,14 @@ struct SparseMatrix {
     MMX_HIP(hipSetDevice(device));
     MMX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     d_ia.upload(ia.data(), ia.size(), st);
-    d_ja.upload(ja.data(), ja.size(), st);
-    d_a.alloc(std::max<long long>(nnz, 1));
-    MMX_HIP(hipMemsetAsync(d_a.p, 0, sizeof(double) * std::max<long long>(nnz, 1), st));
+    {  // 2 padding entries: launch_spmv2 reads whole aligned pairs
+      std::vector<int> jap(ja);
+      jap.resize(ja.size() + 2, 0);
+      d_ja.upload(jap.data(), jap.size(), st);
+      MMX_HIP(hipStreamSynchronize(st));
+    }
+    d_a.alloc(nnz + 2);
+    MMX_HIP(hipMemsetAsync(d_a.p, 0, sizeof(double) * (nnz + 2), st));
     d_b.alloc(n);
     MMX_HIP(hipMemsetAsync(d_b.p, 0, sizeof(double) * n, st));
     // SpMV row blocks: greedy runs of rows with <= kSpmvTile nonzeros (a longer row alone)
@@ -226,6 +241,10 @@ struct SparseMatrix {
     }
     nblk = (int)rb.size() - 1;
     d_rowblk.upload(rb.data(), rb.size(), st);
+    std::vector<int4> desc(nblk);
+    for (int b = 0; b < nblk; ++b) desc[b] = make_int4(rb[b], rb[b + 1], ia[rb[b]], ia[rb[b + 1]]);
+    d_desc.upload(desc.data(), desc.size(), st);
+    MMX_HIP(hipStreamSynchronize(st));
     for (DevBuf<double>* v : {&d_res, &d_res0, &d_p, &d_vbar, &d_avbar, &d_s, &d_z, &d_t, &d_x, &d_tmp}) v->alloc(n);
     d_part.alloc((size_t)std::max(nblk, vec_grid(n)) * 3);
     d_sc.alloc(1);
@@ -443,7 +462,10 @@ struct SparseMatrix {
 
   void spmv(int epi, const double* x, double* y, const double* e1) {
     begin(0);
-    launch_spmv(epi, nblk, d_rowblk.p, d_ia.p, d_ja.p, d_a.p, x, y, e1, d_part.p, st);
+    if (spmv_version() == 1)
+      launch_spmv(epi, nblk, d_rowblk.p, d_ia.p, d_ja.p, d_a.p, x, y, e1, d_part.p, st);
+    else
+      launch_spmv2(epi, nblk, d_desc.p, d_ia.p, d_ja.p, d_a.p, x, y, e1, d_part.p, st);
     MMX_HIP(hipGetLastError());
     const float ms = end(0);
     stats.spmvs++;

@@ -35,6 +35,10 @@ struct SweepCtl {
 // 2: partial sums of y.e1 and y.y.
 void launch_spmv(int epi, int nblk, const int* rowblk, const int* ia, const int* ja, const double* a,
                  const double* x, double* y, const double* e1, double* partials, hipStream_t st);
+// The same product and partial sums from per-block descriptors {r0, r1, ia[r0], ia[r1]}; a and ja
+// must be readable 2 entries past nnz.
+void launch_spmv2(int epi, int nblk, const int4* desc, const int* ia, const int* ja, const double* a,
+                  const double* x, double* y, const double* e1, double* partials, hipStream_t st);
 
 // ILU numeric factor in the factor pattern (iaf/jaf/dg); amap maps A's entries into it.  perm: rows
 // in forward-level order, padded with -1 to whole chunks of kSweepRows.

@@ -163,6 +163,113 @@ __global__ void __launch_bounds__(kSpmvBlock) k_spmv(const int* __restrict__ row
   }
 }
 
+// SpMV v2: the same blocks and the same sums, with the block's memory requests all issued up
+// front.  The block descriptor {r0, r1, k0, k1} comes from one 16-byte load (no rowblk -> ia
+// chain); each lane loads up to 5 aligned pairs of (a, ja) as 16-byte / 8-byte vectors with
+// nontemporal hints (read once: they should not evict x from L2), then gathers x, so a
+// workgroup has its whole tile in flight; the row bounds and e1 are fetched before the tile
+// lands.  Logical blocks are XCD-chunked (each XCD walks a contiguous range of rows, so the x
+// windows of consecutive blocks hit its own L2).  a and ja carry 2 padding entries (host) so the
+// last pair never reads past the arrays.  Partial sums are indexed by logical block: the same
+// rows per partial as k_spmv, so the reductions are unchanged.
+constexpr int kSpmvPairs = kSpmvTile / (2 * kSpmvBlock) + 1;  // 5: covers an odd start
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+typedef double v2d_t __attribute__((ext_vector_type(2)));
+
+template <int EPI>
+__global__ void __launch_bounds__(kSpmvBlock) k_spmv2(const int4* __restrict__ desc, int nblk,
+                                                       const int* __restrict__ ia, const int* __restrict__ ja,
+                                                       const double* __restrict__ a, const double* __restrict__ x,
+                                                       double* __restrict__ y, const double* __restrict__ e1,
+                                                       double* __restrict__ partials) {
+  __shared__ double prod[kSpmvTile + 2];
+  __shared__ double red[kSpmvBlock][2];
+  const int G = (int)gridDim.x;  // a multiple of 8
+  const int b = (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8);
+  if (b >= nblk) return;  // whole workgroup: no barrier is skipped by a part of it
+  const int tid = (int)threadIdx.x;
+  const int4 d = desc[b];
+  const int r0 = d.x, r1 = d.y, k0 = d.z, k1 = d.w;
+  double pv[2] = {0.0, 0.0};
+  if (k1 - k0 <= kSpmvTile) {
+    const int ka = k0 & ~1;
+    const int np = (k1 - ka + 1) >> 1;
+    // first row of this lane: bounds (and e1) requested before the tile.  Every load below is
+    // unconditional (out-of-range lanes re-read a valid pair): no branch separates the requests,
+    // so the compiler issues them all before the first wait.
+    const int rf = r0 + tid;
+    const int rc = rf < r1 ? rf : r1 - 1;
+    int ib = ia[rc], ie = ia[rc + 1];
+    double ef = 0.0;
+    if (EPI != 0) ef = e1[rc];
+    const int pmax = np > 0 ? np - 1 : 0;
+    v2i_t jv[kSpmvPairs];
+    v2d_t av[kSpmvPairs];
+#pragma unroll
+    for (int j = 0; j < kSpmvPairs; ++j) {
+      const int p = min(tid + j * kSpmvBlock, pmax);
+      jv[j] = __builtin_nontemporal_load(reinterpret_cast<const v2i_t*>(ja + ka) + p);
+      av[j] = __builtin_nontemporal_load(reinterpret_cast<const v2d_t*>(a + ka) + p);
+    }
+    double xv0[kSpmvPairs], xv1[kSpmvPairs];
+#pragma unroll
+    for (int j = 0; j < kSpmvPairs; ++j) {
+      xv0[j] = x[jv[j].x];
+      xv1[j] = x[jv[j].y];
+    }
+#pragma unroll
+    for (int j = 0; j < kSpmvPairs; ++j) {
+      const int p = tid + j * kSpmvBlock;
+      if (p < np) {
+        prod[2 * p] = av[j].x * xv0[j];
+        prod[2 * p + 1] = av[j].y * xv1[j];
+      }
+    }
+    __syncthreads();
+    for (int r = rf; r < r1; r += kSpmvBlock) {
+      if (r != rf) {
+        ib = ia[r];
+        ie = ia[r + 1];
+        if (EPI != 0) ef = e1[r];
+      }
+      double s = 0.0;
+      for (int kk = ib; kk < ie; ++kk) s += prod[kk - ka];
+      y[r] = s;
+      if (EPI == 1) pv[0] += ef * s;
+      if (EPI == 2) {
+        pv[0] += s * ef;
+        pv[1] += s * s;
+      }
+    }
+  } else {  // a single row longer than the tile: chunks, summed in order by lane 0
+    double s = 0.0;
+    for (int c = k0; c < k1; c += kSpmvTile) {
+      const int ce = (c + kSpmvTile < k1) ? c + kSpmvTile : k1;
+      for (int k = c + tid; k < ce; k += kSpmvBlock) prod[k - c] = a[k] * x[ja[k]];
+      __syncthreads();
+      if (tid == 0)
+        for (int k = c; k < ce; ++k) s += prod[k - c];
+      __syncthreads();
+    }
+    if (tid == 0) {
+      y[r0] = s;
+      if (EPI == 1) pv[0] += e1[r0] * s;
+      if (EPI == 2) {
+        pv[0] += s * e1[r0];
+        pv[1] += s * s;
+      }
+    }
+  }
+  if (EPI != 0) {
+    __syncthreads();
+    block_sum<2, kSpmvBlock>(pv, red);
+    if (tid == 0) {
+      partials[(size_t)b * 2 + 0] = pv[0];
+      partials[(size_t)b * 2 + 1] = pv[1];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Level-scheduled sync-free factor and sweeps.  At sfac the host assigns every row its level in
 // the dependency DAG of the lower (forward) or upper (backward) factor and lists the rows level by
@@ -492,6 +599,18 @@ void launch_spmv(int epi, int nblk, const int* rowblk, const int* ia, const int*
     hipLaunchKernelGGL(k_spmv<1>, dim3(nblk), dim3(kSpmvBlock), 0, st, rowblk, ia, ja, a, x, y, e1, partials);
   else
     hipLaunchKernelGGL(k_spmv<2>, dim3(nblk), dim3(kSpmvBlock), 0, st, rowblk, ia, ja, a, x, y, e1, partials);
+}
+
+void launch_spmv2(int epi, int nblk, const int4* desc, const int* ia, const int* ja, const double* a, const double* x,
+                  double* y, const double* e1, double* partials, hipStream_t st) {
+  if (nblk <= 0) return;
+  const dim3 g((unsigned)((nblk + 7) / 8 * 8)), bl(kSpmvBlock);
+  if (epi == 0)
+    hipLaunchKernelGGL(k_spmv2<0>, g, bl, 0, st, desc, nblk, ia, ja, a, x, y, e1, partials);
+  else if (epi == 1)
+    hipLaunchKernelGGL(k_spmv2<1>, g, bl, 0, st, desc, nblk, ia, ja, a, x, y, e1, partials);
+  else
+    hipLaunchKernelGGL(k_spmv2<2>, g, bl, 0, st, desc, nblk, ia, ja, a, x, y, e1, partials);
 }
 
 void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
