@@ -165,6 +165,9 @@ class Engine final : public EngineBase {
     }
     z_.alloc((size_t)nF_ * K);
     gcache_.alloc((size_t)nF_ * (K + 1));
+    tieList_.alloc((size_t)nF_ / 64 + 1);  // prox blocks queued for the exact recomputation
+    tieCount_.alloc(1);
+    MMX_HIP(hipMemsetAsync(tieCount_.p, 0, sizeof(unsigned), st_));
     u_.alloc((size_t)nF_ * K);
     gs_.alloc((size_t)nF_ * K);
     MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
@@ -587,6 +590,12 @@ class Engine final : public EngineBase {
     m.inc_off = incOff_.p;
     m.remote = nranks_ > 1 ? remote_.p : nullptr;
     m.gcache = gcache_.p;
+    m.tieList = tieList_.p;
+    m.tieCount = tieCount_.p;
+    {
+      const char* ft = getenv("MMX_FORCE_TIE");
+      m.forceTie = ft ? atoi(ft) : 0;
+    }
     m.invdiag = invdiag_.p;
     m.Vc = compMesh_ ? Vc_.p : nullptr;
     m.gx = gx_.p;
@@ -650,7 +659,8 @@ class Engine final : public EngineBase {
   DevBuf<uint8_t> sbits_, interior_;
   DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, gcache_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
-  DevBuf<int32_t> expOff_;
+  DevBuf<int32_t> expOff_, tieList_;
+  DevBuf<unsigned> tieCount_;
   PartitionPlan plan_;
   Comm* comm_ = nullptr;
   int rank_ = 0, nranks_ = 1;

@@ -187,15 +187,15 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
 }
 
 // exponents d*p/2, d*p/2-1 for this dimension
-template <int D>
-__device__ __forceinline__ double pow_dp2(double x) {
-  if constexpr (D == 2) return cr_pow_p15(x);
-  else return cr_pow_p225(x);
+template <int D, bool EXACT>
+__device__ __forceinline__ double pow_dp2(double x, bool& tie) {
+  if constexpr (D == 2) return cr_pow_p15<EXACT>(x, tie);
+  else return cr_pow_p225<EXACT>(x, tie);
 }
-template <int D>
-__device__ __forceinline__ double pow_dp2m1(double x) {
+template <int D, bool EXACT>
+__device__ __forceinline__ double pow_dp2m1(double x, bool& tie) {
   if constexpr (D == 2) return cr_pow_p05(x);
-  else return cr_pow_p125(x);
+  else return cr_pow_p125<EXACT>(x, tie);
 }
 
 // AdaptationFunctional<D>::blockGrad (src/AdaptationFunctional.cpp:102-287).
@@ -203,10 +203,14 @@ __device__ __forceinline__ double pow_dp2m1(double x) {
 // An inverted element (assert(Edet > 0), line 174) returns NaN and a NaN gradient.
 // ghuang (optional): receives the unregularised gradient |K| dG (K values) and Igt (entry K) --
 // the part of the result that depends on z alone, reused by the next prox at the same z.
-template <int D, bool GRAD, bool REG>
+// EXACT = false (prox fast path): a power too close to a rounding midpoint, or outside the
+// double-double ranges, raises *tie instead of being resolved; the results are then void.
+template <int D, bool GRAD, bool REG, bool EXACT = true>
 __device__ __forceinline__ double blockGrad(const GridView<D>& g, const FunctionalConsts<D>& fc,
                                             const double* z, const double* xi, const double* dxpu,
-                                            double* grad, double& Igt, double* ghuang = nullptr) {
+                                            double* grad, double& Igt, double* ghuang = nullptr,
+                                            bool* tiep = nullptr) {
+  bool tie = false;
   constexpr int K = D * (D + 1);
   const double dFact = (D == 2) ? 2.0 : 6.0;
   M<D> mPre[D + 1], Msum;
@@ -256,8 +260,8 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
   const M<D> JMJt = mul<D>(FJ, MinvJt);
   const double trJMJt = trace<D>(JMJt);
   const double detM = cr_sqrt(1.0 / det<D>(Minv));
-  const double tr_dp2 = pow_dp2<D>(trJMJt);
-  const double G = theta * detM * tr_dp2 + (1.0 - 2.0 * theta) * fc.powd * detM * cr_pow_p15(detFJ / detM);
+  const double tr_dp2 = pow_dp2<D, EXACT>(trJMJt, tie);
+  const double G = theta * detM * tr_dp2 + (1.0 - 2.0 * theta) * fc.powd * detM * cr_pow_p15<EXACT>(detFJ / detM, tie);
   const double absK = __builtin_fabs(Edet / dFact);
   double sq = 0.0;
   if constexpr (REG) {
@@ -267,13 +271,14 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
       sq = (i == 0) ? t * t : sq + t * t;
     }
   }
+  if constexpr (!EXACT) *tiep = *tiep || tie;
   if constexpr (!GRAD) {
     Igt = absK * G;
     if constexpr (REG) return absK * G + 0.5 * fc.w * fc.w * sq;
     return absK * G;
   } else {
-    const double tr_dp2m1 = pow_dp2m1<D>(trJMJt);
-    const double detM_1mp = cr_pow_m05(detM);
+    const double tr_dp2m1 = pow_dp2m1<D, EXACT>(trJMJt, tie);
+    const double detM_1mp = cr_pow_m05<EXACT>(detM, tie);
     M<D> dGdJ;
     {
       const double s = d * p * theta * detM * tr_dp2m1;
@@ -294,7 +299,7 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
         for (int c = 0; c < D; ++c) T.m[r][c] = s1 * MinvT.m[r][c];
       T = mul<D>(mul<D>(mul<D>(T, FJt), FJ), Minv);
       const double s2 = 0.5 * theta * detM * tr_dp2 +
-                        ((0.5 - theta) * (1.0 - p) * fc.powd) * detM_1mp * cr_pow_p15(detFJ);
+                        ((0.5 - theta) * (1.0 - p) * fc.powd) * detM_1mp * cr_pow_p15<EXACT>(detFJ, tie);
 #pragma unroll
       for (int r = 0; r < D; ++r)
 #pragma unroll
@@ -342,6 +347,7 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
     for (int i = 0; i < K; ++i) grad[i] *= absK;
     double Ih = absK * G;
     Igt = Ih;
+    if constexpr (!EXACT) *tiep = *tiep || tie;
     if (ghuang) {
 #pragma unroll
       for (int i = 0; i < K; ++i) ghuang[i] = grad[i];

@@ -21,6 +21,9 @@ struct DeviceMesh {
                           // rank: its D values are row r of `remote` (element partition)
   const double* remote;   // gathered interface-slot values of the other ranks (or nullptr)
   double* gcache;         // per simplex K+1: unregularised gradient and energy at the current z
+  int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
+  unsigned* tieCount;
+  int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)
   const double* Vc;       // nP x D reference positions (CompMesh) or nullptr
   // monitor grid

@@ -324,10 +324,13 @@ struct LdsB {
 
 // Mesh<D>::bfgsOptSimplex iteration loop (src/Mesh.cpp:827-856): inverse-BFGS without line
 // search, <= 50 iterations, stop when ||grad||_1 < tol.  Returns the iteration count.
-template <int D, class BA>
+// EXACT = false: the fast path; a power near a rounding midpoint raises *tie (the caller then
+// recomputes the simplex exactly) and the loop stops.
+template <int D, class BA, bool EXACT = true>
 __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g, const FunctionalConsts<D>& fc,
                                                double* z, const double* xi, const double* dx, double* G,
-                                               unsigned fixedBits, double tol, bool& bad, double* gcache) {
+                                               unsigned fixedBits, double tol, bool& bad, double* gcache,
+                                               bool* tie = nullptr) {
   constexpr int K = D * (D + 1);
   int iter;
   for (iter = 0; iter < 50; iter++) {
@@ -344,9 +347,17 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
 #pragma unroll
     for (int i = 0; i < K; ++i) z[i] += pk[i];
     double G1[K], Igt;
+#ifdef MMX_EXP_NOGRAD  // experiment: no blockGrad in the loop (measures memory + B algebra)
+#pragma unroll
+    for (int i = 0; i < K; ++i) G1[i] = G[i] * 0.5;
+#else
     {
-      const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G1, Igt, gcache);
+      const double e = blockGrad<D, true, true, EXACT>(g, fc, z, xi, dx, G1, Igt, gcache, tie);
       bad |= (e != e);
+    }
+#endif
+    if constexpr (!EXACT) {
+      if (*tie) break;
     }
     zeroFixed<D>(G1, fixedBits);
     double Ix = 0;
@@ -402,6 +413,9 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
     MMX_ROW_FENCE(BA);
 #pragma unroll
     for (int i = 0; i < K; ++i) G[i] = G1[i];
+#ifdef MMX_EXP_ONEITER  // experiment: exactly one BFGS iteration
+    break;
+#endif
     if (Ix < tol) break;
   }
   return (iter == 50) ? 50 : iter + 1;
@@ -410,10 +424,10 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
 // Entry gradient of the prox: the full regularised blockGrad, or -- when z is unchanged since the
 // previous prox -- its cached unregularised part plus the regulariser, added exactly as blockGrad
 // adds it (bit-identical).
-template <int D>
+template <int D, bool EXACT = true>
 __device__ __forceinline__ void entry_grad(const GridView<D>& g, const FunctionalConsts<D>& fc, const double* z,
                                            const double* xi, const double* dx, const double* cache, bool useCache,
-                                           double* G, double& Igt, bool& bad) {
+                                           double* G, double& Igt, bool& bad, bool* tie = nullptr) {
   constexpr int K = D * (D + 1);
   if (useCache) {
 #pragma unroll
@@ -423,7 +437,7 @@ __device__ __forceinline__ void entry_grad(const GridView<D>& g, const Functiona
     for (int i = 0; i < K; ++i) G[i] += fc.w * fc.w * (-dx[i] + z[i]);
     bad |= (Igt != Igt);
   } else {
-    const double e = blockGrad<D, true, true>(g, fc, z, xi, dx, G, Igt);
+    const double e = blockGrad<D, true, true, EXACT>(g, fc, z, xi, dx, G, Igt, nullptr, tie);
     bad |= (e != e);
   }
 }
@@ -431,93 +445,124 @@ __device__ __forceinline__ void entry_grad(const GridView<D>& g, const Functiona
 // The prox (src/Mesh.cpp:930-994 / 777-872), one lane per simplex.  FIRST = the first prox of
 // the run, which builds the finite-difference Hessian and inverts it.
 template <int D, bool FIRST>
+__device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol, const double* __restrict__ x,
+                                             double* __restrict__ zg, double* __restrict__ ug,
+                                             double* __restrict__ Bg, bool useCache, int s, double (&pv)[6]) {
+  constexpr int K = D * (D + 1);
+  const GridView<D> g = gridOf<D>(m);
+  const FunctionalConsts<D> fc = constsOf<D>(m);
+  int f[D + 1];
+  loadVerts<D>(m, s, f);
+  const unsigned bits = m.sbits[s];
+  const unsigned fixedBits = bits & 0xF;
+  double xi[K];
+  loadXi<D>(m, f, xi);
+  double dx[K], z[K], zold[K];
+  gatherX<D>(x, f, dx);
+  double* zs = zg + (size_t)s * K;
+  double* us = ug + (size_t)s * K;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    dx[i] = dx[i] + us[i];  // DXpU = D x + uBar
+    z[i] = zs[i];
+    zold[i] = z[i];
+  }
+  double B[K * K];
+  double* Bs = Bg + (size_t)s * K * K;
+  if constexpr (!FIRST) {
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) B[i] = Bs[i];
+  }
+  double G[K], G1[K], Igt;
+  bool bad = false;
+  (void)G1;
+  double* gc = m.gcache + (size_t)s * (K + 1);
+  entry_grad<D>(g, fc, z, xi, dx, gc, !FIRST && useCache, G, Igt, bad);
+  zeroFixed<D>(G, fixedBits);
+  const double Ihsave = Igt;
+  if constexpr (FIRST) {
+    const double h = 2.0 * cr_sqrt(2.220446049250313080847e-16);
+    double zp[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) zp[i] = z[i];
+    for (int i = 0; i < K; i++) {
+      zp[i] += h;
+      double Ig2;
+      blockGrad<D, true, true>(g, fc, zp, xi, dx, G1, Ig2);
+      zeroFixed<D>(G1, fixedBits);
+#pragma unroll
+      for (int r = 0; r < K; ++r) B[r * K + i] = (G1[r] - G[r]) / h;
+      zp[i] = z[i];
+    }
+#pragma unroll
+    for (int n = 0; n < D + 1; n++)
+      if (bits & (1u << (4 + n)))
+#pragma unroll
+        for (int c = 0; c < D; c++) B[(D * n + c) * K + D * n + c] = 1.0;
+    invertK<K>(B);
+  }
+  RegB<K> Bacc{B};
+  const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc);
+  double dual2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    zs[i] = z[i];
+    us[i] = dx[i] - z[i];  // uBar = DXpU - z
+    const double d = z[i] - zold[i];
+    dual2 += d * d;
+  }
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) Bs[i] = B[i];
+  pv[0] = Ihsave;
+  pv[1] = dual2;
+  pv[3] = (double)its;
+  pv[4] = bad ? 1.0 : 0.0;
+  pv[5] = (double)its;
+}
+
+template <int D, bool FIRST>
 __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                   double* __restrict__ zg, double* __restrict__ ug,
                                                   double* __restrict__ Bg, double* __restrict__ partials,
                                                   int useCache) {
-  constexpr int K = D * (D + 1);
   const int s = blockIdx.x * kBlock + threadIdx.x;
   double pv[6] = {0, 0, 0, 0, 0, 0};
-  if (s < m.nF) {
-    const GridView<D> g = gridOf<D>(m);
-    const FunctionalConsts<D> fc = constsOf<D>(m);
-    int f[D + 1];
-    loadVerts<D>(m, s, f);
-    const unsigned bits = m.sbits[s];
-    const unsigned fixedBits = bits & 0xF;
-    double xi[K];
-    loadXi<D>(m, f, xi);
-    double dx[K], z[K], zold[K];
-    gatherX<D>(x, f, dx);
-    double* zs = zg + (size_t)s * K;
-    double* us = ug + (size_t)s * K;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      dx[i] = dx[i] + us[i];  // DXpU = D x + uBar
-      z[i] = zs[i];
-      zold[i] = z[i];
-    }
-    double B[K * K];
-    double* Bs = Bg + (size_t)s * K * K;
-    if constexpr (!FIRST) {
-#pragma unroll
-      for (int i = 0; i < K * K; ++i) B[i] = Bs[i];
-    }
-    double G[K], G1[K], Igt;
-    bool bad = false;
-    (void)G1;
-    double* gc = m.gcache + (size_t)s * (K + 1);
-    entry_grad<D>(g, fc, z, xi, dx, gc, !FIRST && useCache, G, Igt, bad);
-    zeroFixed<D>(G, fixedBits);
-    const double Ihsave = Igt;
-    if constexpr (FIRST) {
-      const double h = 2.0 * cr_sqrt(2.220446049250313080847e-16);
-      double zp[K];
-#pragma unroll
-      for (int i = 0; i < K; ++i) zp[i] = z[i];
-      for (int i = 0; i < K; i++) {
-        zp[i] += h;
-        double Ig2;
-        blockGrad<D, true, true>(g, fc, zp, xi, dx, G1, Ig2);
-        zeroFixed<D>(G1, fixedBits);
-#pragma unroll
-        for (int r = 0; r < K; ++r) B[r * K + i] = (G1[r] - G[r]) / h;
-        zp[i] = z[i];
-      }
-#pragma unroll
-      for (int n = 0; n < D + 1; n++)
-        if (bits & (1u << (4 + n)))
-#pragma unroll
-          for (int c = 0; c < D; c++) B[(D * n + c) * K + D * n + c] = 1.0;
-      invertK<K>(B);
-    }
-    RegB<K> Bacc{B};
-    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc);
-    double dual2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      zs[i] = z[i];
-      us[i] = dx[i] - z[i];  // uBar = DXpU - z
-      const double d = z[i] - zold[i];
-      dual2 += d * d;
-    }
-#pragma unroll
-    for (int i = 0; i < K * K; ++i) Bs[i] = B[i];
-    pv[0] = Ihsave;
-    pv[1] = dual2;
-    pv[3] = (double)its;
-    pv[4] = bad ? 1.0 : 0.0;
-    pv[5] = (double)its;
-  }
+  if (s < m.nF) prox_simplex<D, FIRST>(m, tol, x, zg, ug, Bg, useCache != 0, s, pv);
   block_partials<6>(pv, partials);
 }
 
+// Exact recomputation of the steady-state prox for the blocks whose fast pass (k_prox_lds) met a
+// power within 2^-95 of a rounding midpoint (or outside the double-double ranges): such a block
+// wrote nothing back (z, u, Bkinv unchanged), so each of its simplices restarts from its inputs
+// with cr_resolve, Bkinv in registers and a full entry blockGrad (bit-identical to the cached
+// form, which the fast pass may have overwritten), and the block's partials are formed with the
+// same workgroup shape -- the same values in the same tree.  One workgroup walks the list (ties
+// are rare; with none it only reads the counter) and re-arms the counter for the next prox.
+template <int D, int BS>
+__global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+                                                 double* __restrict__ zg, double* __restrict__ ug,
+                                                 double* __restrict__ Bg, double* __restrict__ partials) {
+  const unsigned n = *m.tieCount;
+  for (unsigned i = 0; i < n; ++i) {
+    const int b = m.tieList[i];
+    const int s = b * BS + (int)threadIdx.x;
+    double pv[6] = {0, 0, 0, 0, 0, 0};
+    if (s < m.nF) prox_simplex<D, false>(m, tol, x, zg, ug, Bg, false, s, pv);
+    block_partials<6, BS>(pv, partials, b);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && n != 0) *m.tieCount = 0u;
+}
 
 // Steady-state prox (every prox after the first), Bkinv staged through LDS.  The workgroup's
-// 256 simplices own one contiguous Bkinv chunk (256 x K*K doubles): it is read and written
-// back with 16-byte-per-lane fully coalesced accesses and held in LDS as a padded
-// structure-of-arrays image [K*K][257], so each lane's BFGS reads its own matrix
-// conflict-free and the registers it frees give two waves per SIMD.
+// BS simplices own one contiguous Bkinv chunk (BS x K*K doubles): it is read and written back
+// with 16-byte-per-lane fully coalesced accesses and held in LDS as a padded structure-of-arrays
+// image [K*K][BS+1], so each lane's BFGS reads its own matrix conflict-free and the registers it
+// frees give two waves per SIMD.  Each lane's own inputs (vertices, z, u, the cached gradient)
+// are requested before the chunk, so their latency hides under it.
+// Fast path: the powers are not tie-resolved here (EXACT = false).  If any lane of the block
+// meets a near-midpoint power the whole block writes nothing back and is queued for k_prox_fix,
+// which recomputes it exactly from the untouched inputs.
 template <int D, int BS>
 __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                         double* __restrict__ zg, double* __restrict__ ug,
@@ -528,6 +573,25 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   const int tid = threadIdx.x;
   const int s0 = blockIdx.x * BS;
   const int nIn = min(BS, m.nF - s0);
+  const bool act = tid < nIn;
+  const int s = act ? s0 + tid : s0;  // inactive lanes shadow the first simplex, store nothing
+  // the lane's inputs, requested first
+  int f[D + 1];
+  loadVerts<D>(m, s, f);
+  const unsigned fixedBits = m.sbits[s] & 0xF;
+  double* zs = zg + (size_t)s * K;
+  double* us = ug + (size_t)s * K;
+  double* gc = m.gcache + (size_t)s * (K + 1);
+  double z[K], dx[K], gcv[K + 1];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    z[i] = zs[i];
+    dx[i] = us[i];
+  }
+  if (useCache) {
+#pragma unroll
+    for (int i = 0; i <= K; ++i) gcv[i] = gc[i];
+  }
   double* chunk = Bg + (size_t)s0 * KK;
   const int tot = nIn * KK;  // even: K*K is even
 #pragma unroll 4
@@ -543,52 +607,55 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     lds[ka * (BS + 1) + sa] = v.x;
     lds[kb * (BS + 1) + sb] = v.y;
   }
+  double xi[K];
+  loadXi<D>(m, f, xi);
+  {
+    double dxv[K];
+    gatherX<D>(x, f, dxv);
+#pragma unroll
+    for (int i = 0; i < K; ++i) dx[i] = dxv[i] + dx[i];  // DXpU = D x + uBar
+  }
   __syncthreads();
   double pv[6] = {0, 0, 0, 0, 0, 0};
-  const int s = s0 + tid;
-  if (tid < nIn) {
+  bool tie = false;
+  if (act) {
     const GridView<D> g = gridOf<D>(m);
     const FunctionalConsts<D> fc = constsOf<D>(m);
-    int f[D + 1];
-    loadVerts<D>(m, s, f);
-    const unsigned fixedBits = m.sbits[s] & 0xF;
-    double xi[K];
-    loadXi<D>(m, f, xi);
-    double dx[K], z[K];
-    gatherX<D>(x, f, dx);
-    double* zs = zg + (size_t)s * K;
-    double* us = ug + (size_t)s * K;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      dx[i] = dx[i] + us[i];  // DXpU = D x + uBar
-      z[i] = zs[i];
-    }
     double G[K], Igt;
     bool bad = false;
-    double* gc = m.gcache + (size_t)s * (K + 1);
-    entry_grad<D>(g, fc, z, xi, dx, gc, useCache != 0, G, Igt, bad);
+    entry_grad<D, false>(g, fc, z, xi, dx, gcv, useCache != 0, G, Igt, bad, &tie);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
     LdsB<K, BS + 1> Bacc{lds + tid};
-    const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc);
+    const int its =
+        tie ? 0 : bfgs_iterations<D, LdsB<K, BS + 1>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       const double d = z[i] - zs[i];
       dual2 += d * d;
     }
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      zs[i] = z[i];
-      us[i] = dx[i] - z[i];  // uBar = DXpU - z
-    }
+#if defined(MMX_EXP_NOGRAD) || defined(MMX_EXP_NOB)
+    bad = false;  // timing experiments: the numerics are meaningless
+#endif
     pv[0] = Ihsave;
     pv[1] = dual2;
     pv[3] = (double)its;
     pv[4] = bad ? 1.0 : 0.0;
     pv[5] = (double)its;
   }
-  __syncthreads();
+  if (m.forceTie > 0 && tid == 0 && (int)(blockIdx.x % (unsigned)m.forceTie) == 0) tie = true;
+  if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to k_prox_fix
+    if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = (int)blockIdx.x;
+    return;
+  }
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      zs[i] = z[i];
+      us[i] = dx[i] - z[i];  // uBar = DXpU - z
+    }
+  }
 #pragma unroll 4
   for (int e = tid * 2; e < tot; e += BS * 2) {
     const int sa = e / KK, ka = e - sa * KK;
@@ -944,12 +1011,16 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
     if constexpr (D == 2) {
       const int bs = prox_block();
       *nblocks = (m.nF + bs - 1) / bs;
-      if (bs == 64)
+      if (bs == 64) {
         hipLaunchKernelGGL((k_prox_lds<D, 64>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, B, partials, uc);
-      else if (bs == 128)
+        hipLaunchKernelGGL((k_prox_fix<D, 64>), dim3(1), dim3(64), 0, st, m, tol, x, z, u, B, partials);
+      } else if (bs == 128) {
         hipLaunchKernelGGL((k_prox_lds<D, 128>), dim3(*nblocks), dim3(128), 0, st, m, tol, x, z, u, B, partials, uc);
-      else
+        hipLaunchKernelGGL((k_prox_fix<D, 128>), dim3(1), dim3(128), 0, st, m, tol, x, z, u, B, partials);
+      } else {
         hipLaunchKernelGGL((k_prox_lds<D, 256>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, B, partials, uc);
+        hipLaunchKernelGGL((k_prox_fix<D, 256>), dim3(1), dim3(256), 0, st, m, tol, x, z, u, B, partials);
+      }
     } else {
       hipLaunchKernelGGL((k_prox<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials, uc);
     }

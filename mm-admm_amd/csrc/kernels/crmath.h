@@ -279,8 +279,12 @@ MMX_HD_COLD double cr_resolve(double x, int num, int den, double h, int dir) {
 }
 
 // Round a normalised double-double (hi = RN(hi + lo)) that approximates x^(num/den) with
-// relative error < 2^-100; falls back to the exact decision near a midpoint.
-MMX_HD double cr_round(double x, int num, int den, double hi, double lo) {
+// relative error < 2^-100; near a midpoint the exact decision (cr_resolve) is needed.
+// EXACT = false is the fast path of the prox kernels: instead of resolving it raises `tie` and
+// returns a placeholder; the caller discards the lane's results and recomputes the simplex with
+// EXACT = true (so cr_resolve, its calls and its stack stay out of the hot kernel body).
+template <bool EXACT>
+MMX_HD double cr_round_t(double x, int num, int den, double hi, double lo, bool& tie) {
   double h, l;
   xp::two_sum(hi, lo, h, l);
   if (l == 0.0) {
@@ -295,8 +299,18 @@ MMX_HD double cr_round(double x, int num, int den, double hi, double lo) {
 #ifdef MMX_CR_NO_RESOLVE  // performance experiments only: skips the exact tie decision
   return h;
 #else
-  return cr_resolve(x, num, den, h, dir);
+  if constexpr (EXACT) {
+    return cr_resolve(x, num, den, h, dir);
+  } else {
+    tie = true;
+    return h;
+  }
 #endif
+}
+
+MMX_HD double cr_round(double x, int num, int den, double hi, double lo) {
+  bool t = false;
+  return cr_round_t<true>(x, num, den, hi, lo, t);
 }
 
 // sqrt(x) = s + e, |error| < 2^-104 |s|
@@ -309,25 +323,39 @@ MMX_HD void cr_sqrt_dd(double x, double& s, double& e) {
 // x^0.5 -- correctly rounded sqrt
 MMX_HD double cr_pow_p05(double x) { return cr_sqrt(x); }
 
+// Outside the ranges below the powers defer to the library pow (EXACT) or raise `tie` (fast
+// path: the exact recomputation takes the library call).
+#define MMX_CR_RANGE(lo, hi, e)         \
+  if (!cr_in(x, lo, hi)) {              \
+    if constexpr (EXACT) {              \
+      return ::pow(x, e);               \
+    } else {                            \
+      tie = true;                       \
+      return 1.0;                       \
+    }                                   \
+  }
+
 // x^1.5
-MMX_HD double cr_pow_p15(double x) {
-  if (!cr_in(x, 1e-90, 1e90)) return ::pow(x, 1.5);
+template <bool EXACT>
+MMX_HD double cr_pow_p15(double x, bool& tie) {
+  MMX_CR_RANGE(1e-90, 1e90, 1.5)
   double s, e;
   cr_sqrt_dd(x, s, e);
   const double p = x * s;
   const double lo = cr_fma(x, s, -p) + x * e;
-  return cr_round(x, 3, 2, p, lo);
+  return cr_round_t<EXACT>(x, 3, 2, p, lo, tie);
 }
 
 // x^-0.5
-MMX_HD double cr_pow_m05(double x) {
-  if (!cr_in(x, 1e-100, 1e100)) return ::pow(x, -0.5);
+template <bool EXACT>
+MMX_HD double cr_pow_m05(double x, bool& tie) {
+  MMX_CR_RANGE(1e-100, 1e100, -0.5)
   double s, e;
   cr_sqrt_dd(x, s, e);
   const double q = 1.0 / s;
   const double d = cr_fma(-q, s, 1.0);  // 1 - q*s, exact
   const double u = d - q * e;           // 1 - q*(s + e)
-  return cr_round(x, -1, 2, q, q * u);
+  return cr_round_t<EXACT>(x, -1, 2, q, q * u, tie);
 }
 
 // x^0.25 as hi + lo, |error| < 2^-103 |hi|
@@ -341,25 +369,46 @@ MMX_HD void cr_qrt_dd(double x, double& hi, double& lo) {
 }
 
 // x^2.25 = x^2 * x^0.25
-MMX_HD double cr_pow_p225(double x) {
-  if (!cr_in(x, 1e-30, 1e30)) return ::pow(x, 2.25);
+template <bool EXACT>
+MMX_HD double cr_pow_p225(double x, bool& tie) {
+  MMX_CR_RANGE(1e-30, 1e30, 2.25)
   double b, lo4;
   cr_qrt_dd(x, b, lo4);
   const double X2 = x * x;
   const double X2e = cr_fma(x, x, -X2);
   const double hi = X2 * b;
   const double lo = cr_fma(X2, b, -hi) + (X2 * lo4 + X2e * b);
-  return cr_round(x, 9, 4, hi, lo);
+  return cr_round_t<EXACT>(x, 9, 4, hi, lo, tie);
 }
 
 // x^1.25 = x * x^0.25
-MMX_HD double cr_pow_p125(double x) {
-  if (!cr_in(x, 1e-50, 1e50)) return ::pow(x, 1.25);
+template <bool EXACT>
+MMX_HD double cr_pow_p125(double x, bool& tie) {
+  MMX_CR_RANGE(1e-50, 1e50, 1.25)
   double b, lo4;
   cr_qrt_dd(x, b, lo4);
   const double hi = x * b;
   const double lo = cr_fma(x, b, -hi) + x * lo4;
-  return cr_round(x, 5, 4, hi, lo);
+  return cr_round_t<EXACT>(x, 5, 4, hi, lo, tie);
+}
+#undef MMX_CR_RANGE
+
+// the correctly rounded powers as plain functions
+MMX_HD double cr_pow_p15(double x) {
+  bool t = false;
+  return cr_pow_p15<true>(x, t);
+}
+MMX_HD double cr_pow_m05(double x) {
+  bool t = false;
+  return cr_pow_m05<true>(x, t);
+}
+MMX_HD double cr_pow_p225(double x) {
+  bool t = false;
+  return cr_pow_p225<true>(x, t);
+}
+MMX_HD double cr_pow_p125(double x) {
+  bool t = false;
+  return cr_pow_p125<true>(x, t);
 }
 
 // c2^2 (reference src/Mesh.cpp:847 pow(c2, 2.0)) is exactly the rounded square.

@@ -94,6 +94,29 @@ def test_steps_bitwise(name):
     assert G.stats()["bfgs_iters"] == O.bfgs_iters()
 
 
+@pytest.mark.parametrize("name", ["hexdisc12_mex1", "rect16_mex2", "C1_circle24_mex5"])
+def test_exact_recompute_path_bitwise(name, monkeypatch):
+    """The steady-state prox skips cr_resolve; a block whose powers come near a rounding midpoint
+    is recomputed exactly by k_prox_fix.  MMX_FORCE_TIE=2 sends every second block down that path:
+    the state and the energies (same partial-sum trees) must not change by a bit."""
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    O, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    monkeypatch.setenv("MMX_FORCE_TIE", "2")
+    _, Gt = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    monkeypatch.delenv("MMX_FORCE_TIE")
+    for s in range(3):
+        ih_o = O.step(5, -1.0)[0]
+        ih_g = G.step(5, -1.0)[0]
+        ih_t = Gt.step(5, -1.0)[0]
+        assert ih_t == ih_g
+        for f in ("x", "z", "u"):
+            np.testing.assert_array_equal(Gt.get(f), O.get(f), err_msg=f"{f} step {s}")
+    np.testing.assert_array_equal(Gt.get("hess"), O.get("hess"))
+    np.testing.assert_array_equal(Gt.get("hess"), G.get("hess"))
+    assert Gt.stats()["bfgs_iters"] == O.bfgs_iters()
+
+
 @pytest.mark.parametrize("name", list(cases()))
 def test_steps_reference_semantics(name):
     """glibc pow + Eigen Jacobi-CG (the reference's arithmetic): <= 1e-10 node positions."""
