@@ -172,10 +172,14 @@ class Engine final : public EngineBase {
     gs_.alloc((size_t)nF_ * K);
     MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
     {
-      std::vector<double> eye((size_t)nF_ * K * K, 0.0);  // hessInvs = I (src/Mesh.cpp:456-464)
+      // hessInvs = I (src/Mesh.cpp:456-464).  2D: simplex-major; 3D: wave-interleaved and
+      // double-buffered (k_prox_wave), padded to whole groups of 64 simplices
+      const size_t nB = (D == 2) ? (size_t)nF_ * K * K : (size_t)((nF_ + 63) / 64) * 64 * K * K;
+      std::vector<double> eye(nB, 0.0);
       for (int s = 0; s < nF_; ++s)
-        for (int i = 0; i < K; ++i) eye[(size_t)s * K * K + i * K + i] = 1.0;
+        for (int i = 0; i < K; ++i) eye[bIndex(s, i * K + i)] = 1.0;
       B_.upload(eye.data(), eye.size(), st_);
+      if (D == 3) B2_.alloc(nB);
     }
     // prox workgroups can be 64 lanes; node kernels pad their grid to a multiple of 8 (XCD map)
     const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 63) / 64, (nP_ + 255) / 256 + 8));
@@ -233,8 +237,10 @@ class Engine final : public EngineBase {
         a0 = nextEvent();
         MMX_HIP(hipEventRecord(a0, st_));
       }
+      const bool swapB = (D == 3) && hessComputed_;  // 3D steady state: B_ -> B2_, then swap
       launch_prox<D>(m_, !hessComputed_, gcacheValid_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p,
-                     partA_.p, &nbp, st_);
+                     swapB ? B2_.p : B_.p, partA_.p, &nbp, st_);
+      if (swapB) std::swap(B_.p, B2_.p);
       gcacheValid_ = true;  // the prox's last blockGrad left the gradient at the final z
       if (timing) {
         a1 = nextEvent();
@@ -427,8 +433,22 @@ class Engine final : public EngineBase {
     } else {
       throw Error(MMADMM_ERR_INVALID, "mmadmm_get: unknown field '" + what + "'");
     }
+    if (b == &B_ && D == 3) {  // wave-interleaved on the device: return simplex-major
+      std::vector<double> h(b->n);
+      MMX_HIP(hipMemcpyAsync(h.data(), b->p, b->n * sizeof(double), hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+      for (int s = 0; s < nF_; ++s)
+        for (int ij = 0; ij < K * K; ++ij) out[(size_t)s * K * K + ij] = h[bIndex(s, ij)];
+      return;
+    }
     MMX_HIP(hipMemcpyAsync(out, b->p, b->n * sizeof(double), hipMemcpyDeviceToHost, st_));
     MMX_HIP(hipStreamSynchronize(st_));
+  }
+
+  // host mirror of bidx<D> (admm_kernels.hip)
+  static size_t bIndex(int s, int ij) {
+    if (D == 2) return (size_t)s * K * K + ij;
+    return ((size_t)(s >> 6) * K * K + ij) * 64 + (s & 63);
   }
 
   void getSimplices(int32_t* F) override {  // this rank's simplices, global node ids, re-oriented
@@ -657,7 +677,7 @@ class Engine final : public EngineBase {
   hipStream_t st_ = nullptr;
   DevBuf<int32_t> F_, incPtr_, incOff_;
   DevBuf<uint8_t> sbits_, interior_;
-  DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, gcache_;
+  DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
   DevBuf<int32_t> expOff_, tieList_;
   DevBuf<unsigned> tieCount_;

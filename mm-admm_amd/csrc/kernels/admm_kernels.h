@@ -60,7 +60,7 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
 // gradient in m.gcache; the entry blockGrad then reduces to adding the regulariser.
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z,
-                 double* u, double* B, double* partials, int* nblocks, hipStream_t st);
+                 double* u, const double* Bin, double* Bout, double* partials, int* nblocks, hipStream_t st);
 template <int D>
 void launch_energy(const DeviceMesh<D>& m, const double* x, double* partials, int* nblocks,
                    hipStream_t st);

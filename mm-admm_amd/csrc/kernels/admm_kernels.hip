@@ -304,12 +304,17 @@ __device__ void invertK(double* A) {
 }
 
 
-// Bkinv accessors: registers (first prox) or the workgroup's LDS image (steady state)
+// Bkinv accessors: registers (first prox), the workgroup's LDS image (2D steady state) or the
+// wave-interleaved global layout (3D steady state).  get/set address one entry; advance() is
+// called after each BFGS update (the global accessor then reads what it wrote).
 template <int K>
 struct RegB {
   static constexpr bool kRowFence = false;
   double* b;
-  __device__ __forceinline__ double& operator()(int i, int j) const { return b[i * K + j]; }
+  __device__ __forceinline__ double get(int i, int j) const { return b[i * K + j]; }
+  __device__ __forceinline__ void set(int i, int j, double v) const { b[i * K + j] = v; }
+  __device__ __forceinline__ void advance() {}
+  __device__ __forceinline__ void fresh() {}
 };
 // LDS image: a scheduling fence per matrix row keeps one row live at a time (otherwise the
 // scheduler hoists all K*K reads and the kernel spills)
@@ -317,8 +322,38 @@ template <int K, int STRIDE = kLdsStride>
 struct LdsB {
   static constexpr bool kRowFence = true;
   double* base;  // &lds[tid], entries strided by STRIDE
-  __device__ __forceinline__ double& operator()(int i, int j) const { return base[(i * K + j) * STRIDE]; }
+  __device__ __forceinline__ double get(int i, int j) const { return base[(i * K + j) * STRIDE]; }
+  __device__ __forceinline__ void set(int i, int j, double v) const { base[(i * K + j) * STRIDE] = v; }
+  __device__ __forceinline__ void advance() {}
+  // 2D: keeping the previous pass's K*K = 36 values in registers is cheaper than re-reading LDS
+  __device__ __forceinline__ void fresh() {}
 };
+// Global, wave-interleaved (entry ij of simplex s at ((s/64)*K*K + ij)*64 + s%64: a wavefront's
+// access to one entry is 512 contiguous bytes).  Double-buffered across proxes: the first BFGS
+// iteration reads the previous prox's buffer `rd` and writes `wr`, later iterations work in `wr`,
+// so `rd` stays intact for an exact recomputation of the block.
+template <int K>
+struct WaveB {
+  static constexpr bool kRowFence = true;
+  const double* rd;
+  double* wr;
+  __device__ __forceinline__ double get(int i, int j) const { return rd[(i * K + j) * 64]; }
+  __device__ __forceinline__ void set(int i, int j, double v) const { wr[(i * K + j) * 64] = v; }
+  __device__ __forceinline__ void advance() { rd = wr; }
+  // a pass over the matrix re-reads it: an opaque pointer stops the compiler from forwarding the
+  // previous pass's K*K = 144 loads in registers (3D spilled)
+  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)); }
+};
+
+// index of Bkinv entry ij of simplex s: 2D simplex-major (the LDS kernel's chunks), 3D
+// wave-interleaved (WaveB)
+template <int D>
+__device__ __forceinline__ size_t bidx(int s, int ij) {
+  constexpr int KK = D * (D + 1) * D * (D + 1);
+  if constexpr (D == 2) return (size_t)s * KK + ij;
+  else return ((size_t)(s >> 6) * KK + ij) * 64 + (s & 63);
+}
+
 #define MMX_ROW_FENCE(BA) \
   if constexpr (BA::kRowFence) __builtin_amdgcn_sched_barrier(0)
 
@@ -326,21 +361,27 @@ struct LdsB {
 // search, <= 50 iterations, stop when ||grad||_1 < tol.  Returns the iteration count.
 // EXACT = false: the fast path; a power near a rounding midpoint raises *tie (the caller then
 // recomputes the simplex exactly) and the loop stops.
-template <int D, class BA, bool EXACT = true>
-__device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g, const FunctionalConsts<D>& fc,
+// PS > 0 (3D): register relief for the blockGrad in the loop -- DXpU lives in LDS (`park`, entries
+// strided by PS: [0, K) DXpU, [K, 2K) G, [2K, 3K) p; the caller stores DXpU there and `dx` is
+// unused), G and p are parked there across the blockGrad, and the regulariser is added after an
+// unregularised blockGrad with blockGrad's own expressions (bit-identical, as entry_grad's cache
+// path does).
+template <int D, class BA, bool EXACT = true, int PS = 0>
+__device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const FunctionalConsts<D>& fc,
                                                double* z, const double* xi, const double* dx, double* G,
                                                unsigned fixedBits, double tol, bool& bad, double* gcache,
-                                               bool* tie = nullptr) {
+                                               bool* tie = nullptr, double* park = nullptr) {
   constexpr int K = D * (D + 1);
   int iter;
   for (iter = 0; iter < 50; iter++) {
+    B.fresh();
     double pk[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
-      double sacc = (-B(i, 0)) * G[0];
+      double sacc = (-B.get(i, 0)) * G[0];
 #pragma unroll
-      for (int j = 1; j < K; ++j) sacc += (-B(i, j)) * G[j];
+      for (int j = 1; j < K; ++j) sacc += (-B.get(i, j)) * G[j];
       pk[i] = sacc;
     }
     MMX_ROW_FENCE(BA);
@@ -351,9 +392,31 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
 #pragma unroll
     for (int i = 0; i < K; ++i) G1[i] = G[i] * 0.5;
 #else
-    {
+    if constexpr (PS == 0) {
       const double e = blockGrad<D, true, true, EXACT>(g, fc, z, xi, dx, G1, Igt, gcache, tie);
       bad |= (e != e);
+    } else {
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        park[(K + i) * PS] = G[i];
+        park[(2 * K + i) * PS] = pk[i];
+      }
+      const double e = blockGrad<D, true, false, EXACT>(g, fc, z, xi, nullptr, G1, Igt, gcache, tie);
+      double sq = 0.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const double t = park[i * PS] - z[i];
+        sq = (i == 0) ? t * t : sq + t * t;
+      }
+      const double er = e + 0.5 * fc.w * fc.w * sq;  // blockGrad<REG>'s return value
+      bad |= (er != er);
+#pragma unroll
+      for (int i = 0; i < K; ++i) G1[i] += fc.w * fc.w * (-park[i * PS] + z[i]);
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        G[i] = park[(K + i) * PS];
+        pk[i] = park[(2 * K + i) * PS];
+      }
     }
 #endif
     if constexpr (!EXACT) {
@@ -369,6 +432,7 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
     double c2 = pk[0] * yk[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) c2 += pk[i] * yk[i];
+    B.fresh();
     // one pass over B: By_i = sum_j B_ij y_j, yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij
     double yBy = 0.0, yB[K];
 #pragma unroll
@@ -376,7 +440,7 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
       MMX_ROW_FENCE(BA);
       double row[K];
 #pragma unroll
-      for (int j = 0; j < K; ++j) row[j] = B(i, j);
+      for (int j = 0; j < K; ++j) row[j] = B.get(i, j);
       double by = row[0] * yk[0];
 #pragma unroll
       for (int j = 1; j < K; ++j) by += row[j] * yk[j];
@@ -389,18 +453,26 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
 #ifdef MMX_BFGS_DIVBY
     const double rc2 = 1.0 / c2;  // the K*K divisions by c2 below: div_by, bit-identical
 #endif
+    B.fresh();
     // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
-      double row[K], nrow[K];
+      double row[K], nrow[K], ykr[K];
 #pragma unroll
-      for (int j = 0; j < K; ++j) row[j] = B(i, j);
+      for (int j = 0; j < K; ++j) row[j] = B.get(i, j);
+      // 3D: (y p^T)_qj is formed again for every row -- laundering y per row stops the compiler
+      // from keeping all K*K = 144 products live across the rows (they spilled); 2D keeps its 36
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        ykr[q] = yk[q];
+        if constexpr (D == 3) asm volatile("" : "+v"(ykr[q]));
+      }
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        double by = row[0] * (yk[0] * pk[j]);
+        double by = row[0] * (ykr[0] * pk[j]);
 #pragma unroll
-        for (int q = 1; q < K; ++q) by += row[q] * (yk[q] * pk[j]);
+        for (int q = 1; q < K; ++q) by += row[q] * (ykr[q] * pk[j]);
 #ifdef MMX_BFGS_DIVBY
         nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - div_by(by, c2, rc2)) - div_by(pk[i] * yB[j], c2, rc2));
 #else
@@ -408,9 +480,10 @@ __device__ __forceinline__ int bfgs_iterations(const BA& B, const GridView<D>& g
 #endif
       }
 #pragma unroll
-      for (int j = 0; j < K; ++j) B(i, j) = nrow[j];
+      for (int j = 0; j < K; ++j) B.set(i, j, nrow[j]);
     }
     MMX_ROW_FENCE(BA);
+    B.advance();
 #pragma unroll
     for (int i = 0; i < K; ++i) G[i] = G1[i];
 #ifdef MMX_EXP_ONEITER  // experiment: exactly one BFGS iteration
@@ -447,7 +520,8 @@ __device__ __forceinline__ void entry_grad(const GridView<D>& g, const Functiona
 template <int D, bool FIRST>
 __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol, const double* __restrict__ x,
                                              double* __restrict__ zg, double* __restrict__ ug,
-                                             double* __restrict__ Bg, bool useCache, int s, double (&pv)[6]) {
+                                             const double* Bin, double* Bout, bool useCache, int s,
+                                             double (&pv)[6]) {
   constexpr int K = D * (D + 1);
   const GridView<D> g = gridOf<D>(m);
   const FunctionalConsts<D> fc = constsOf<D>(m);
@@ -468,10 +542,9 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
     zold[i] = z[i];
   }
   double B[K * K];
-  double* Bs = Bg + (size_t)s * K * K;
   if constexpr (!FIRST) {
 #pragma unroll
-    for (int i = 0; i < K * K; ++i) B[i] = Bs[i];
+    for (int i = 0; i < K * K; ++i) B[i] = Bin[bidx<D>(s, i)];
   }
   double G[K], G1[K], Igt;
   bool bad = false;
@@ -512,7 +585,7 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
     dual2 += d * d;
   }
 #pragma unroll
-  for (int i = 0; i < K * K; ++i) Bs[i] = B[i];
+  for (int i = 0; i < K * K; ++i) Bout[bidx<D>(s, i)] = B[i];
   pv[0] = Ihsave;
   pv[1] = dual2;
   pv[3] = (double)its;
@@ -523,11 +596,11 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
 template <int D, bool FIRST>
 __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                   double* __restrict__ zg, double* __restrict__ ug,
-                                                  double* __restrict__ Bg, double* __restrict__ partials,
+                                                  const double* Bin, double* Bout, double* __restrict__ partials,
                                                   int useCache) {
   const int s = blockIdx.x * kBlock + threadIdx.x;
   double pv[6] = {0, 0, 0, 0, 0, 0};
-  if (s < m.nF) prox_simplex<D, FIRST>(m, tol, x, zg, ug, Bg, useCache != 0, s, pv);
+  if (s < m.nF) prox_simplex<D, FIRST>(m, tol, x, zg, ug, Bin, Bout, useCache != 0, s, pv);
   block_partials<6>(pv, partials);
 }
 
@@ -541,13 +614,13 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
 template <int D, int BS>
 __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                  double* __restrict__ zg, double* __restrict__ ug,
-                                                 double* __restrict__ Bg, double* __restrict__ partials) {
+                                                 const double* Bin, double* Bout, double* __restrict__ partials) {
   const unsigned n = *m.tieCount;
   for (unsigned i = 0; i < n; ++i) {
     const int b = m.tieList[i];
     const int s = b * BS + (int)threadIdx.x;
     double pv[6] = {0, 0, 0, 0, 0, 0};
-    if (s < m.nF) prox_simplex<D, false>(m, tol, x, zg, ug, Bg, false, s, pv);
+    if (s < m.nF) prox_simplex<D, false>(m, tol, x, zg, ug, Bin, Bout, false, s, pv);
     block_partials<6, BS>(pv, partials, b);
     __syncthreads();
   }
@@ -670,6 +743,95 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 #endif
   }
   block_partials<6, BS>(pv, partials);
+}
+
+// Steady-state 3D prox: one wavefront per workgroup, one lane per tetrahedron, Bkinv (144
+// doubles per tet, 1152 B: too large to stage in LDS) read straight from global memory in the
+// wave-interleaved layout -- every access of a wavefront to one entry is 512 contiguous bytes --
+// and double-buffered (WaveB): the previous prox's buffer is only read, so a block whose fast
+// pass meets a near-midpoint power (EXACT = false) is abandoned unwritten and recomputed exactly
+// by k_prox_fix from the untouched inputs, as in the 2D kernel.
+template <int D, bool COMP>
+__global__ void __launch_bounds__(64, 2) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+                                                     double* __restrict__ zg, double* __restrict__ ug,
+                                                     const double* Bin, double* Bout, double* __restrict__ partials,
+                                                     int useCache) {
+  constexpr int K = D * (D + 1), KK = K * K;
+  __shared__ double park[3 * K * 64];  // DXpU, G, p per lane (bfgs_iterations PS = 64)
+  const int tid = threadIdx.x;
+  const int s0 = blockIdx.x * 64;
+  const bool act = s0 + tid < m.nF;
+  const int s = act ? s0 + tid : s0;
+  double* pk = park + tid;
+  int f[D + 1];
+  loadVerts<D>(m, s, f);
+  const unsigned fixedBits = m.sbits[s] & 0xF;
+  double* zs = zg + (size_t)s * K;
+  double* us = ug + (size_t)s * K;
+  double* gc = m.gcache + (size_t)s * (K + 1);
+  double z[K], dx[K], gcv[K + 1];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    z[i] = zs[i];
+    dx[i] = us[i];
+  }
+  if (useCache) {
+#pragma unroll
+    for (int i = 0; i <= K; ++i) gcv[i] = gc[i];
+  }
+  double xi[K];
+  if constexpr (COMP) gatherX<D>(m.Vc, f, xi);
+  {
+    double dxv[K];
+    gatherX<D>(x, f, dxv);
+#pragma unroll
+    for (int i = 0; i < K; ++i) dx[i] = dxv[i] + dx[i];  // DXpU = D x + uBar
+  }
+  double pv[6] = {0, 0, 0, 0, 0, 0};
+  bool tie = false;
+  if (act) {
+    const GridView<D> g = gridOf<D>(m);
+    FunctionalConsts<D> fc = constsOf<D>(m);
+    fc.compMesh = COMP ? 1 : 0;
+    double G[K], Igt;
+    bool bad = false;
+    entry_grad<D, false>(g, fc, z, xi, dx, gcv, useCache != 0, G, Igt, bad, &tie);
+    zeroFixed<D>(G, fixedBits);
+    const double Ihsave = Igt;
+#pragma unroll
+    for (int i = 0; i < K; ++i) pk[i * 64] = dx[i];
+    const size_t gb = (size_t)blockIdx.x * KK * 64 + tid;
+    WaveB<K> Bacc{Bin + gb, Bout + gb};
+    const int its = tie ? 0
+                        : bfgs_iterations<D, WaveB<K>, false, 64>(Bacc, g, fc, z, xi, nullptr, G, fixedBits, tol,
+                                                                  bad, gc, &tie, pk);
+#pragma unroll
+    for (int i = 0; i < K; ++i) dx[i] = pk[i * 64];
+    double dual2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const double d = z[i] - zs[i];
+      dual2 += d * d;
+    }
+    pv[0] = Ihsave;
+    pv[1] = dual2;
+    pv[3] = (double)its;
+    pv[4] = bad ? 1.0 : 0.0;
+    pv[5] = (double)its;
+  }
+  if (m.forceTie > 0 && tid == 0 && (int)(blockIdx.x % (unsigned)m.forceTie) == 0) tie = true;
+  if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to k_prox_fix
+    if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = (int)blockIdx.x;
+    return;
+  }
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      zs[i] = z[i];
+      us[i] = dx[i] - z[i];  // uBar = DXpU - z
+    }
+  }
+  block_partials<6, 64>(pv, partials);
 }
 
 // Mesh::computeEnergy (src/Mesh.cpp:496-530) on positions x
@@ -1001,29 +1163,33 @@ static int prox_block() {
 
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z, double* u,
-                 double* B, double* partials, int* nblocks, hipStream_t st) {
+                 const double* Bin, double* Bout, double* partials, int* nblocks, hipStream_t st) {
   const int uc = (useCache && cache_enabled()) ? 1 : 0;
   *nblocks = nblk(m.nF);
   if (m.nF == 0) return;
   if (first) {
-    hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials, 0);
-  } else {
-    if constexpr (D == 2) {
-      const int bs = prox_block();
-      *nblocks = (m.nF + bs - 1) / bs;
-      if (bs == 64) {
-        hipLaunchKernelGGL((k_prox_lds<D, 64>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, B, partials, uc);
-        hipLaunchKernelGGL((k_prox_fix<D, 64>), dim3(1), dim3(64), 0, st, m, tol, x, z, u, B, partials);
-      } else if (bs == 128) {
-        hipLaunchKernelGGL((k_prox_lds<D, 128>), dim3(*nblocks), dim3(128), 0, st, m, tol, x, z, u, B, partials, uc);
-        hipLaunchKernelGGL((k_prox_fix<D, 128>), dim3(1), dim3(128), 0, st, m, tol, x, z, u, B, partials);
-      } else {
-        hipLaunchKernelGGL((k_prox_lds<D, 256>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, B, partials, uc);
-        hipLaunchKernelGGL((k_prox_fix<D, 256>), dim3(1), dim3(256), 0, st, m, tol, x, z, u, B, partials);
-      }
+    hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+  } else if constexpr (D == 2) {
+    double* B = Bout;  // in place (LDS image)
+    const int bs = prox_block();
+    *nblocks = (m.nF + bs - 1) / bs;
+    if (bs == 64) {
+      hipLaunchKernelGGL((k_prox_lds<D, 64>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, B, partials, uc);
+      hipLaunchKernelGGL((k_prox_fix<D, 64>), dim3(1), dim3(64), 0, st, m, tol, x, z, u, B, B, partials);
+    } else if (bs == 128) {
+      hipLaunchKernelGGL((k_prox_lds<D, 128>), dim3(*nblocks), dim3(128), 0, st, m, tol, x, z, u, B, partials, uc);
+      hipLaunchKernelGGL((k_prox_fix<D, 128>), dim3(1), dim3(128), 0, st, m, tol, x, z, u, B, B, partials);
     } else {
-      hipLaunchKernelGGL((k_prox<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, B, partials, uc);
+      hipLaunchKernelGGL((k_prox_lds<D, 256>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, B, partials, uc);
+      hipLaunchKernelGGL((k_prox_fix<D, 256>), dim3(1), dim3(256), 0, st, m, tol, x, z, u, B, B, partials);
     }
+  } else {
+    *nblocks = (m.nF + 63) / 64;
+    if (m.compMesh)
+      hipLaunchKernelGGL((k_prox_wave<D, true>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
+    else
+      hipLaunchKernelGGL((k_prox_wave<D, false>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
+    hipLaunchKernelGGL((k_prox_fix<D, 64>), dim3(1), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
   }
 }
 template <int D>
@@ -1105,6 +1271,7 @@ void launch_add_inplace(int n, double* x, const double* dx, hipStream_t st) {
   template void launch_xupdate<D>(const DeviceMesh<D>&, const StepScalars&, const double*, const double*, \
                                   const double*, double*, double*, int*, bool, hipStream_t);            \
   template void launch_prox<D>(const DeviceMesh<D>&, bool, bool, double, const double*, double*, double*,      \
+                               const double*,                                                                \
                                double*, double*, int*, hipStream_t);                                    \
   template void launch_energy<D>(const DeviceMesh<D>&, const double*, double*, int*, hipStream_t);       \
   template void launch_euler_apply<D>(const DeviceMesh<D>&, const double*, double*, double, hipStream_t);     \

@@ -94,7 +94,7 @@ def test_steps_bitwise(name):
     assert G.stats()["bfgs_iters"] == O.bfgs_iters()
 
 
-@pytest.mark.parametrize("name", ["hexdisc12_mex1", "rect16_mex2", "C1_circle24_mex5"])
+@pytest.mark.parametrize("name", ["hexdisc12_mex1", "rect16_mex2", "C1_circle24_mex5", "rect3d_3_mex1", "circle3d6_compmesh"])
 def test_exact_recompute_path_bitwise(name, monkeypatch):
     """The steady-state prox skips cr_resolve; a block whose powers come near a rounding midpoint
     is recomputed exactly by k_prox_fix.  MMX_FORCE_TIE=2 sends every second block down that path:
