@@ -203,13 +203,17 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
 }
 
 // x-update: vec = tau*xBar + dt^2 WD_T (w (z - u)), x = vec / t_vv (block-diagonal t),
-// optional |D x - z|^2 partial sums (primal residual, src/MeshIntegrator.cpp:162)
+// optional |D x - z|^2 partial sums (primal residual, src/MeshIntegrator.cpp:162).
+// A node's incident slots are taken 8 at a time: their offsets, then all their z and u values
+// are requested before the first is added (branch-free: lanes past the end re-read the last
+// slot, a slot of another rank reads its gathered row), then summed in ascending order.
 template <int D, bool RESID>
 __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
                                                      const double* __restrict__ xBar,
                                                      const double* __restrict__ z,
                                                      const double* __restrict__ u, double* __restrict__ x,
                                                      double* __restrict__ partials, int xcd) {
+  constexpr int CH = 8;
   const int lb = logical_block(xcd);
   const int v = lb * kBlock + threadIdx.x;
   double pv[3] = {0, 0, 0};
@@ -218,22 +222,39 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
 #pragma unroll
     for (int c = 0; c < D; ++c) acc[c] = 0.0;
     const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
-    for (int t = b; t < e; ++t) {
-      const int off = m.inc_off[t];
-      if (off >= 0) {
+    double xb[D];
 #pragma unroll
-        for (int c = 0; c < D; ++c) acc[c] += sc.w * (sc.w * (z[(size_t)off + c] - u[(size_t)off + c]));
-      } else {  // another rank's slot: the same term, formed there (launch_pack_export mode 0)
-        const double* r = m.remote + (size_t)(-1 - off) * D;
+    for (int c = 0; c < D; ++c) xb[c] = xBar[(size_t)v * D + c];
+    const double inv = m.invdiag[v];
+    for (int t0 = b; t0 < e; t0 += CH) {
+      int off[CH];
 #pragma unroll
-        for (int c = 0; c < D; ++c) acc[c] += r[c];
+      for (int j = 0; j < CH; ++j) off[j] = m.inc_off[min(t0 + j, e - 1)];
+      double zv[CH][D], uv[CH][D];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const bool loc = off[j] >= 0;
+        const double* pz = loc ? z + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
+        const double* pu = loc ? u + off[j] : pz;
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+          zv[j][c] = pz[c];
+          uv[j][c] = pu[c];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        if (t0 + j < e) {
+#pragma unroll
+          for (int c = 0; c < D; ++c)  // another rank's slot: the term formed there (launch_pack_export mode 0)
+            acc[c] += (off[j] >= 0) ? sc.w * (sc.w * (zv[j][c] - uv[j][c])) : zv[j][c];
+        }
       }
     }
-    const double inv = m.invdiag[v];
     double xn[D];
 #pragma unroll
     for (int c = 0; c < D; ++c) {
-      xn[c] = ((sc.tau * xBar[(size_t)v * D + c]) + sc.dtsq * acc[c]) * inv;
+      xn[c] = ((sc.tau * xb[c]) + sc.dtsq * acc[c]) * inv;
       x[(size_t)v * D + c] = xn[c];
     }
     if constexpr (RESID) {
