@@ -257,15 +257,28 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
       xn[c] = ((sc.tau * xb[c]) + sc.dtsq * acc[c]) * inv;
       x[(size_t)v * D + c] = xn[c];
     }
-    if constexpr (RESID) {
+    if constexpr (RESID) {  // same chunking; a slot of another rank is counted by its owner
       double r2 = 0.0;
-      for (int t = b; t < e; ++t) {
-        const int off = m.inc_off[t];
-        if (off < 0) continue;  // counted by the rank that owns the slot
+      for (int t0 = b; t0 < e; t0 += CH) {
+        int off[CH];
 #pragma unroll
-        for (int c = 0; c < D; ++c) {
-          const double d = xn[c] - z[(size_t)off + c];
-          r2 += d * d;
+        for (int j = 0; j < CH; ++j) off[j] = m.inc_off[min(t0 + j, e - 1)];
+        double zv[CH][D];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const double* pz = z + (off[j] >= 0 ? off[j] : 0);
+#pragma unroll
+          for (int c = 0; c < D; ++c) zv[j][c] = pz[c];
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          if (t0 + j < e && off[j] >= 0) {
+#pragma unroll
+            for (int c = 0; c < D; ++c) {
+              const double d = xn[c] - zv[j][c];
+              r2 += d * d;
+            }
+          }
         }
       }
       pv[2] = r2;
