@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-spmv", action="store_true")
     ap.add_argument("--no-be", action="store_true", help="skip the backward-Euler (method 2) section")
+    ap.add_argument("--no-3d", action="store_true", help="skip the 3D (BASELINE config 4) section")
+    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
+                    help="c3: 2D 1M-node disc (the headline); c4: 3D 512k-node cube, anisotropic monitor")
     return ap.parse_args()
 
 
@@ -81,8 +84,8 @@ def spmv_bench(torch, la, mx, with_cpu):
     out = {"matrix": "SquareGrid n=707 backward-Euler Jacobian pattern (src/Mesh.cpp:309-345), values U(-1,1)",
            "rows": n, "nnz": int(len(ja)), "bytes_per_spmv": st["spmv_bytes"], "avg_ms": round(ms, 5),
            "achieved_GBs": round(gbs, 1), "peak_GBs": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
-           "kernel": "k_spmv<0>", "reps": reps}
-    tr, trr = pmc_traffic("k_spmv<0>")
+           "kernel": "k_spmv2<0>", "reps": reps}
+    tr, trr = pmc_traffic("k_spmv2<0>")
     out["traffic"], out["traffic_fetch_uncorrected"] = tr, trr
     # one solve: diagonally dominant values, src/Mesh.cpp parameters
     rows = np.repeat(np.arange(n), np.diff(ia))
@@ -158,6 +161,61 @@ def be_bench(mx, with_cpu):
                                "step_ms_per_1M_nodes": round(cdt * 1e3 * 1001113 / om.nP, 1),
                                "sample": "oracle/oracle.cpp backwards_euler_step (FD Jacobian + LASolver "
                                          "restatement) on SquareGrid n=%d, 3 steady steps after the first" % n}
+    return out
+
+
+def c4_bench(mx, with_cpu, threads, admm_iter):
+    """BASELINE config 4 / SURVEY C4 on one GPU: 3D SquareGrid n = 63 (512,191 nodes, 3,000,564
+    tetrahedra), the anisotropic shell monitor (MonType 6), dt 0.025 tau 0.5 (the 3DMonitor2x0
+    family) and rho 2000 (at the family's rho 50 this monitor inverts elements under the reference
+    algorithm -- the CPU oracle asserts by the third step on n = 16; at rho 500 the n = 63 mesh
+    inverts by the fifth step), 10 ADMM iterations per step, early exit off.  The
+    element-partitioned multi-GPU form of this workload is `bench.py --workload c4` under
+    torch.distributed.run."""
+    mesh = mx.MeshData.rect(3, 63)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(3, 6), rho=2000.0, tau=0.5)
+    E = mx.Engine(M, 0.025)
+    t0 = time.perf_counter()
+    E.step(admm_iter, -1.0)
+    E.sync()
+    first = time.perf_counter() - t0
+    E.step(admm_iter, -1.0)
+    E.set_timing(True)
+    E.reset_stats()
+    E.sync()
+    steps = 3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        E.step(admm_iter, -1.0)
+    E.sync()
+    el = time.perf_counter() - t0
+    st = E.stats()
+    prox_ms = st["t_prox_ms"] / max(st["n_prox"], 1)
+    xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
+    prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
+    out = {"workload": "C4: 3D SquareGrid n=63, %d nodes, %d tetrahedra, anisotropic shell monitor (MonType 6), "
+                       "dt 0.025 tau 0.5 rho 2000, %d ADMM iterations per step" % (mesh.nP, mesh.nF, admm_iter),
+           "value": round(steps * admm_iter / el, 3), "unit": "ADMM it/s", "first_step_ms": round(first * 1e3, 1),
+           "kernels": {"k_prox_wave_ms": round(prox_ms, 4), "k_xupdate_ms": round(xup_ms, 4),
+                       "bfgs_iters_per_prox": round(st["bfgs_iters"] / max(st["admm_iters"], 1) / mesh.nF, 4)},
+           "roofline": {"bound": "hbm", "kernel": "k_prox_wave<3, false>", "achieved": round(prox_gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
+                        "bytes_per_launch": st["prox_bytes"], "avg_launch_ms": round(prox_ms, 4)}}
+    tr, trr = pmc_traffic("k_prox_wave<3, false>")
+    out["roofline"]["traffic"], out["roofline"]["traffic_fetch_uncorrected"] = tr, trr
+    E.close()
+    if with_cpu:  # the oracle (OpenMP prox), same mesh: the FD-Hessian step untimed, then 1 iteration
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_py
+        om = oracle_py.Mesh(3, mesh.Xp, mesh.F, mesh.mask)
+        O = oracle_py.Integrator(om, 6, 0.025, 0.5, 2000.0, nthreads=threads)
+        O.step(1, -1.0)
+        t0 = time.perf_counter()
+        O.step(1, -1.0)
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(1.0 / cdt, 3), "unit": "ADMM it/s", "cores": threads, "kind": "port",
+                               "sample": "C4 mesh, 1 timed step of 1 ADMM iteration after set-up and the FD-Hessian "
+                                         "step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, %d threads)" % threads}
     return out
 
 
@@ -248,11 +306,28 @@ def main():
     import mmadmm_amd as mx
     import lasolver_amd as la
 
-    c3_nodes = 1000519
+    c4 = args.workload == "c4"
+    base_nodes = 512191 if c4 else 1000519
+    dt = 0.025 if c4 else 0.055
     disc_n = args.disc_n if world == 1 else int(round(args.disc_n * world ** 0.5))
-    log(f"rank {rank}/{world}: hexdisc N={disc_n}")
-    mesh = mx.MeshData.hexdisc(disc_n, 0.5, 0.5, 0.5)
-    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5, device=local)
+    cube_n = 63 if world == 1 else int(round(63 * world ** (1.0 / 3.0)))
+
+    used = {}
+
+    def make_mesh(n_ranks):
+        if c4:
+            n = 63 if n_ranks == 1 else cube_n
+            used["n"] = n
+            log(f"rank {rank}/{world}: 3D cube n={n}")
+            m = mx.MeshData.rect(3, n)
+            return m, mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 6), rho=2000.0, tau=0.5, device=local)
+        n = args.disc_n if n_ranks == 1 else disc_n
+        used["n"] = n
+        log(f"rank {rank}/{world}: hexdisc N={n}")
+        m = mx.MeshData.hexdisc(n, 0.5, 0.5, 0.5)
+        return m, mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5, device=local)
+
+    mesh, M = make_mesh(world)
     t_setup = time.perf_counter()
     parallelism = "single"
     comm = None
@@ -261,16 +336,15 @@ def main():
             uid = [mx.Comm.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             comm = mx.Comm.rccl(world, rank, uid[0], local)
-            eng = mx.Engine(M, 0.055, rank=rank, nranks=world, comm=comm)
+            eng = mx.Engine(M, dt, rank=rank, nranks=world, comm=comm)
             parallelism = f"element-partition x{world} (RCCL all-gather of interface slots)"
         except mx.MMADMMError as e:  # report, and measure independent replicas instead
             log(f"partitioned engine unavailable ({e}); running replicas")
-            mesh = mx.MeshData.hexdisc(args.disc_n, 0.5, 0.5, 0.5)
-            M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5, device=local)
-            eng = mx.Engine(M, 0.055)
+            mesh, M = make_mesh(1)
+            eng = mx.Engine(M, dt)
             parallelism = f"replicas x{world} (partitioned engine failed: {e})"
     else:
-        eng = mx.Engine(M, 0.055)
+        eng = mx.Engine(M, dt)
     t_setup = time.perf_counter() - t_setup
     log(f"rank {rank}: setup {t_setup:.1f}s, local nodes {eng.nP}, local simplices {eng.nF}")
 
@@ -309,15 +383,16 @@ def main():
         eng.step(args.admm_iter, 1e-3)
     st_early = eng.stats()
     iters = args.steps * args.admm_iter
-    scale = mesh.nP / c3_nodes if parallelism.startswith("element") else (world if world > 1 else mesh.nP / c3_nodes)
+    scale = mesh.nP / base_nodes if parallelism.startswith("element") else (world if world > 1 else mesh.nP / base_nodes)
     prox_ms = st["t_prox_ms"] / max(st["n_prox"], 1)
     xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
     prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
     xup_gbs = st["xupdate_bytes"] / (xup_ms * 1e-3) / 1e9
-    prox_name = "k_prox_lds<2, %d>" % int(os.environ.get("MMX_PROX_BLOCK", "256"))
+    prox_name = "k_prox_wave<3, false>" if c4 else "k_prox_lds<2, %d>" % int(os.environ.get("MMX_PROX_BLOCK", "256"))
     traffic, traffic_raw = pmc_traffic(prox_name)
     result = {
-        "metric": "ADMM iterations/sec on 1M-node 2D mesh; achieved HBM GB/s in SpMV",
+        "metric": ("ADMM iterations/sec on 512k-node 3D mesh (BASELINE config 4)" if c4 else
+                   "ADMM iterations/sec on 1M-node 2D mesh; achieved HBM GB/s in SpMV"),
         "value": round(iters / elapsed * scale, 3),
         "unit": "ADMM it/s",
         "n_gpus": world,
@@ -329,12 +404,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "C3: 2D circular mesh (hexagonal disc N=%d), %d nodes, %d triangles, MEx1 "
-                               "monitor, dt 0.055 tau 0.5 rho 50, %d ADMM iterations per step"
-                               % (disc_n, mesh.nP, mesh.nF, args.admm_iter),
+        "config": {"workload": ("C4: 3D SquareGrid n=%d, %d nodes, %d tetrahedra, anisotropic shell monitor "
+                                "(MonType 6), dt 0.025 tau 0.5 rho 2000, %d ADMM iterations per step"
+                                % (used["n"], mesh.nP, mesh.nF, args.admm_iter)) if c4 else
+                               ("C3: 2D circular mesh (hexagonal disc N=%d), %d nodes, %d triangles, MEx1 "
+                                "monitor, dt 0.055 tau 0.5 rho 50, %d ADMM iterations per step"
+                                % (used["n"], mesh.nP, mesh.nF, args.admm_iter)),
                    "global_nodes": mesh.nP, "global_simplices": mesh.nF, "nodes_rank0": eng.nP,
                    "simplices_rank0": eng.nF, "admm_iter": args.admm_iter, "parallelism": parallelism,
-                   "value_unit_note": "ADMM it/s x global nodes / 1,000,519"},
+                   "value_unit_note": "ADMM it/s x global nodes / %d" % base_nodes},
         "roofline": {"bound": "hbm", "kernel": prox_name,
                      "achieved": round(prox_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
@@ -359,15 +437,18 @@ def main():
                                          "(profiles/pmc_summary.json); peak: AMD MI355X fp64 vector spec"}
     if rank == 0 and world == 1:
         result["roofline"]["measured_copy_ceiling_GBs"] = stream_copy_ceiling(torch)
-    if not args.no_spmv:
+    if not args.no_spmv and not c4:
         log("spmv microbenchmark")
         result["spmv"] = spmv_bench(torch, la, mx, with_cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
-    if not args.no_be and world == 1:
+    if not args.no_be and world == 1 and not c4:
         log("backward Euler")
         result["backward_euler"] = be_bench(mx, with_cpu=not args.no_cpu_baseline)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
+    if not args.no_3d and world == 1 and not c4:
+        log("3D C4")
+        result["c4_3d"] = c4_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not c4:
         log("cpu baseline")
-        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
         result["cpu_baseline"] = cpu_baseline(mesh, args.admm_iter, threads)
     if rank == 0:
         print(json.dumps(result), flush=True)

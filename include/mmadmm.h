@@ -92,7 +92,10 @@ typedef struct mmadmm_stats {
 const char* mmadmm_last_error(void);
 int mmadmm_version(void);
 
-/* built-in monitors MEx0..MEx5 (dim 2) and MEx0/13D/23D/33D/0/53D (dim 3) by MonType */
+/* built-in monitors MEx0..MEx5 (dim 2) and MEx0/13D/23D/33D/0/53D (dim 3) by MonType 0..5
+ * (main.cpp:836-864), plus MonType 6: an anisotropic shell monitor M = lam2 I + (lam1 - lam2) n n^T (radial n,
+ * lam1 = 1 + sech(50 (|x - c| - 0.3)^2), 1/lam1 across n; MEx2.h's construction around a
+ * sphere) with no reference counterpart (BASELINE config 4) */
 int mmadmm_builtin_monitor(int dim, int mon_type, mmadmm_monitor_fn* fn, void** user);
 
 /* Mesh<D> + MeshIntegrator<D>.  Xp: nP x dim row-major; Xc: reference positions (CompMesh)

@@ -94,6 +94,27 @@ void spiral3Mon(const double* x, double* M) {
   scaledIdentity(3, M, pow(1 + pow(sqrt(g0 * g0 + g1 * g1), 2.0), 1.0 / 4.0));
 }
 
+// MonType 6 (no reference counterpart; BASELINE config 4 "anisotropic monitor"):
+// MEx2's construction (Experiments/TestMonitors/MEx2.h) around a spherical (2D: circular) shell
+// of radius 0.3: eigenvalue lam1 = 1 + sech(50 phi^2) along the radial unit vector n, 1/lam1 across
+// it, phi = |x - c| - 0.3: M = lam2 I + (lam1 - lam2) n n^T.  Restated term for term in
+// oracle/oracle.cpp (anisoShell).
+void anisoShell(int D, const double* x, double* M) {
+  double d[3], r2 = 0.0;
+  for (int i = 0; i < D; ++i) {
+    d[i] = x[i] - 0.5;
+    r2 = (i == 0) ? d[i] * d[i] : r2 + d[i] * d[i];
+  }
+  const double r = sqrt(r2);
+  const double phi = r - 0.3;
+  const double lam1 = 1 + (1.0 / cosh(50 * phi * phi));
+  const double lam2 = 1.0 / lam1;
+  double n[3];
+  for (int i = 0; i < D; ++i) n[i] = (r > 1e-12) ? d[i] / r : (i == 0 ? 1.0 : 0.0);
+  for (int i = 0; i < D; ++i)
+    for (int j = 0; j < D; ++j) M[i * D + j] = ((i == j) ? lam2 : 0.0) + ((lam1 - lam2) * n[i]) * n[j];
+}
+
 }  // namespace
 
 void builtin_monitor_eval(int dim, int monType, const double* x, double* M) {
@@ -104,6 +125,7 @@ void builtin_monitor_eval(int dim, int monType, const double* x, double* M) {
       case 2: aniso(x, M); return;
       case 3: ring(2, x, M); return;
       case 4: step2(2, x, M); return;
+      case 6: anisoShell(2, x, M); return;
       default: spiralMon(2, x, M); return;
     }
   }
@@ -113,6 +135,7 @@ void builtin_monitor_eval(int dim, int monType, const double* x, double* M) {
     case 1: bump(3, x, M); return;
     case 2:
     case 3: ring(3, x, M); return;
+    case 6: anisoShell(3, x, M); return;
     default: spiral3Mon(x, M); return;
   }
 }
@@ -123,8 +146,8 @@ namespace {
 struct BuiltinTag {
   int dim, monType;
 };
-BuiltinTag g_tags[2][6] = {{{2, 0}, {2, 1}, {2, 2}, {2, 3}, {2, 4}, {2, 5}},
-                           {{3, 0}, {3, 1}, {3, 2}, {3, 3}, {3, 4}, {3, 5}}};
+BuiltinTag g_tags[2][7] = {{{2, 0}, {2, 1}, {2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}},
+                           {{3, 0}, {3, 1}, {3, 2}, {3, 3}, {3, 4}, {3, 5}, {3, 6}}};
 void builtin_trampoline(int dim, const double* x, double* M, void* user) {
   const BuiltinTag* t = static_cast<const BuiltinTag*>(user);
   mmx::builtin_monitor_eval(dim, t->monType, x, M);
@@ -133,8 +156,8 @@ void builtin_trampoline(int dim, const double* x, double* M, void* user) {
 
 extern "C" int mmadmm_builtin_monitor(int dim, int mon_type, mmadmm_monitor_fn* fn, void** user) {
   return mmx::guarded([&] {
-    if ((dim != 2 && dim != 3) || mon_type < 0 || mon_type > 5 || !fn || !user)
-      throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_builtin_monitor: dim must be 2|3, mon_type 0..5");
+    if ((dim != 2 && dim != 3) || mon_type < 0 || mon_type > 6 || !fn || !user)
+      throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_builtin_monitor: dim must be 2|3, mon_type 0..6");
     *fn = &builtin_trampoline;
     *user = &g_tags[dim - 2][mon_type];
   });

@@ -245,7 +245,25 @@ static void mex53(int D, const double* x, double* M) {
   monScale(D, M, pow(1 + pow(nrm, 2.0), 1.0 / 4.0));
 }
 
-// Registry by MonType (main.cpp:836-864)
+// MonType 6: the build's anisotropic shell monitor (mm-admm_amd/csrc/host/monitors.cpp
+// anisoShell; no reference counterpart -- BASELINE config 4), restated term for term
+static void anisoShell(int D, const double* x, double* M) {
+  double d[3], r2 = 0.0;
+  for (int i = 0; i < D; ++i) {
+    d[i] = x[i] - 0.5;
+    r2 = (i == 0) ? d[i] * d[i] : r2 + d[i] * d[i];
+  }
+  const double r = sqrt(r2);
+  const double phi = r - 0.3;
+  const double lam1 = 1 + (1.0 / cosh(50 * phi * phi));
+  const double lam2 = 1.0 / lam1;
+  double n[3];
+  for (int i = 0; i < D; ++i) n[i] = (r > 1e-12) ? d[i] / r : (i == 0 ? 1.0 : 0.0);
+  for (int i = 0; i < D; ++i)
+    for (int j = 0; j < D; ++j) M[i * D + j] = ((i == j) ? lam2 : 0.0) + ((lam1 - lam2) * n[i]) * n[j];
+}
+
+// Registry by MonType (main.cpp:836-864; 6 = anisoShell)
 static void monitorAt(int D, int monType, const double* x, double* M) {
   if (D == 2) {
     switch (monType) {
@@ -254,6 +272,7 @@ static void monitorAt(int D, int monType, const double* x, double* M) {
       case 2: mex2(2, x, M); return;
       case 3: mex3(2, x, M); return;
       case 4: mex4(2, x, M); return;
+      case 6: anisoShell(2, x, M); return;
       default: mex5(2, x, M); return;
     }
   }
@@ -261,6 +280,7 @@ static void monitorAt(int D, int monType, const double* x, double* M) {
     case 0: case 4: monIdentity(3, M); return;
     case 1: mex1(3, x, M); return;
     case 2: case 3: mex3(3, x, M); return;
+    case 6: anisoShell(3, x, M); return;
     default: mex53(3, x, M); return;
   }
 }

@@ -34,6 +34,7 @@ def cases():
         "rect16_mex2": (lambda: oracle_py.Mesh.rect(2, 16), 2, 0.025, 0.5, 100.0, False),
         "hexdisc12_mex1": (lambda: _hexdisc(12), 1, 0.055, 0.5, 50.0, False),
         "rect3d_3_mex1": (lambda: oracle_py.Mesh.rect(3, 3), 1, 0.025, 0.5, 50.0, False),
+        "rect3d_4_aniso6": (lambda: oracle_py.Mesh.rect(3, 4), 6, 0.025, 0.5, 50.0, False),
         "circle3d6_compmesh": (lambda: circle_mesh("3DCircleEx6"), 5, 0.1, 0.1, 0.5, True),
     }
 
