@@ -87,12 +87,26 @@ typedef struct mmadmm_stats {
   double t_jac_ms;        /* backward Euler: wall time in Jacobian builds (FD + assembly) */
   double t_solve_ms;      /* backward Euler: wall time in the linear solves (ILU(0) + CG-STAB) */
   double t_be_ms;         /* backward Euler: wall time of whole steps */
+  long long regrids;      /* monitor-grid rebuilds on the device (mmadmm_regrid / set_regrid) */
 } mmadmm_stats;
+
+/* Time-varying monitors (the reference's Mesh<D>::setUp hook, commented out at
+ * src/Mesh.cpp:1006-1014, would re-run MeshInterpolator::updateMesh + interpolateMonitor,
+ * src/MeshInterpolator.cpp:68-130, 166-259, 366-404, at every step start).
+ * mmadmm_regrid rebuilds the smoothed monitor grid on the device from the current mesh positions,
+ * the monitor evaluated at time t (built-in MonType 7 on the device; any other monitor through its
+ * host callback at the current vertices); bit-identical to the host set-up.  mmadmm_set_regrid(h, 1)
+ * does that at the start of every mmadmm_step with t = steps taken * dt.  Single-rank engines only
+ * (MMADMM_ERR_INVALID on a partition: the grid needs every vertex). */
+int mmadmm_regrid(mmadmm_handle h, double t);
+int mmadmm_set_regrid(mmadmm_handle h, int every_step);
 
 const char* mmadmm_last_error(void);
 int mmadmm_version(void);
 
-/* built-in monitors MEx0..MEx5 (dim 2) and MEx0/13D/23D/33D/0/53D (dim 3) by MonType 0..5
+/* built-in monitors MEx0..MEx5 (dim 2) and MEx0/13D/23D/33D/0/53D (dim 3) by MonType 0..5, MonType 7 a
+ * time-varying bump M = (1 + 5 / (1 + 50 |x - c(t)|^2)) I, c(t) = (0.5 + 0.2 cos 2 pi t, 0.5 + 0.2 sin 2 pi t,
+ * 0.5) (used with mmadmm_set_regrid; set-up evaluates it at t = 0)
  * (main.cpp:836-864), plus MonType 6: an anisotropic shell monitor M = lam2 I + (lam1 - lam2) n n^T (radial n,
  * lam1 = 1 + sech(50 (|x - c| - 0.3)^2), 1/lam1 across n; MEx2.h's construction around a
  * sphere) with no reference counterpart (BASELINE config 4) */

@@ -87,6 +87,13 @@ struct HostGrid {
 };
 void build_monitor_grid(int dim, const double* X, int nP, mmadmm_monitor_fn fn, void* user,
                         HostGrid& g);
+// grid size and linspace coordinates from the vertex count and bounding box (updateMesh,
+// src/MeshInterpolator.cpp:68-130); vals is not touched
+void grid_geometry(int dim, int nP, const double* lo, const double* hi, HostGrid& g);
+// built-in monitor behind (fn, user) (MonType), or -1 for a user callback
+int builtin_monitor_kind(mmadmm_monitor_fn fn, void* user);
+// MonType 7's centre at time t
+void moving_bump_centre(double t, double c[3]);
 
 struct Comm;
 Comm* comm_of(mmadmm_comm c);

@@ -15,6 +15,7 @@
 
 #include "../../../include/mmx_sparse.h"
 #include "../kernels/admm_kernels.h"
+#include "../kernels/regrid_kernels.h"
 #include "comm.h"
 #include "common.h"
 #include "partition.h"
@@ -50,6 +51,8 @@ struct EngineBase {
   virtual void stats(mmadmm_stats* s) = 0;
   virtual void resetStats() = 0;
   virtual void sync() = 0;
+  virtual void regrid(double t) = 0;
+  virtual void setRegrid(bool on) = 0;
   virtual void debugBlockGrad(int s, const double* z, const double* dx, int flags, double* out) = 0;
 };
 
@@ -84,6 +87,8 @@ class Engine final : public EngineBase {
     }
     // monitor grid (MeshInterpolator set-up), once per run on the initial vertices
     build_monitor_grid(D, Vp.data(), nP, fn, user, grid_);
+    monFn_ = fn;
+    monUser_ = user;
     // functional constants (src/AdaptationFunctional.cpp:176-220, src/Mesh.cpp:451)
     const double w = 0.5 * sqrt(p.rho);
     w_ = w;
@@ -194,6 +199,7 @@ class Engine final : public EngineBase {
   }
 
   ~Engine() override {
+    if (rgHost_) (void)hipHostFree(rgHost_);
     if (jac_) (void)mmx_matrix_destroy(jac_);
     for (auto& e : evPool_) (void)hipEventDestroy(e);
     if (st_) (void)hipStreamDestroy(st_);
@@ -202,6 +208,8 @@ class Engine final : public EngineBase {
   // MeshIntegrator<D>::step (src/MeshIntegrator.cpp:101-191)
   void step(int nIters, double tol, double* Ih, int* itersOut) override {
     if (nIters < 1) throw Error(MMADMM_ERR_INVALID, "step: nIters must be >= 1");
+    // Mesh<D>::setUp (src/Mesh.cpp:1006-1014, commented in the reference): time-varying monitors
+    if (regridEachStep_) regrid(stepsTaken_ * prm_.dt);
     ensureResults(nIters);
     const bool timing = timing_;
     hipEvent_t eStep0 = nullptr, eStep1 = nullptr;
@@ -425,7 +433,12 @@ class Engine final : public EngineBase {
     else if (what == "hess") b = &B_;
     else if (what == "gs") b = &gs_;
     else if (what == "grid") {
-      std::memcpy(out, grid_.vals.data(), grid_.vals.size() * sizeof(double));
+      if (gridOnDevice_) {
+        MMX_HIP(hipMemcpyAsync(out, gvals_.p, gvals_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
+        MMX_HIP(hipStreamSynchronize(st_));
+      } else {
+        std::memcpy(out, grid_.vals.data(), grid_.vals.size() * sizeof(double));
+      }
       return;
     } else if (what == "Ehat") {
       std::memcpy(out, EhatH_, D * D * sizeof(double));
@@ -599,6 +612,99 @@ class Engine final : public EngineBase {
     }
   }
 
+  // The monitor grid rebuilt on the device from the current vertices Vp: bounding
+  // box, monitor at the vertices (MonType 7 on the device at time t; any other monitor through its
+  // host callback), nearest vertex of every grid point, smoothing -- bit-identical to the host
+  // set-up (regrid_kernels.hip).  One 2D-double readback (the bounding box) per call.
+  void setRegrid(bool on) override {
+    if (on && nranks_ > 1)
+      throw Error(MMADMM_ERR_INVALID, "regrid: the monitor grid needs every vertex; not available on a partition");
+    regridEachStep_ = on;
+  }
+
+  void regrid(double t) override {
+    if (nranks_ > 1)
+      throw Error(MMADMM_ERR_INVALID, "regrid: the monitor grid needs every vertex; not available on a partition");
+    constexpr int DD = D * D;
+    const int nb = std::max(1, std::min(256, (nP_ + 255) / 256));
+    if (!rgPart_.p) {
+      rgPart_.alloc((size_t)256 * 2 * D);
+      rgMon_.alloc((size_t)nP_ * DD);
+      rgCellOf_.alloc(nP_);
+      rgNodes_.alloc(nP_);
+      rgTmp_.alloc(gvals_.n);
+      MMX_HIP(hipHostMalloc((void**)&rgHost_, sizeof(double) * 256 * 2 * D, hipHostMallocDefault));
+    }
+    launch_bbox<D>(Vp_.p, nP_, rgPart_.p, nb, st_);
+    MMX_HIP(hipMemcpyAsync(rgHost_, rgPart_.p, sizeof(double) * nb * 2 * D, hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int b = 0; b < nb; ++b)
+      for (int d = 0; d < D; ++d) {
+        lo[d] = std::min(lo[d], rgHost_[(size_t)b * 2 * D + d]);
+        hi[d] = std::max(hi[d], rgHost_[(size_t)b * 2 * D + D + d]);
+      }
+    grid_geometry(D, nP_, lo, hi, grid_);
+    gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
+    gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
+    if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
+    // vertex cells: about two vertices per cell
+    CellGrid cg{};
+    const int gn[3] = {grid_.nx, grid_.ny, grid_.nz};
+    cg.hmin = INFINITY;
+    for (int d = 0; d < 3; ++d) {
+      const double ext = d < D ? hi[d] - lo[d] : 0.0;
+      cg.lo[d] = d < D ? lo[d] : 0.0;
+      cg.n[d] = (d < D && ext > 0) ? std::max(1, gn[d] / 2) : 1;
+      cg.inv[d] = (d < D && ext > 0) ? cg.n[d] / ext : 0.0;
+      if (d < D && ext > 0) cg.hmin = std::min(cg.hmin, ext / cg.n[d]);
+    }
+    if (!(cg.hmin < INFINITY)) cg.hmin = 0.0;
+    const int ncell = cg.n[0] * cg.n[1] * cg.n[2];
+    if ((int)rgStarts_.n < ncell + 1) {
+      rgCounts_.alloc(ncell + 1);
+      rgStarts_.alloc(ncell + 1);
+      rgFill_.alloc(ncell);
+      rgScanBytes_ = bin_scan_bytes(ncell);
+      rgScan_.alloc(std::max<size_t>(rgScanBytes_, 1));
+    }
+    launch_bin<D>(Vp_.p, nP_, cg, rgCellOf_.p, rgCounts_.p, rgStarts_.p, rgFill_.p, rgNodes_.p, rgScan_.p,
+                  rgScanBytes_, st_);
+    // the monitor at the vertices (MonitorFunction::evaluateAtVertices, src/MonitorFunction.cpp:16-32)
+    if (builtin_monitor_kind(monFn_, monUser_) == 7) {
+      double c[3];
+      moving_bump_centre(t, c);
+      launch_monitor_tv<D>(Vp_.p, nP_, c, rgMon_.p, st_);
+    } else {  // a host plugin: evaluated on the host at the current vertices, as the reference does
+      std::vector<double> X((size_t)nP_ * D), mv((size_t)nP_ * DD);
+      MMX_HIP(hipMemcpyAsync(X.data(), Vp_.p, X.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+      for (int v = 0; v < nP_; ++v) {
+        double M[9];
+        for (int i = 0; i < DD; ++i) M[i] = 0.0;
+        monFn_(D, &X[(size_t)v * D], M, monUser_);
+        std::memcpy(&mv[(size_t)v * DD], M, DD * sizeof(double));
+      }
+      MMX_HIP(hipMemcpyAsync(rgMon_.p, mv.data(), mv.size() * sizeof(double), hipMemcpyHostToDevice, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+    }
+    launch_nn_fill<D>(Vp_.p, cg, rgStarts_.p, rgNodes_.p, gx_.p, gy_.p, D == 3 ? gz_.p : gy_.p, grid_.nx, grid_.ny,
+                      grid_.nz, rgMon_.p, rgTmp_.p, st_);
+    const int passes = (D == 2) ? 5 : 2;  // smoothMonitorGrid
+    double* cur = rgTmp_.p;
+    double* oth = gvals_.p;
+    for (int it = 0; it < passes; ++it) {
+      launch_smooth<D>(cur, oth, grid_.nx, grid_.ny, grid_.nz, st_);
+      std::swap(cur, oth);
+    }
+    if (cur != gvals_.p)
+      MMX_HIP(hipMemcpyAsync(gvals_.p, cur, gvals_.n * sizeof(double), hipMemcpyDeviceToDevice, st_));
+    MMX_HIP(hipGetLastError());
+    gridOnDevice_ = true;
+    m_ = makeView();
+    st_stats_.regrids += 1;
+  }
+
   DeviceMesh<D> makeView() const {
     DeviceMesh<D> m{};
     m.nP = nP_;
@@ -674,6 +780,15 @@ class Engine final : public EngineBase {
   double EhatH_[9] = {0};
   std::vector<int32_t> Fh_, maskH_;
   HostGrid grid_;
+  // time-varying monitors: the monitor plugin, per-step regrid flag and the device set-up buffers
+  mmadmm_monitor_fn monFn_ = nullptr;
+  void* monUser_ = nullptr;
+  bool regridEachStep_ = false, gridOnDevice_ = false;
+  DevBuf<double> rgPart_, rgMon_, rgTmp_;
+  DevBuf<int> rgCellOf_, rgNodes_, rgCounts_, rgStarts_, rgFill_;
+  DevBuf<unsigned char> rgScan_;
+  size_t rgScanBytes_ = 0;
+  double* rgHost_ = nullptr;
   hipStream_t st_ = nullptr;
   DevBuf<int32_t> F_, incPtr_, incOff_;
   DevBuf<uint8_t> sbits_, interior_;
@@ -838,6 +953,12 @@ int mmadmm_stats_get(mmadmm_handle h, mmadmm_stats* s) {
 }
 int mmadmm_stats_reset(mmadmm_handle h) {
   return guarded([&] { eng(h).resetStats(); });
+}
+int mmadmm_regrid(mmadmm_handle h, double t) {
+  return guarded([&] { eng(h).regrid(t); });
+}
+int mmadmm_set_regrid(mmadmm_handle h, int every_step) {
+  return guarded([&] { eng(h).setRegrid(every_step != 0); });
 }
 int mmadmm_sync(mmadmm_handle h) {
   return guarded([&] { eng(h).sync(); });

@@ -108,10 +108,6 @@ class KdNN {
 template <int D>
 void buildGrid(const double* X, int nP, mmadmm_monitor_fn fn, void* user, HostGrid& g) {
   constexpr int DD = D * D;
-  const int sz = (int)std::pow((double)((long)nP * D), 1.0 / D);  // src/MeshInterpolator.cpp:78-84
-  g.nx = sz;
-  g.ny = sz;
-  g.nz = (D == 2) ? 1 : sz;
   double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (int i = 0; i < nP; i++)
     for (int d = 0; d < D; ++d) {
@@ -119,13 +115,7 @@ void buildGrid(const double* X, int nP, mmadmm_monitor_fn fn, void* user, HostGr
       mn[d] = (v < mn[d]) ? v : mn[d];
       mx[d] = (v > mx[d]) ? v : mx[d];
     }
-  for (int d = 0; d < D; ++d) {
-    g.lo[d] = mn[d];
-    g.hi[d] = mx[d];
-  }
-  linspace(mn[0], mx[0], g.nx, g.gx);
-  linspace(mn[1], mx[1], g.ny, g.gy);
-  if (D == 3) linspace(mn[2], mx[2], g.nz, g.gz);
+  grid_geometry(D, nP, mn, mx, g);
   const size_t rows = (size_t)(g.nx + 1) * (g.ny + 1) * (g.nz + 1);
   g.vals.assign(rows * DD, 0.0);
   // MonitorFunction<D>::evaluateAtVertices (src/MonitorFunction.cpp:16-32)
@@ -197,6 +187,20 @@ void buildGrid(const double* X, int nP, mmadmm_monitor_fn fn, void* user, HostGr
 }
 
 }  // namespace
+
+void grid_geometry(int dim, int nP, const double* lo, const double* hi, HostGrid& g) {
+  const int sz = (int)std::pow((double)((long)nP * dim), 1.0 / dim);  // src/MeshInterpolator.cpp:78-84
+  g.nx = sz;
+  g.ny = sz;
+  g.nz = (dim == 2) ? 1 : sz;
+  for (int d = 0; d < 3; ++d) {
+    g.lo[d] = d < dim ? lo[d] : 0.0;
+    g.hi[d] = d < dim ? hi[d] : 0.0;
+  }
+  linspace(lo[0], hi[0], g.nx, g.gx);
+  linspace(lo[1], hi[1], g.ny, g.gy);
+  if (dim == 3) linspace(lo[2], hi[2], g.nz, g.gz);
+}
 
 void build_monitor_grid(int dim, const double* X, int nP, mmadmm_monitor_fn fn, void* user, HostGrid& g) {
   if (dim == 2)

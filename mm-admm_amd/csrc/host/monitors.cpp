@@ -117,7 +117,34 @@ void anisoShell(int D, const double* x, double* M) {
 
 }  // namespace
 
+// MonType 7 (no reference counterpart; BASELINE config 5 "time-varying monitor"):
+// a bump moving on a circle, M = (1 + 5 / (1 + 50 |x - c(t)|^2)) I with
+// c(t) = (0.5 + 0.2 cos 2 pi t, 0.5 + 0.2 sin 2 pi t, 0.5).  Set-up evaluates it at t = 0; with
+// mmadmm_set_regrid the engine re-evaluates it on the device at every step start
+// (regrid_kernels.hip k_monitor_tv, from this centre).  Restated in oracle/oracle.cpp (movingBump).
+void moving_bump_centre(double t, double c[3]) {
+  const double PI = 3.141592653589793238462643383;
+  c[0] = 0.5 + 0.2 * cos((2.0 * PI) * t);
+  c[1] = 0.5 + 0.2 * sin((2.0 * PI) * t);
+  c[2] = 0.5;
+}
+static void movingBump(int D, const double* x, double t, double* M) {
+  double c[3];
+  moving_bump_centre(t, c);
+  double sq = 0.0;
+  for (int d = 0; d < D; ++d) {
+    const double u = x[d] - c[d];
+    sq = (d == 0) ? u * u : sq + u * u;
+  }
+  const double sc = 1 + 5.0 / (1 + 50.0 * sq);
+  for (int i = 0; i < D * D; ++i) M[i] = (i / D == i % D) ? sc : 0.0;
+}
+
 void builtin_monitor_eval(int dim, int monType, const double* x, double* M) {
+  if (monType == 7) {
+    movingBump(dim, x, 0.0, M);
+    return;
+  }
   if (dim == 2) {
     switch (monType) {
       case 0: identity(2, M); return;
@@ -146,8 +173,8 @@ namespace {
 struct BuiltinTag {
   int dim, monType;
 };
-BuiltinTag g_tags[2][7] = {{{2, 0}, {2, 1}, {2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}},
-                           {{3, 0}, {3, 1}, {3, 2}, {3, 3}, {3, 4}, {3, 5}, {3, 6}}};
+BuiltinTag g_tags[2][8] = {{{2, 0}, {2, 1}, {2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}, {2, 7}},
+                           {{3, 0}, {3, 1}, {3, 2}, {3, 3}, {3, 4}, {3, 5}, {3, 6}, {3, 7}}};
 void builtin_trampoline(int dim, const double* x, double* M, void* user) {
   const BuiltinTag* t = static_cast<const BuiltinTag*>(user);
   mmx::builtin_monitor_eval(dim, t->monType, x, M);
@@ -156,9 +183,20 @@ void builtin_trampoline(int dim, const double* x, double* M, void* user) {
 
 extern "C" int mmadmm_builtin_monitor(int dim, int mon_type, mmadmm_monitor_fn* fn, void** user) {
   return mmx::guarded([&] {
-    if ((dim != 2 && dim != 3) || mon_type < 0 || mon_type > 6 || !fn || !user)
-      throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_builtin_monitor: dim must be 2|3, mon_type 0..6");
+    if ((dim != 2 && dim != 3) || mon_type < 0 || mon_type > 7 || !fn || !user)
+      throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_builtin_monitor: dim must be 2|3, mon_type 0..7");
     *fn = &builtin_trampoline;
     *user = &g_tags[dim - 2][mon_type];
   });
 }
+
+namespace mmx {
+// the built-in monitor behind (fn, user), or -1 for a user callback
+int builtin_monitor_kind(mmadmm_monitor_fn fn, void* user) {
+  if (fn != &builtin_trampoline) return -1;
+  for (int d = 0; d < 2; ++d)
+    for (int k = 0; k < 8; ++k)
+      if (user == &g_tags[d][k]) return k;
+  return -1;
+}
+}  // namespace mmx

@@ -1,0 +1,38 @@
+// regrid_kernels.h -- launch interface of the device monitor-grid set-up (regrid_kernels.hip),
+// the time-varying-monitor path (DESIGN.md §Time-varying monitors).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace mmx {
+
+// uniform cell grid over the vertices' bounding box (the nearest-vertex search structure)
+struct CellGrid {
+  double lo[3];
+  double inv[3];  // cells per unit length (0 for a degenerate axis)
+  int n[3];       // cells per axis (n[2] = 1 in 2D)
+  double hmin;    // smallest cell edge
+};
+
+// per-block partial bounding boxes: partials[b * 2D + d] = min_d, [b * 2D + D + d] = max_d
+template <int D>
+void launch_bbox(const double* X, int n, double* partials, int nblocks, hipStream_t st);
+// counting sort of the vertices into cells: starts[ncell + 1] (exclusive scan of counts),
+// cellNodes[n]; counts must hold ncell + 1 ints, fill ncell
+template <int D>
+void launch_bin(const double* X, int n, const CellGrid& cg, int* cellOfV, int* counts, int* starts, int* fill,
+                int* cellNodes, void* scanTmp, size_t scanTmpBytes, hipStream_t st);
+size_t bin_scan_bytes(int ncell);
+// MonType 7 at the vertices, centre c[3] of the moving bump at the current time
+template <int D>
+void launch_monitor_tv(const double* X, int n, const double* c, double* monVals, hipStream_t st);
+// nearest vertex of every grid point -> grid rows (host layout, 3D x/y swap included)
+template <int D>
+void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, const int* cellNodes, const double* gx,
+                    const double* gy, const double* gz, int nx, int ny, int nz, const double* monVals, double* vals,
+                    hipStream_t st);
+// one Jacobi smoothing pass in -> out
+template <int D>
+void launch_smooth(const double* in, double* out, int nx, int ny, int nz, hipStream_t st);
+
+}  // namespace mmx

@@ -1,0 +1,264 @@
+// regrid_kernels.hip -- the monitor-grid set-up on the device, for time-varying monitors
+// (SURVEY §8f-2): the reference's commented Mesh<D>::setUp hook (src/Mesh.cpp:1006-1014) would
+// re-run MeshInterpolator::updateMesh + interpolateMonitor (src/MeshInterpolator.cpp:68-130,
+// 166-259, 366-404) at the start of every step.  Here that is: bounding box of the current
+// vertices, monitor at the vertices, nearest vertex of every grid point, Jacobi smoothing --
+// all on the device, bit-identical to the host set-up (csrc/host/monitor_grid.cpp):
+//   * the nearest vertex is exact: vertices are binned into a uniform cell grid, a grid point
+//     searches Chebyshev rings of cells until no unvisited cell can hold a vertex as near as the
+//     best one, with the host's squared-distance sums and lowest-id tie rule;
+//   * min/max and the smoothing stencil are order-independent / written in the host's order.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "regrid_kernels.h"
+
+namespace mmx {
+namespace {
+
+constexpr int kRB = 256;
+
+template <int D>
+__global__ void __launch_bounds__(kRB) k_bbox(const double* __restrict__ X, int n, double* __restrict__ part) {
+  __shared__ double sm[2 * D][kRB];
+  double lo[D], hi[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    lo[d] = INFINITY;
+    hi[d] = -INFINITY;
+  }
+  for (int v = blockIdx.x * kRB + threadIdx.x; v < n; v += gridDim.x * kRB)
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const double x = X[(size_t)v * D + d];
+      lo[d] = x < lo[d] ? x : lo[d];
+      hi[d] = x > hi[d] ? x : hi[d];
+    }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    sm[d][threadIdx.x] = lo[d];
+    sm[D + d][threadIdx.x] = hi[d];
+  }
+  __syncthreads();
+  for (int w = kRB / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const double a = sm[d][threadIdx.x + w], b = sm[D + d][threadIdx.x + w];
+        sm[d][threadIdx.x] = a < sm[d][threadIdx.x] ? a : sm[d][threadIdx.x];
+        sm[D + d][threadIdx.x] = b > sm[D + d][threadIdx.x] ? b : sm[D + d][threadIdx.x];
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < 2 * D) part[(size_t)blockIdx.x * 2 * D + threadIdx.x] = sm[threadIdx.x][0];
+}
+
+template <int D>
+__device__ __forceinline__ int cellOf(const double* x, const CellGrid& cg, int (&c)[3]) {
+  int id = 0;
+#pragma unroll
+  for (int d = D - 1; d >= 0; --d) {
+    int k = (int)((x[d] - cg.lo[d]) * cg.inv[d]);
+    k = k < 0 ? 0 : (k >= cg.n[d] ? cg.n[d] - 1 : k);
+    c[d] = k;
+    id = id * cg.n[d] + k;
+  }
+  return id;  // x fastest
+}
+
+template <int D>
+__global__ void __launch_bounds__(kRB) k_bin_count(const double* __restrict__ X, int n, CellGrid cg,
+                                                   int* __restrict__ cellOfV, int* __restrict__ counts) {
+  const int v = blockIdx.x * kRB + threadIdx.x;
+  if (v >= n) return;
+  double x[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) x[d] = X[(size_t)v * D + d];
+  int c[3];
+  const int id = cellOf<D>(x, cg, c);
+  cellOfV[v] = id;
+  atomicAdd(&counts[id], 1);
+}
+
+__global__ void __launch_bounds__(kRB) k_bin_fill(int n, const int* __restrict__ cellOfV,
+                                                  const int* __restrict__ starts, int* __restrict__ fill,
+                                                  int* __restrict__ cellNodes) {
+  const int v = blockIdx.x * kRB + threadIdx.x;
+  if (v >= n) return;
+  const int c = cellOfV[v];
+  cellNodes[starts[c] + atomicAdd(&fill[c], 1)] = v;
+}
+
+// MonType 7 (time-varying moving bump): M = (1 + 5 / (1 + 50 |x - c(t)|^2)) I, c(t) from the host
+template <int D>
+__global__ void __launch_bounds__(kRB) k_monitor_tv(const double* __restrict__ X, int n, double c0, double c1,
+                                                    double c2, double* __restrict__ monVals) {
+  const int v = blockIdx.x * kRB + threadIdx.x;
+  if (v >= n) return;
+  const double c[3] = {c0, c1, c2};
+  double sq = 0.0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const double t = X[(size_t)v * D + d] - c[d];
+    sq = (d == 0) ? t * t : sq + t * t;
+  }
+  const double s = 1 + 5.0 / (1 + 50.0 * sq);
+#pragma unroll
+  for (int i = 0; i < D * D; ++i) monVals[(size_t)v * D * D + i] = (i / D == i % D) ? s : 0.0;
+}
+
+// nearest vertex of every grid point; the grid row takes that vertex's monitor value
+template <int D>
+__global__ void __launch_bounds__(kRB) k_nn_fill(const double* __restrict__ X, CellGrid cg,
+                                                 const int* __restrict__ starts, const int* __restrict__ cellNodes,
+                                                 const double* __restrict__ gx, const double* __restrict__ gy,
+                                                 const double* __restrict__ gz, int nx, int ny, int nz,
+                                                 const double* __restrict__ monVals, double* __restrict__ vals) {
+  constexpr int DD = D * D;
+  const long long p = (long long)blockIdx.x * kRB + threadIdx.x;
+  const long long npts = (long long)(nx + 1) * (ny + 1) * (D == 3 ? nz + 1 : 1);
+  if (p >= npts) return;
+  // p enumerates (i fastest, then j, then k); rows follow the host set-up's layout
+  const int i = (int)(p % (nx + 1));
+  const int j = (int)((p / (nx + 1)) % (ny + 1));
+  const int k = (D == 3) ? (int)(p / ((long long)(nx + 1) * (ny + 1))) : 0;
+  double q[3] = {gx[i], gy[j], D == 3 ? gz[k] : 0.0};
+  size_t row;
+  if constexpr (D == 2)
+    row = (size_t)j * (nx + 1) + i;
+  else  // src/MeshInterpolator.cpp:234: (nx+1)(ny+1)k + i(nx+1) + j (x and y swapped)
+    row = (size_t)(nx + 1) * (ny + 1) * k + (size_t)i * (nx + 1) + j;
+  int c[3] = {0, 0, 0};
+  cellOf<D>(q, cg, c);
+  double best = INFINITY;
+  int bi = -1;
+  int rmax = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) rmax = max(rmax, max(c[d], cg.n[d] - 1 - c[d]));
+  for (int r = 0; r <= rmax; ++r) {
+    const int z0 = (D == 3) ? max(c[2] - r, 0) : 0, z1 = (D == 3) ? min(c[2] + r, cg.n[2] - 1) : 0;
+    const int y0 = max(c[1] - r, 0), y1 = min(c[1] + r, cg.n[1] - 1);
+    const int x0 = max(c[0] - r, 0), x1 = min(c[0] + r, cg.n[0] - 1);
+    for (int cz = z0; cz <= z1; ++cz)
+      for (int cy = y0; cy <= y1; ++cy)
+        for (int cx = x0; cx <= x1; ++cx) {
+          const int dz = (D == 3) ? abs(cz - c[2]) : 0;
+          if (max(max(abs(cx - c[0]), abs(cy - c[1])), dz) != r) continue;  // ring r only
+          const int cell = (cz * cg.n[1] + cy) * cg.n[0] + cx;
+          for (int t = starts[cell]; t < starts[cell + 1]; ++t) {
+            const int v = cellNodes[t];
+            double dd = 0.0;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+              const double df = q[d] - X[(size_t)v * D + d];
+              dd += df * df;
+            }
+            if (dd < best || (dd == best && v < bi)) {
+              best = dd;
+              bi = v;
+            }
+          }
+        }
+    // every unvisited vertex lies >= r cells away along some axis: at distance >= r * h_min
+    // (less a margin for the binning's rounding); stop once the best is strictly nearer
+    const double lb = ((double)r - 1e-6) * cg.hmin;
+    if (bi >= 0 && r > 0 && best < lb * lb) break;
+  }
+#pragma unroll
+  for (int e = 0; e < DD; ++e) vals[row * DD + e] = monVals[(size_t)bi * DD + e];
+}
+
+// smoothMonitorGrid (src/MeshInterpolator.cpp:366-404): one Jacobi pass, interior points
+template <int D>
+__global__ void __launch_bounds__(kRB) k_smooth(const double* __restrict__ in, double* __restrict__ out, int nx,
+                                                int ny, int nz) {
+  constexpr int DD = D * D;
+  const long long c = (long long)blockIdx.x * kRB + threadIdx.x;
+  const long long P = (long long)(nx + 1) * (ny + 1);
+  const long long rows = P * (D == 3 ? nz + 1 : 1);
+  if (c >= rows) return;
+  const int i = (int)(c % (nx + 1));
+  const int j = (int)((c / (nx + 1)) % (ny + 1));
+  const int k = (D == 3) ? (int)(c / P) : 0;
+  const bool interior = i >= 1 && i < nx && j >= 1 && j < ny && (D == 2 || (k >= 1 && k < nz));
+  for (int q = 0; q < DD; ++q) {
+    double v;
+    if (!interior) {
+      v = in[c * DD + q];
+    } else if constexpr (D == 2) {
+      v = 0.6 * in[c * DD + q];
+      v += 0.1 * in[(c + 1) * DD + q];
+      v += 0.1 * in[(c - 1) * DD + q];
+      v += 0.1 * in[(c + nx + 1) * DD + q];
+      v += 0.1 * in[(c - nx - 1) * DD + q];
+    } else {
+      const double h = 0.4 / 6.0;
+      v = 0.6 * in[c * DD + q] + h * in[(c + 1) * DD + q] + h * in[(c - 1) * DD + q] + h * in[(c + nx + 1) * DD + q] +
+          h * in[(c - nx - 1) * DD + q] + h * in[(c + P) * DD + q] + h * in[(c - P) * DD + q];
+    }
+    out[c * DD + q] = v;
+  }
+}
+
+inline unsigned blocks(long long n) { return (unsigned)((n + kRB - 1) / kRB); }
+
+}  // namespace
+
+template <int D>
+void launch_bbox(const double* X, int n, double* partials, int nblocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_bbox<D>, dim3(nblocks), dim3(kRB), 0, st, X, n, partials);
+}
+
+template <int D>
+void launch_bin(const double* X, int n, const CellGrid& cg, int* cellOfV, int* counts, int* starts, int* fill,
+                int* cellNodes, void* scanTmp, size_t scanTmpBytes, hipStream_t st) {
+  const int ncell = cg.n[0] * cg.n[1] * cg.n[2];
+  (void)hipMemsetAsync(counts, 0, sizeof(int) * (ncell + 1), st);
+  (void)hipMemsetAsync(fill, 0, sizeof(int) * ncell, st);
+  hipLaunchKernelGGL(k_bin_count<D>, dim3(blocks(n)), dim3(kRB), 0, st, X, n, cg, cellOfV, counts);
+  size_t bytes = scanTmpBytes;
+  (void)hipcub::DeviceScan::ExclusiveSum(scanTmp, bytes, counts, starts, ncell + 1, st);
+  hipLaunchKernelGGL(k_bin_fill, dim3(blocks(n)), dim3(kRB), 0, st, n, cellOfV, starts, fill, cellNodes);
+}
+
+size_t bin_scan_bytes(int ncell) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (int*)nullptr, (int*)nullptr, ncell + 1, (hipStream_t)0);
+  return bytes;
+}
+
+template <int D>
+void launch_monitor_tv(const double* X, int n, const double* c, double* monVals, hipStream_t st) {
+  hipLaunchKernelGGL(k_monitor_tv<D>, dim3(blocks(n)), dim3(kRB), 0, st, X, n, c[0], c[1], c[2], monVals);
+}
+
+template <int D>
+void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, const int* cellNodes, const double* gx,
+                    const double* gy, const double* gz, int nx, int ny, int nz, const double* monVals, double* vals,
+                    hipStream_t st) {
+  const long long npts = (long long)(nx + 1) * (ny + 1) * (D == 3 ? nz + 1 : 1);
+  hipLaunchKernelGGL(k_nn_fill<D>, dim3(blocks(npts)), dim3(kRB), 0, st, X, cg, starts, cellNodes, gx, gy, gz, nx, ny,
+                     nz, monVals, vals);
+}
+
+template <int D>
+void launch_smooth(const double* in, double* out, int nx, int ny, int nz, hipStream_t st) {
+  const long long rows = (long long)(nx + 1) * (ny + 1) * (D == 3 ? nz + 1 : 1);
+  hipLaunchKernelGGL(k_smooth<D>, dim3(blocks(rows)), dim3(kRB), 0, st, in, out, nx, ny, nz);
+}
+
+#define MMX_REGRID_INST(D)                                                                                       \
+  template void launch_bbox<D>(const double*, int, double*, int, hipStream_t);                                 \
+  template void launch_bin<D>(const double*, int, const CellGrid&, int*, int*, int*, int*, int*, void*, size_t, \
+                              hipStream_t);                                                                    \
+  template void launch_monitor_tv<D>(const double*, int, const double*, double*, hipStream_t);                  \
+  template void launch_nn_fill<D>(const double*, const CellGrid&, const int*, const int*, const double*,        \
+                                  const double*, const double*, int, int, int, const double*, double*,          \
+                                  hipStream_t);                                                                \
+  template void launch_smooth<D>(const double*, double*, int, int, int, hipStream_t);
+MMX_REGRID_INST(2)
+MMX_REGRID_INST(3)
+#undef MMX_REGRID_INST
+
+}  // namespace mmx

@@ -42,7 +42,7 @@ class mmadmm_stats(ctypes.Structure):
                 ("prox_bytes", ctypes.c_double), ("xupdate_bytes", ctypes.c_double),
                 ("newton_iters", ctypes.c_longlong), ("jacobians", ctypes.c_longlong),
                 ("cg_iters", ctypes.c_longlong), ("t_jac_ms", ctypes.c_double), ("t_solve_ms", ctypes.c_double),
-                ("t_be_ms", ctypes.c_double)]
+                ("t_be_ms", ctypes.c_double), ("regrids", ctypes.c_longlong)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -90,6 +90,8 @@ def lib():
     L.mmadmm_stats_get.argtypes = [ctypes.c_void_p, ctypes.POINTER(mmadmm_stats)]
     L.mmadmm_stats_reset.argtypes = [ctypes.c_void_p]
     L.mmadmm_sync.argtypes = [ctypes.c_void_p]
+    L.mmadmm_regrid.argtypes = [ctypes.c_void_p, ctypes.c_double]
+    L.mmadmm_set_regrid.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.mmadmm_destroy.argtypes = [ctypes.c_void_p]
     L.mmadmm_mesh_rect.argtypes = [ctypes.c_int] * 4 + [ctypes.c_double] * 6 + [ctypes.c_int,
                                                                                  ctypes.POINTER(ctypes.c_void_p)]
@@ -422,6 +424,15 @@ class Engine:
 
     def sync(self):
         _check(lib().mmadmm_sync(self.h))
+
+    def regrid(self, t):
+        """Rebuild the monitor grid on the device from the current mesh at time t (the reference's
+        commented Mesh::setUp hook, src/Mesh.cpp:1006-1014; SURVEY §8f-2)."""
+        _check(lib().mmadmm_regrid(self.h, t))
+
+    def set_regrid(self, every_step=True):
+        """Time-varying monitor: rebuild the grid at the start of every step, t = steps * dt."""
+        _check(lib().mmadmm_set_regrid(self.h, 1 if every_step else 0))
 
     def block_grad(self, sid, z, dxpu=None, computeGrad=True, regularize=False):
         """Device Mesh::computeBlockGrad of one simplex -> (energy, grad, Igt)."""

@@ -263,8 +263,28 @@ static void anisoShell(int D, const double* x, double* M) {
     for (int j = 0; j < D; ++j) M[i * D + j] = ((i == j) ? lam2 : 0.0) + ((lam1 - lam2) * n[i]) * n[j];
 }
 
-// Registry by MonType (main.cpp:836-864; 6 = anisoShell)
-static void monitorAt(int D, int monType, const double* x, double* M) {
+// MonType 7: the build's time-varying monitor (no reference counterpart; BASELINE config 5,
+// SURVEY §8f-2): a bump moving on a circle, M = (1 + 5 / (1 + 50 |x - c(t)|^2)) I,
+// c(t) = (0.5 + 0.2 cos 2 pi t, 0.5 + 0.2 sin 2 pi t, 0.5) -- mm-admm_amd/csrc/host/monitors.cpp
+// (moving_bump_centre) and csrc/kernels/regrid_kernels.hip (k_monitor_tv), restated
+static void movingBump(int D, const double* x, double t, double* M) {
+  const double PI = 3.141592653589793238462643383;
+  const double c[3] = {0.5 + 0.2 * cos((2.0 * PI) * t), 0.5 + 0.2 * sin((2.0 * PI) * t), 0.5};
+  double sq = 0.0;
+  for (int d = 0; d < D; ++d) {
+    const double u = x[d] - c[d];
+    sq = (d == 0) ? u * u : sq + u * u;
+  }
+  const double sc = 1 + 5.0 / (1 + 50.0 * sq);
+  for (int i = 0; i < D * D; ++i) M[i] = (i / D == i % D) ? sc : 0.0;
+}
+
+// Registry by MonType (main.cpp:836-864; 6 = anisoShell, 7 = movingBump at time t)
+static void monitorAt(int D, int monType, const double* x, double* M, double t = 0.0) {
+  if (monType == 7) {
+    movingBump(D, x, t, M);
+    return;
+  }
   if (D == 2) {
     switch (monType) {
       case 0: monIdentity(2, M); return;
@@ -603,7 +623,7 @@ struct NN {
 };
 
 template <int D>
-static void buildGrid(const double* X, int nP, int monType, Grid<D>& g) {
+static void buildGrid(const double* X, int nP, int monType, Grid<D>& g, double t = 0.0) {
   // updateMesh (68-130): nx = ny = nz = (int)pow(X.size(), 1/D), bbox of the mesh
   const int sz = (int)std::pow((double)((long)nP * D), 1.0 / D);
   g.nx = sz;
@@ -623,7 +643,7 @@ static void buildGrid(const double* X, int nP, int monType, Grid<D>& g) {
   g.vals.assign(rows * D * D, 0.0);
   // evaluateAtVertices (MonitorFunction.cpp:16-32)
   std::vector<double> monVals((size_t)nP * D * D);
-  for (int v = 0; v < nP; ++v) monitorAt(D, monType, &X[v * D], &monVals[(size_t)v * D * D]);
+  for (int v = 0; v < nP; ++v) monitorAt(D, monType, &X[v * D], &monVals[(size_t)v * D * D], t);
   NN<D> nn;
   nn.build(X, nP);
   const int nx = g.nx, ny = g.ny;
@@ -744,6 +764,8 @@ struct Base {
   virtual ~Base() {}
   int dim = 2;
   int err = 0;
+  int regrid = 0;   // rebuild the monitor grid at every step start (time-varying monitors)
+  int monType = 0;
 };
 
 template <int D>
@@ -766,11 +788,12 @@ struct Integrator : Base {
   long long bfgsIters = 0;
 
   void init(int nP_, const double* Vp_, const double* Vc_, int nF_, const int* F_, const int* mask_,
-            int monType, double dt_, double tau_, double rho_, int gradUse_, int cgMode_) {
+            int monType_, double dt_, double tau_, double rho_, int gradUse_, int cgMode_) {
     dim = D;
     nP = nP_;
     nF = nF_;
     Vp.assign(Vp_, Vp_ + (size_t)nP * D);
+    monType = monType_;
     compMesh = (Vc_ != nullptr);
     if (compMesh) Vc.assign(Vc_, Vc_ + (size_t)nP * D);
     F.assign(F_, F_ + (size_t)nF * (D + 1));
@@ -1197,6 +1220,9 @@ struct Integrator : Base {
 
   // MeshIntegrator<D>::step (MeshIntegrator.cpp:101-191)
   double step(int nIters, double tol, int* itersOut, double* primalOut, double* dualOut) {
+    // Mesh<D>::setUp (src/Mesh.cpp:1006-1014, commented in the reference): with regrid on, the
+    // monitor grid is rebuilt from the current Vp and the monitor at t = steps * dt
+    if (regrid) buildGrid<D>(Vp.data(), nP, monType, grid, stepsTaken * dt);
     predictX(stepsTaken);
     xPrev = x;
     x = xBar;
@@ -1501,6 +1527,7 @@ int orc_step(void* h, int nIters, double tol, double* Ih, int* admmIters, double
   *Ih = r;
   return e;
 }
+void orc_set_regrid(void* h, int on) { ((Base*)h)->regrid = on; }
 int orc_euler_step(void* h, double* Ih) {
   double r = 0;
   DISPATCH(h, r = s->eulerStep(), r = s->eulerStep());

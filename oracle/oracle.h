@@ -44,6 +44,9 @@ void* orc_create(int dim, int nP, const double* Vp, const double* Vc, int nF, co
 int orc_step(void* h, int nIters, double tol, double* Ih, int* admmIters, double* primal,
              double* dual);
 int orc_euler_step(void* h, double* Ih);
+/* time-varying monitors: rebuild the monitor grid from Vp at every step start,
+ * monitor at t = steps * dt (MonType 7 moves with t) */
+void orc_set_regrid(void* h, int on);
 /* MeshIntegrator::backwardsEulerStep (method 2): Newton with the FD Jacobian at the initial mesh
  * and the LASolver restatement; dotMode 0 reference sums, 1 the GPU's reduction order */
 int orc_backward_euler_step(void* h, double dt, double tol, int dotMode, double* Ih, int* newtonIters);

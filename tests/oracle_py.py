@@ -46,6 +46,7 @@ def lib():
         L.orc_step.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, c_double_p, c_int_p,
                                c_double_p, c_double_p]
         L.orc_euler_step.argtypes = [ctypes.c_void_p, c_double_p]
+        L.orc_set_regrid.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_energy.restype = ctypes.c_double
         L.orc_energy.argtypes = [ctypes.c_void_p]
         L.orc_done.argtypes = [ctypes.c_void_p]
@@ -130,7 +131,7 @@ def set_threads(n):
 class Integrator:
     """Mesh<D> + MeshIntegrator<D> of the reference, restated on the CPU."""
 
-    def __init__(self, mesh, monType, dt, tau, rho, gradUse=False, Vc=None, nthreads=0, cgMode=0):
+    def __init__(self, mesh, monType, dt, tau, rho, gradUse=False, Vc=None, nthreads=0, cgMode=0, regrid=False):
         L = lib()
         self.dim = mesh.dim
         Vc_p = None
@@ -145,6 +146,8 @@ class Integrator:
         self.nP, self.nF, self.gridRows = nP.value, nF.value, gr.value
         self.gridN = (gx.value, gy.value, gz.value)
         self.K = self.dim * (self.dim + 1)
+        if regrid:  # time-varying monitor: grid rebuilt at every step start
+            L.orc_set_regrid(self.h, 1)
 
     def __del__(self):
         if getattr(self, "h", None):

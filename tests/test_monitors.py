@@ -23,7 +23,7 @@ def product_monitor(dim, mon):
     return ev
 
 
-@pytest.mark.parametrize("dim,mon", [(d, m) for d in (2, 3) for m in range(7)])
+@pytest.mark.parametrize("dim,mon", [(d, m) for d in (2, 3) for m in range(8)])
 def test_builtin_monitor_matches_oracle(dim, mon):
     rng = np.random.default_rng(10 * dim + mon)
     ev = product_monitor(dim, mon)
@@ -41,4 +41,4 @@ def test_aniso_shell_is_anisotropic():
 
 def test_builtin_monitor_range_checked():
     fn, user = mx.MONITOR_FN(), ctypes.c_void_p()
-    assert mx.lib().mmadmm_builtin_monitor(3, 7, ctypes.byref(fn), ctypes.byref(user)) != 0
+    assert mx.lib().mmadmm_builtin_monitor(3, 8, ctypes.byref(fn), ctypes.byref(user)) != 0
