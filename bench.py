@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-spmv", action="store_true")
     ap.add_argument("--no-be", action="store_true", help="skip the backward-Euler (method 2) section")
     ap.add_argument("--no-3d", action="store_true", help="skip the 3D (BASELINE config 4) section")
+    ap.add_argument("--c5", action="store_true",
+                    help="add BASELINE config 5 on one GPU: 3D 5.09M-node mesh, time-varying monitor")
     ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
                     help="c3: 2D 1M-node disc (the headline); c4: 3D 512k-node cube, anisotropic monitor")
     return ap.parse_args()
@@ -216,6 +218,45 @@ def c4_bench(mx, with_cpu, threads, admm_iter):
         out["cpu_baseline"] = {"value": round(1.0 / cdt, 3), "unit": "ADMM it/s", "cores": threads, "kind": "port",
                                "sample": "C4 mesh, 1 timed step of 1 ADMM iteration after set-up and the FD-Hessian "
                                          "step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, %d threads)" % threads}
+    return out
+
+
+def tv_bench(mx, n, admm_iter, steps=3):
+    """Time-varying monitor (BASELINE config 5's "time-varying monitor") on one GPU:
+    3D SquareGrid n (63: the C4 mesh; 136: C5, 5.09 M nodes), MonType 7 (a bump moving on a circle),
+    the monitor grid rebuilt on the device at every step start (mmadmm_set_regrid), dt 0.025 tau 0.5
+    rho 2000, admm_iter ADMM iterations per step.  value = ADMM it/s including the rebuilds."""
+    mesh = mx.MeshData.rect(3, n)
+    t0 = time.perf_counter()
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(3, 7), rho=2000.0, tau=0.5)
+    E = mx.Engine(M, 0.025)
+    E.set_regrid(True)
+    setup = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    E.step(admm_iter, -1.0)
+    E.sync()
+    first = time.perf_counter() - t0
+    E.step(admm_iter, -1.0)
+    E.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        E.step(admm_iter, -1.0)
+    E.sync()
+    el = time.perf_counter() - t0
+    E.set_regrid(False)
+    reps = 3
+    t1 = time.perf_counter()
+    for r in range(reps):
+        E.regrid(0.1 * r)
+    E.sync()
+    rg = (time.perf_counter() - t1) / reps
+    out = {"workload": "3D SquareGrid n=%d, %d nodes, %d tetrahedra, time-varying moving-bump monitor (MonType 7), "
+                       "grid rebuilt on the device every step, dt 0.025 tau 0.5 rho 2000, %d ADMM iterations per step"
+                       % (n, mesh.nP, mesh.nF, admm_iter),
+           "value": round(steps * admm_iter / el, 3), "unit": "ADMM it/s", "ms_per_step": round(el / steps * 1e3, 2),
+           "regrid_ms": round(rg * 1e3, 3), "first_step_ms": round(first * 1e3, 1), "setup_s": round(setup, 2),
+           "regrids": E.stats()["regrids"]}
+    E.close()
     return out
 
 
@@ -447,6 +488,11 @@ def main():
     if not args.no_3d and world == 1 and not c4:
         log("3D C4")
         result["c4_3d"] = c4_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
+        log("3D time-varying monitor")
+        result["c4_time_varying"] = tv_bench(mx, 63, args.admm_iter)
+    if args.c5 and world == 1 and rank == 0:
+        log("3D C5 time-varying (5.09 M nodes)")
+        result["c5_time_varying"] = tv_bench(mx, 136, args.admm_iter, steps=2)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c4:
         log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(mesh, args.admm_iter, threads)
