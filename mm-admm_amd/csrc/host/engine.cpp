@@ -119,6 +119,31 @@ class Engine final : public EngineBase {
     plan_ = make_partition_plan(D, nP, nF, Fh_.data(), nranks_, rank_);
     nP_ = (int)plan_.localNodes.size();
     nF_ = plan_.s1 - plan_.s0;
+    if (nranks_ > 1) {  // vertex owners for the partitioned regrid: the rank of the lowest incident simplex
+      std::vector<long long> minS(nP, (long long)nF);
+      for (long long sI = 0; sI < nF; ++sI)
+        for (int n = 0; n < D + 1; ++n) {
+          const int v = Fh_[(size_t)sI * (D + 1) + n];
+          if (sI < minS[v]) minS[v] = sI;
+        }
+      std::vector<std::vector<int>> owned(nranks_);
+      for (int v = 0; v < nP; ++v) {
+        int q = 0;  // isolated vertices: rank 0 (as the plan places them)
+        if (minS[v] < nF) q = (int)(std::upper_bound(plan_.sbeg.begin(), plan_.sbeg.end(), minS[v]) - plan_.sbeg.begin()) - 1;
+        owned[q].push_back(v);
+      }
+      size_t mx = 1;
+      for (auto& o : owned) mx = std::max(mx, o.size());
+      maxOwned_ = (int)mx;
+      std::vector<int> all((size_t)nranks_ * mx, -1), mine;
+      for (int q = 0; q < nranks_; ++q) std::copy(owned[q].begin(), owned[q].end(), all.begin() + (size_t)q * mx);
+      for (int v : owned[rank_])
+        mine.push_back((int)(std::lower_bound(plan_.localNodes.begin(), plan_.localNodes.end(), v) - plan_.localNodes.begin()));
+      nOwned_ = (int)mine.size();
+      ownAllGid_.upload(all.data(), all.size(), st_);
+      ownLocal_.upload(mine.data(), std::max<size_t>(mine.size(), 1), st_);
+      MMX_HIP(hipStreamSynchronize(st_));
+    }
     const int nl = nP_;
     // t = M + dt^2 WD_T W D is block diagonal: t_vv = tau + dt^2 * (w*w summed valence times)
     std::vector<double> invdiag(nl);
@@ -616,26 +641,37 @@ class Engine final : public EngineBase {
   // box, monitor at the vertices (MonType 7 on the device at time t; any other monitor through its
   // host callback), nearest vertex of every grid point, smoothing -- bit-identical to the host
   // set-up (regrid_kernels.hip).  One 2D-double readback (the bounding box) per call.
-  void setRegrid(bool on) override {
-    if (on && nranks_ > 1)
-      throw Error(MMADMM_ERR_INVALID, "regrid: the monitor grid needs every vertex; not available on a partition");
-    regridEachStep_ = on;
-  }
+  // On an element partition every rank needs every vertex: each rank sends the positions of the
+  // vertices it owns (lowest incident simplex), one all-gather, and every rank places all of them
+  // at their global ids and builds the same grid (the replicated interface positions are
+  // bit-identical across ranks, so the owner choice does not matter).
+  void setRegrid(bool on) override { regridEachStep_ = on; }
 
   void regrid(double t) override {
-    if (nranks_ > 1)
-      throw Error(MMADMM_ERR_INVALID, "regrid: the monitor grid needs every vertex; not available on a partition");
     constexpr int DD = D * D;
-    const int nb = std::max(1, std::min(256, (nP_ + 255) / 256));
+    const int nG = (nranks_ > 1) ? plan_.nP : nP_;  // vertices the grid is built from
+    const int nb = std::max(1, std::min(256, (nG + 255) / 256));
     if (!rgPart_.p) {
       rgPart_.alloc((size_t)256 * 2 * D);
-      rgMon_.alloc((size_t)nP_ * DD);
-      rgCellOf_.alloc(nP_);
-      rgNodes_.alloc(nP_);
+      rgMon_.alloc((size_t)nG * DD);
+      rgCellOf_.alloc(nG);
+      rgNodes_.alloc(nG);
       rgTmp_.alloc(gvals_.n);
+      if (nranks_ > 1) {
+        rgXg_.alloc((size_t)nG * D);
+        rgSend_.alloc((size_t)maxOwned_ * D);
+        rgRecv_.alloc((size_t)nranks_ * maxOwned_ * D);
+      }
       MMX_HIP(hipHostMalloc((void**)&rgHost_, sizeof(double) * 256 * 2 * D, hipHostMallocDefault));
     }
-    launch_bbox<D>(Vp_.p, nP_, rgPart_.p, nb, st_);
+    const double* X = Vp_.p;
+    if (nranks_ > 1) {
+      launch_rows_gather(D, ownLocal_.p, nOwned_, Vp_.p, rgSend_.p, st_);
+      comm_->allgather(rank_, rgSend_.p, rgRecv_.p, (size_t)maxOwned_ * D, st_);
+      launch_rows_scatter(D, ownAllGid_.p, nranks_ * maxOwned_, rgRecv_.p, rgXg_.p, st_);
+      X = rgXg_.p;
+    }
+    launch_bbox<D>(X, nG, rgPart_.p, nb, st_);
     MMX_HIP(hipMemcpyAsync(rgHost_, rgPart_.p, sizeof(double) * nb * 2 * D, hipMemcpyDeviceToHost, st_));
     MMX_HIP(hipStreamSynchronize(st_));
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -644,7 +680,7 @@ class Engine final : public EngineBase {
         lo[d] = std::min(lo[d], rgHost_[(size_t)b * 2 * D + d]);
         hi[d] = std::max(hi[d], rgHost_[(size_t)b * 2 * D + D + d]);
       }
-    grid_geometry(D, nP_, lo, hi, grid_);
+    grid_geometry(D, nG, lo, hi, grid_);
     gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
     gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
     if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
@@ -668,27 +704,27 @@ class Engine final : public EngineBase {
       rgScanBytes_ = bin_scan_bytes(ncell);
       rgScan_.alloc(std::max<size_t>(rgScanBytes_, 1));
     }
-    launch_bin<D>(Vp_.p, nP_, cg, rgCellOf_.p, rgCounts_.p, rgStarts_.p, rgFill_.p, rgNodes_.p, rgScan_.p,
-                  rgScanBytes_, st_);
+    launch_bin<D>(X, nG, cg, rgCellOf_.p, rgCounts_.p, rgStarts_.p, rgFill_.p, rgNodes_.p, rgScan_.p, rgScanBytes_,
+                  st_);
     // the monitor at the vertices (MonitorFunction::evaluateAtVertices, src/MonitorFunction.cpp:16-32)
     if (builtin_monitor_kind(monFn_, monUser_) == 7) {
       double c[3];
       moving_bump_centre(t, c);
-      launch_monitor_tv<D>(Vp_.p, nP_, c, rgMon_.p, st_);
+      launch_monitor_tv<D>(X, nG, c, rgMon_.p, st_);
     } else {  // a host plugin: evaluated on the host at the current vertices, as the reference does
-      std::vector<double> X((size_t)nP_ * D), mv((size_t)nP_ * DD);
-      MMX_HIP(hipMemcpyAsync(X.data(), Vp_.p, X.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
+      std::vector<double> Xh((size_t)nG * D), mv((size_t)nG * DD);
+      MMX_HIP(hipMemcpyAsync(Xh.data(), X, Xh.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
       MMX_HIP(hipStreamSynchronize(st_));
-      for (int v = 0; v < nP_; ++v) {
+      for (int v = 0; v < nG; ++v) {
         double M[9];
         for (int i = 0; i < DD; ++i) M[i] = 0.0;
-        monFn_(D, &X[(size_t)v * D], M, monUser_);
+        monFn_(D, &Xh[(size_t)v * D], M, monUser_);
         std::memcpy(&mv[(size_t)v * DD], M, DD * sizeof(double));
       }
       MMX_HIP(hipMemcpyAsync(rgMon_.p, mv.data(), mv.size() * sizeof(double), hipMemcpyHostToDevice, st_));
       MMX_HIP(hipStreamSynchronize(st_));
     }
-    launch_nn_fill<D>(Vp_.p, cg, rgStarts_.p, rgNodes_.p, gx_.p, gy_.p, D == 3 ? gz_.p : gy_.p, grid_.nx, grid_.ny,
+    launch_nn_fill<D>(X, cg, rgStarts_.p, rgNodes_.p, gx_.p, gy_.p, D == 3 ? gz_.p : gy_.p, grid_.nx, grid_.ny,
                       grid_.nz, rgMon_.p, rgTmp_.p, st_);
     const int passes = (D == 2) ? 5 : 2;  // smoothMonitorGrid
     double* cur = rgTmp_.p;
@@ -784,7 +820,9 @@ class Engine final : public EngineBase {
   mmadmm_monitor_fn monFn_ = nullptr;
   void* monUser_ = nullptr;
   bool regridEachStep_ = false, gridOnDevice_ = false;
-  DevBuf<double> rgPart_, rgMon_, rgTmp_;
+  DevBuf<double> rgPart_, rgMon_, rgTmp_, rgXg_, rgSend_, rgRecv_;
+  DevBuf<int> ownLocal_, ownAllGid_;  // partitioned regrid: my owned vertices (local ids), all ranks' (global ids)
+  int nOwned_ = 0, maxOwned_ = 1;
   DevBuf<int> rgCellOf_, rgNodes_, rgCounts_, rgStarts_, rgFill_;
   DevBuf<unsigned char> rgScan_;
   size_t rgScanBytes_ = 0;

@@ -35,4 +35,8 @@ void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, cons
 template <int D>
 void launch_smooth(const double* in, double* out, int nx, int ny, int nz, hipStream_t st);
 
+// rows of D doubles: out[i] = in[idx[i]] (gather) / out[idx[i]] = in[i] for idx[i] >= 0 (scatter)
+void launch_rows_gather(int D, const int* idx, int n, const double* in, double* out, hipStream_t st);
+void launch_rows_scatter(int D, const int* idx, int n, const double* in, double* out, hipStream_t st);
+
 }  // namespace mmx

@@ -201,6 +201,21 @@ __global__ void __launch_bounds__(kRB) k_smooth(const double* __restrict__ in, d
   }
 }
 
+// partitioned regrid: rows of D doubles gathered by index (pack a rank's owned vertices) or
+// scattered by index (place every rank's vertices at their global ids; idx < 0 = padding)
+__global__ void __launch_bounds__(kRB) k_rows_gather(int D, const int* __restrict__ idx, int n,
+                                                     const double* __restrict__ in, double* __restrict__ out) {
+  const int i = blockIdx.x * kRB + threadIdx.x;
+  if (i >= n) return;
+  for (int c = 0; c < D; ++c) out[(size_t)i * D + c] = in[(size_t)idx[i] * D + c];
+}
+__global__ void __launch_bounds__(kRB) k_rows_scatter(int D, const int* __restrict__ idx, int n,
+                                                      const double* __restrict__ in, double* __restrict__ out) {
+  const int i = blockIdx.x * kRB + threadIdx.x;
+  if (i >= n || idx[i] < 0) return;
+  for (int c = 0; c < D; ++c) out[(size_t)idx[i] * D + c] = in[(size_t)i * D + c];
+}
+
 inline unsigned blocks(long long n) { return (unsigned)((n + kRB - 1) / kRB); }
 
 }  // namespace
@@ -246,6 +261,13 @@ template <int D>
 void launch_smooth(const double* in, double* out, int nx, int ny, int nz, hipStream_t st) {
   const long long rows = (long long)(nx + 1) * (ny + 1) * (D == 3 ? nz + 1 : 1);
   hipLaunchKernelGGL(k_smooth<D>, dim3(blocks(rows)), dim3(kRB), 0, st, in, out, nx, ny, nz);
+}
+
+void launch_rows_gather(int D, const int* idx, int n, const double* in, double* out, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_rows_gather, dim3(blocks(n)), dim3(kRB), 0, st, D, idx, n, in, out);
+}
+void launch_rows_scatter(int D, const int* idx, int n, const double* in, double* out, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_rows_scatter, dim3(blocks(n)), dim3(kRB), 0, st, D, idx, n, in, out);
 }
 
 #define MMX_REGRID_INST(D)                                                                                       \
