@@ -442,7 +442,7 @@ def main():
     xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
     prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
     xup_gbs = st["xupdate_bytes"] / (xup_ms * 1e-3) / 1e9
-    prox_name = "k_prox_wave<3, false>" if c4 else "k_prox_lds<2, %d>" % int(os.environ.get("MMX_PROX_BLOCK", "256"))
+    prox_name = "k_prox_wave<3, false>" if c4 else "k_prox_lds<2, %d>" % int(os.environ.get("MMX_PROX_BLOCK", "128"))
     # the committed PMC passes profile the default run (C3 and the C4 section): per-launch figures
     # of another mesh size do not apply to C5
     traffic, traffic_raw = pmc_traffic(prox_name) if not c5 else (None, None)

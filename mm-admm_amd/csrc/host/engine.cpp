@@ -282,14 +282,20 @@ class Engine final : public EngineBase {
       hessComputed_ = true;
       stepTaken_ = true;
       exchange(0);
-      launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, true, st_);
+      // the primal residual ||D x - z|| (src/MeshIntegrator.cpp:162) only feeds the early-exit test
+      // and the reported last residual: without the early exit it is formed on the last iteration
+      const bool resid = early || i == nIters - 1;
+      launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, resid, st_);
       if (timing) {
         b1 = nextEvent();
         MMX_HIP(hipEventRecord(b1, st_));
         timed_.push_back({a0, a1, b1});
       }
-      launch_reduce_partials2(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, partB_.p, nbx,
-                              results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
+      if (resid)
+        launch_reduce_partials2(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, partB_.p, nbx,
+                                results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
+      else
+        launch_reduce_partials(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, st_);
       done = i + 1;
       if (early) {
         std::vector<double> rv;

@@ -22,7 +22,7 @@ namespace mmx {
 
 constexpr int kBlock = 256;
 constexpr int kLdsStride = kBlock + 1;  // padded SoA stride of the LDS Bkinv image
-constexpr int kProxBlock = 256;         // steady-state 2D prox workgroup (measured)
+constexpr int kProxBlock = 128;         // steady-state 2D prox workgroup (measured: 128 > 256 > 64 end to end)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -832,21 +832,30 @@ __global__ void __launch_bounds__(64, 2) k_prox_wave(DeviceMesh<D> m, double tol
     entry_grad<D, false>(g, fc, z, xi, dx, gcv, useCache != 0, G, Igt, bad, &tie);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
-#pragma unroll
-    for (int i = 0; i < K; ++i) pk[i * 64] = dx[i];
     const size_t gb = (size_t)blockIdx.x * KK * 64 + tid;
     WaveB<K> Bacc{Bin + gb, Bout + gb};
+#ifdef MMX_EXP_NOPARK  // experiment: BFGS state in registers
+    const int its = tie ? 0
+                        : bfgs_iterations<D, WaveB<K>, false, 0>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc,
+                                                                 &tie);
+#else
+#pragma unroll
+    for (int i = 0; i < K; ++i) pk[i * 64] = dx[i];
     const int its = tie ? 0
                         : bfgs_iterations<D, WaveB<K>, false, 64>(Bacc, g, fc, z, xi, nullptr, G, fixedBits, tol,
                                                                   bad, gc, &tie, pk);
 #pragma unroll
     for (int i = 0; i < K; ++i) dx[i] = pk[i * 64];
+#endif
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       const double d = z[i] - zs[i];
       dual2 += d * d;
     }
+#if defined(MMX_EXP_NOGRAD)
+    bad = false;  // timing experiments: the numerics are meaningless
+#endif
     pv[0] = Ihsave;
     pv[1] = dual2;
     pv[3] = (double)its;
@@ -1045,39 +1054,51 @@ __global__ void __launch_bounds__(kBlock) k_pack_export(int mode, int nExp, cons
     out[(size_t)e * D + c] = (mode == 0) ? w * (w * (z[off + c] - u[off + c])) : gs[off + c];
 }
 
-__global__ void __launch_bounds__(kBlock) k_reduce_partials(const double* __restrict__ partials, int nblocks,
-                                                             double* __restrict__ out, const double* __restrict__ partials2,
-                                                             int nblocks2, double* __restrict__ out2) {
+constexpr int kRed = 1024;
+__global__ void __launch_bounds__(kRed) k_reduce_partials(const double* __restrict__ partials, int nblocks,
+                                                           double* __restrict__ out, const double* __restrict__ partials2,
+                                                           int nblocks2, double* __restrict__ out2) {
   if (blockIdx.x == 1) {  // second set in the same launch
     partials = partials2;
     nblocks = nblocks2;
     out = out2;
   }
-  // one workgroup; lane-strided partial sums then a fixed-shape tree
-  __shared__ double red[kBlock][kNumPartials];
+  // one workgroup of 1024: lane-strided sums in a fixed order (four rows requested at a time),
+  // then the wavefront butterflies and the 16 wavefront results in order -- a fixed shape
+  __shared__ double red[kRed / 64][kNumPartials];
+  const int tid = threadIdx.x;
   double acc[kNumPartials];
 #pragma unroll
-  for (int i = 0; i < kNumPartials; ++i) acc[i] = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+  for (int i = 0; i < kNumPartials; ++i) acc[i] = 0.0;  // entry 5 (a max of counts >= 0) too
+  int b = tid;
+  for (; b + 3 * kRed < nblocks; b += 4 * kRed) {
+    double v[4][kNumPartials];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < kNumPartials; ++i) v[q][i] = partials[(size_t)(b + q * kRed) * kNumPartials + i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < kNumPartials; ++i) acc[i] = (i == 5) ? fmax(acc[i], v[q][i]) : acc[i] + v[q][i];
+  }
+  for (; b < nblocks; b += kRed)
 #pragma unroll
     for (int i = 0; i < kNumPartials; ++i) {
       const double v = partials[(size_t)b * kNumPartials + i];
       acc[i] = (i == 5) ? fmax(acc[i], v) : acc[i] + v;
     }
-  }
 #pragma unroll
-  for (int i = 0; i < kNumPartials; ++i) red[threadIdx.x][i] = acc[i];
+  for (int i = 0; i < kNumPartials; ++i) acc[i] = (i == 5) ? wave_max(acc[i]) : wave_sum(acc[i]);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < kNumPartials; ++i) red[tid >> 6][i] = acc[i];
   __syncthreads();
-  for (int w = kBlock / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) {
-#pragma unroll
-      for (int i = 0; i < kNumPartials; ++i)
-        red[threadIdx.x][i] = (i == 5) ? fmax(red[threadIdx.x][i], red[threadIdx.x + w][i])
-                                       : red[threadIdx.x][i] + red[threadIdx.x + w][i];
-    }
-    __syncthreads();
+  if (tid < kNumPartials) {
+    double r = red[0][tid];
+    for (int w = 1; w < kRed / 64; ++w) r = (tid == 5) ? fmax(r, red[w][tid]) : r + red[w][tid];
+    out[tid] = r;
   }
-  if (threadIdx.x < kNumPartials) out[threadIdx.x] = red[0][threadIdx.x];
 }
 
 // one-simplex evaluation for tests: Mesh::computeBlockGrad (regularised, FIXED rows zeroed)
@@ -1239,11 +1260,11 @@ void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, dou
   hipLaunchKernelGGL(k_euler_apply<D>, dim3(nblk_xcd(m.nP)), dim3(kBlock), 0, st, m, gs, x, dt_over_tau, xcd_map());
 }
 void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, st, partials, nblocks, out, partials, nblocks, out);
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kRed), 0, st, partials, nblocks, out, partials, nblocks, out);
 }
 void launch_reduce_partials2(const double* partials, int nblocks, double* out, const double* partials2, int nblocks2,
                              double* out2, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_partials, dim3(2), dim3(kBlock), 0, st, partials, nblocks, out, partials2, nblocks2, out2);
+  hipLaunchKernelGGL(k_reduce_partials, dim3(2), dim3(kRed), 0, st, partials, nblocks, out, partials2, nblocks2, out2);
 }
 template <int D>
 void launch_debug_blockgrad(const DeviceMesh<D>& m, int s, const double* z, const double* dx, double* out, int flags,
