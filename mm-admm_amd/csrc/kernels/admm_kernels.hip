@@ -362,6 +362,11 @@ struct LdsB {
   // 2D: keeping the previous pass's K*K = 36 values in registers is cheaper than re-reading LDS
   __device__ __forceinline__ void fresh() {}
 };
+// address-space-qualified pointers: they keep global (and LDS) accesses as global_/ds_ instructions
+// through the pointer laundering below (a plain pointer out of an asm operand becomes flat)
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(3))) double ldouble;
+
 // Global, wave-interleaved (entry ij of simplex s at ((s/64)*K*K + ij)*64 + s%64: a wavefront's
 // access to one entry is 512 contiguous bytes).  Double-buffered across proxes: the first BFGS
 // iteration reads the previous prox's buffer `rd` and writes `wr`, later iterations work in `wr`,
@@ -369,14 +374,37 @@ struct LdsB {
 template <int K>
 struct WaveB {
   static constexpr bool kRowFence = true;
-  const double* rd;
-  double* wr;
+  const gdouble* rd;
+  gdouble* wr;
   __device__ __forceinline__ double get(int i, int j) const { return rd[(i * K + j) * 64]; }
   __device__ __forceinline__ void set(int i, int j, double v) const { wr[(i * K + j) * 64] = v; }
   __device__ __forceinline__ void advance() { rd = wr; }
   // a pass over the matrix re-reads it: an opaque pointer stops the compiler from forwarding the
   // previous pass's K*K = 144 loads in registers (3D spilled)
-  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)); }
+  // the memory clobber keeps the LDS rows in LDS (no store-to-load forwarding into registers)
+  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
+};
+
+// 3D with one wavefront per SIMD: the first RL rows of the lane's Bkinv held in LDS for the whole
+// prox (read from global once, in the prologue), the rest streamed from global as in WaveB.  Row
+// indices are compile-time in the unrolled passes, so every get/set resolves to one of the two.
+template <int K, int RL>
+struct HybB {
+  static constexpr bool kRowFence = true;
+  const gdouble* rd;
+  gdouble* wr;
+  ldouble* lds;  // &ldsRows[lane], entries strided by 64
+  __device__ __forceinline__ double get(int i, int j) const {
+    return (i < RL) ? lds[(i * K + j) * 64] : rd[(i * K + j) * 64];
+  }
+  __device__ __forceinline__ void set(int i, int j, double v) const {
+    if (i < RL) lds[(i * K + j) * 64] = v;
+    wr[(i * K + j) * 64] = v;
+  }
+  __device__ __forceinline__ void advance() { rd = wr; }
+  // each pass re-reads: the laundered pointers keep the global rows from being held across passes
+  // the memory clobber keeps the LDS rows in LDS (no store-to-load forwarding into registers)
+  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
 };
 
 // index of Bkinv entry ij of simplex s: 2D simplex-major (the LDS kernel's chunks), 3D
@@ -786,17 +814,23 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 // pass meets a near-midpoint power (EXACT = false) is abandoned unwritten and recomputed exactly
 // by k_prox_fix from the untouched inputs, as in the 2D kernel.
 template <int D, bool COMP>
-__global__ void __launch_bounds__(64, 2) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+#ifndef MMX_WAVE_OCC
+#define MMX_WAVE_OCC 1  // measured: one wave per SIMD without spills beats two with 75 spilled VGPRs
+#endif
+__global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                      double* __restrict__ zg, double* __restrict__ ug,
                                                      const double* Bin, double* Bout, double* __restrict__ partials,
                                                      int useCache) {
   constexpr int K = D * (D + 1), KK = K * K;
-  __shared__ double park[3 * K * 64];  // DXpU, G, p per lane (bfgs_iterations PS = 64)
+#ifndef MMX_HYB_RL
+#define MMX_HYB_RL 0
+#endif
+  constexpr int RL = MMX_HYB_RL;  // Bkinv rows held in LDS for the whole prox (0: all streamed)
+  __shared__ double ldsRows[(RL > 0 ? RL : 1) * K * 64];
   const int tid = threadIdx.x;
   const int s0 = blockIdx.x * 64;
   const bool act = s0 + tid < m.nF;
   const int s = act ? s0 + tid : s0;
-  double* pk = park + tid;
   int f[D + 1];
   loadVerts<D>(m, s, f);
   const unsigned fixedBits = m.sbits[s] & 0xF;
@@ -833,20 +867,18 @@ __global__ void __launch_bounds__(64, 2) k_prox_wave(DeviceMesh<D> m, double tol
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
     const size_t gb = (size_t)blockIdx.x * KK * 64 + tid;
-    WaveB<K> Bacc{Bin + gb, Bout + gb};
-#ifdef MMX_EXP_NOPARK  // experiment: BFGS state in registers
-    const int its = tie ? 0
-                        : bfgs_iterations<D, WaveB<K>, false, 0>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc,
-                                                                 &tie);
-#else
-#pragma unroll
-    for (int i = 0; i < K; ++i) pk[i * 64] = dx[i];
-    const int its = tie ? 0
-                        : bfgs_iterations<D, WaveB<K>, false, 64>(Bacc, g, fc, z, xi, nullptr, G, fixedBits, tol,
-                                                                  bad, gc, &tie, pk);
-#pragma unroll
-    for (int i = 0; i < K; ++i) dx[i] = pk[i * 64];
-#endif
+    int its;
+    if constexpr (RL > 0) {
+#pragma unroll 8
+      for (int e = 0; e < RL * K; ++e) ldsRows[e * 64 + tid] = Bin[gb + (size_t)e * 64];
+      HybB<K, RL> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsRows + tid)};
+      its = tie ? 0
+                : bfgs_iterations<D, HybB<K, RL>, false, 0>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+    } else {
+      WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb)};
+      its = tie ? 0
+                : bfgs_iterations<D, WaveB<K>, false, 0>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+    }
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
