@@ -30,6 +30,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mm-admm_amd", "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, spec)
+# CPU-baseline legs, run after all GPU timing so host threads (OpenMP workers still spinning after a
+# parallel region) cannot delay the launches of a measured GPU section
+DEFERRED = []
 
 
 def parse():
@@ -109,7 +112,7 @@ def spmv_bench(torch, la, mx, with_cpu):
                      "sweep_ms": round(st["t_sweep_ms"] / max(st["n_sweep_timed"], 1), 3),
                      "sweep_kernel": "k_chain_sweep (E=%d)" % st["sweep_e"] if st["sweep_mode"] else "k_sweep",
                      "ms_per_iter": round((st["t_solve_ms"] - st["t_factor_ms"]) / max(nitr, 1), 2)}
-    if with_cpu:
+    def _cpu():
         import time as _t
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import lasolver_py as L
@@ -123,6 +126,8 @@ def spmv_bench(torch, la, mx, with_cpu):
         out["cpu_baseline"] = {"matmult_ms": round(cms, 2), "solve_ms": round(csolve, 1), "nitr": cit, "cores": 1,
                                "kind": "port", "sample": "oracle/lasolver.cpp (bit-identical restatement of "
                                "lib/LASolver, itself pinned to the reference build): 3 matmults + 1 solve"}
+    if with_cpu:  # CPU baselines run after every GPU measurement (main)
+        DEFERRED.append(_cpu)
     A.close()
     return out
 
@@ -150,7 +155,7 @@ def be_bench(mx, with_cpu):
            "newton_per_step": st["newton_iters"] / steps, "cg_iters_per_step": st["cg_iters"] / steps,
            "solve_ms_per_step": round(st["t_solve_ms"] / steps, 2)}
     E.close()
-    if with_cpu:  # the oracle's restatement, one core, on a bounded sample of the same family
+    def _cpu():  # the oracle's restatement, one core, on a bounded sample of the same family
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_py
         n = 400
@@ -165,6 +170,8 @@ def be_bench(mx, with_cpu):
                                "step_ms_per_1M_nodes": round(cdt * 1e3 * 1001113 / om.nP, 1),
                                "sample": "oracle/oracle.cpp backwards_euler_step (FD Jacobian + LASolver "
                                          "restatement) on SquareGrid n=%d, 3 steady steps after the first" % n}
+    if with_cpu:  # CPU baselines run after every GPU measurement (main)
+        DEFERRED.append(_cpu)
     return out
 
 
@@ -208,7 +215,7 @@ def c4_bench(mx, with_cpu, threads, admm_iter):
     tr, trr = pmc_traffic("k_prox_wave<3, false>")
     out["roofline"]["traffic"], out["roofline"]["traffic_fetch_uncorrected"] = tr, trr
     E.close()
-    if with_cpu:  # the oracle (OpenMP prox), same mesh: the FD-Hessian step untimed, then 1 iteration
+    def _cpu():  # the oracle (OpenMP prox), same mesh: the FD-Hessian step untimed, then 1 iteration
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_py
         om = oracle_py.Mesh(3, mesh.Xp, mesh.F, mesh.mask)
@@ -220,6 +227,8 @@ def c4_bench(mx, with_cpu, threads, admm_iter):
         out["cpu_baseline"] = {"value": round(1.0 / cdt, 3), "unit": "ADMM it/s", "cores": threads, "kind": "port",
                                "sample": "C4 mesh, 1 timed step of 1 ADMM iteration after set-up and the FD-Hessian "
                                          "step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, %d threads)" % threads}
+    if with_cpu:  # CPU baselines run after every GPU measurement (main)
+        DEFERRED.append(_cpu)
     return out
 
 
@@ -515,6 +524,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c4:
         log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(mesh, args.admm_iter, threads)
+    for f in DEFERRED:  # the sections' CPU baselines, after every GPU measurement
+        f()
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
