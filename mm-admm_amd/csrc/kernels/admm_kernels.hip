@@ -423,16 +423,11 @@ __device__ __forceinline__ size_t bidx(int s, int ij) {
 // search, <= 50 iterations, stop when ||grad||_1 < tol.  Returns the iteration count.
 // EXACT = false: the fast path; a power near a rounding midpoint raises *tie (the caller then
 // recomputes the simplex exactly) and the loop stops.
-// PS > 0 (3D): register relief for the blockGrad in the loop -- DXpU lives in LDS (`park`, entries
-// strided by PS: [0, K) DXpU, [K, 2K) G, [2K, 3K) p; the caller stores DXpU there and `dx` is
-// unused), G and p are parked there across the blockGrad, and the regulariser is added after an
-// unregularised blockGrad with blockGrad's own expressions (bit-identical, as entry_grad's cache
-// path does).
-template <int D, class BA, bool EXACT = true, int PS = 0>
+template <int D, class BA, bool EXACT = true>
 __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const FunctionalConsts<D>& fc,
                                                double* z, const double* xi, const double* dx, double* G,
                                                unsigned fixedBits, double tol, bool& bad, double* gcache,
-                                               bool* tie = nullptr, double* park = nullptr) {
+                                               bool* tie = nullptr) {
   constexpr int K = D * (D + 1);
   int iter;
   for (iter = 0; iter < 50; iter++) {
@@ -454,31 +449,9 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
 #pragma unroll
     for (int i = 0; i < K; ++i) G1[i] = G[i] * 0.5;
 #else
-    if constexpr (PS == 0) {
+    {
       const double e = blockGrad<D, true, true, EXACT>(g, fc, z, xi, dx, G1, Igt, gcache, tie);
       bad |= (e != e);
-    } else {
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        park[(K + i) * PS] = G[i];
-        park[(2 * K + i) * PS] = pk[i];
-      }
-      const double e = blockGrad<D, true, false, EXACT>(g, fc, z, xi, nullptr, G1, Igt, gcache, tie);
-      double sq = 0.0;
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        const double t = park[i * PS] - z[i];
-        sq = (i == 0) ? t * t : sq + t * t;
-      }
-      const double er = e + 0.5 * fc.w * fc.w * sq;  // blockGrad<REG>'s return value
-      bad |= (er != er);
-#pragma unroll
-      for (int i = 0; i < K; ++i) G1[i] += fc.w * fc.w * (-park[i * PS] + z[i]);
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        G[i] = park[(K + i) * PS];
-        pk[i] = park[(2 * K + i) * PS];
-      }
     }
 #endif
     if constexpr (!EXACT) {
@@ -873,11 +846,11 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
       for (int e = 0; e < RL * K; ++e) ldsRows[e * 64 + tid] = Bin[gb + (size_t)e * 64];
       HybB<K, RL> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsRows + tid)};
       its = tie ? 0
-                : bfgs_iterations<D, HybB<K, RL>, false, 0>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+                : bfgs_iterations<D, HybB<K, RL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     } else {
       WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb)};
       its = tie ? 0
-                : bfgs_iterations<D, WaveB<K>, false, 0>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+                : bfgs_iterations<D, WaveB<K>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     }
     double dual2 = 0.0;
 #pragma unroll
