@@ -184,6 +184,10 @@ class Engine final : public EngineBase {
     gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
     if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
     gvals_.upload(grid_.vals.data(), grid_.vals.size(), st_);
+    if (D == 3) {
+      gpad_.alloc(gvals_.n / 9 * 10);
+      launch_pad_rows(gvals_.p, (long long)(gvals_.n / 9), gpad_.p, st_);
+    }
     Vp_.upload(Vl.data(), Vl.size(), st_);  // Mesh::Vp
     x_.upload(Vl.data(), Vl.size(), st_);   // MeshIntegrator ctor: x = xPrev = xBar = copyX(Vp)
     xPrev_.upload(Vl.data(), Vl.size(), st_);
@@ -741,6 +745,7 @@ class Engine final : public EngineBase {
     }
     if (cur != gvals_.p)
       MMX_HIP(hipMemcpyAsync(gvals_.p, cur, gvals_.n * sizeof(double), hipMemcpyDeviceToDevice, st_));
+    if (D == 3) launch_pad_rows(gvals_.p, (long long)(gvals_.n / 9), gpad_.p, st_);
     MMX_HIP(hipGetLastError());
     gridOnDevice_ = true;
     m_ = makeView();
@@ -770,6 +775,7 @@ class Engine final : public EngineBase {
     m.gy = gy_.p;
     m.gz = (D == 3) ? gz_.p : gy_.p;
     m.gvals = gvals_.p;
+    m.gpad = (D == 3) ? gpad_.p : nullptr;
     m.gnx = grid_.nx;
     m.gny = grid_.ny;
     m.gnz = grid_.nz;
@@ -836,7 +842,7 @@ class Engine final : public EngineBase {
   hipStream_t st_ = nullptr;
   DevBuf<int32_t> F_, incPtr_, incOff_;
   DevBuf<uint8_t> sbits_, interior_;
-  DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_;
+  DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_, gpad_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
   DevBuf<int32_t> expOff_, tieList_;
   DevBuf<unsigned> tieCount_;

@@ -23,6 +23,7 @@ struct GridView {  // the smoothed monitor grid, rows of D*D doubles
   const double* gy;
   const double* gz;
   const double* vals;
+  const double* pad;  // 3D: the grid rows padded to 10 doubles (16-byte aligned rows)
   int nx, ny, nz;
   double hx, hy, hz;     // gx[1]-gx[0] etc., the divisors of findLimInfMeshPoint
   double rhx, rhy, rhz;  // RN(1/h)
@@ -157,6 +158,10 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     mv.m[1][0] = c0 * a1.x + c1 * b1.x + c2 * e1.x + c3 * f1.x;
     mv.m[1][1] = c0 * a1.y + c1 * b1.y + c2 * e1.y + c3 * f1.y;
   } else {
+#ifdef MMX_EXP_NOMON  // timing experiment: no grid gathers (numerics meaningless)
+    for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = (n % 4 == 0) ? 1.0 + 1e-3 * pnt[n / 3] : 0.0;
+    return;
+#endif
     const int zInd = findLimInf(pnt[2], g.az, g.nz + 1, g.hz, g.rhz);
     const double x0 = g.gx[xInd], x1 = g.gx[xInd + 1];
     const double y0 = g.gy[yInd], y1 = g.gy[yInd + 1];
@@ -172,12 +177,21 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
     const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
                             base + P, base + P + 1, base + P + nx + 1, base + P + nx + 2};
+    // rows read from the 10-double padded copy: 5 16-byte loads per row instead of 9 8-byte ones
+    // (the same values; the sums below are unchanged)
     double f[9];
 #pragma unroll
     for (int n = 0; n < 9; ++n) f[n] = 0.0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const double* r = g.vals + rows[q] * 9;
+      const double2* rp = reinterpret_cast<const double2*>(g.pad + rows[q] * 10);
+      double r[10];
+#pragma unroll
+      for (int e = 0; e < 5; ++e) {
+        const double2 v = rp[e];
+        r[2 * e] = v.x;
+        r[2 * e + 1] = v.y;
+      }
 #pragma unroll
       for (int n = 0; n < 9; ++n) f[n] += c[q] * r[n];
     }

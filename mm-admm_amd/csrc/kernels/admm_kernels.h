@@ -31,6 +31,7 @@ struct DeviceMesh {
   const double* gy;
   const double* gz;
   const double* gvals;
+  const double* gpad;    // 3D: the grid rows padded to 10 doubles (launch_pad_rows)
   int gnx, gny, gnz;
   double ghx, ghy, ghz, grhx, grhy, grhz;  // grid spacings of findLimInf and RN(1/h)
   double gax, gay, gaz, gspx, gspy, gspz, gnsx, gnsy, gnsz, grnsx, grnsy, grnsz;  // linspace params
@@ -58,6 +59,9 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
                     bool resid, hipStream_t st);
 // useCache: z is unchanged since the previous prox, whose last blockGrad left the unregularised
 // gradient in m.gcache; the entry blockGrad then reduces to adding the regulariser.
+// 3D: pad[r 10 + n] = vals[r 9 + n], pad[r 10 + 9] = 0 (rebuilt whenever vals changes)
+void launch_pad_rows(const double* vals, long long rows, double* pad, hipStream_t st);
+
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z,
                  double* u, const double* Bin, double* Bout, double* partials, int* nblocks, hipStream_t st);

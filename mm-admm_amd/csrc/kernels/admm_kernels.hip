@@ -67,6 +67,7 @@ __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   g.gy = m.gy;
   g.gz = m.gz;
   g.vals = m.gvals;
+  g.pad = m.gpad;
   g.nx = m.gnx;
   g.ny = m.gny;
   g.nz = m.gnz;
@@ -1202,6 +1203,16 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   else
     hipLaunchKernelGGL((k_xupdate<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
                        partials, xcd_map());
+}
+__global__ void __launch_bounds__(kBlock) k_pad_rows(const double* __restrict__ vals, long long rows,
+                                                      double* __restrict__ pad) {
+  const long long r = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= rows) return;
+  for (int n = 0; n < 9; ++n) pad[r * 10 + n] = vals[r * 9 + n];
+  pad[r * 10 + 9] = 0.0;
+}
+void launch_pad_rows(const double* vals, long long rows, double* pad, hipStream_t st) {
+  if (rows > 0) hipLaunchKernelGGL(k_pad_rows, dim3((unsigned)((rows + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vals, rows, pad);
 }
 // reuse of the previous prox's last gradient at the prox entry (MMX_GRAD_CACHE=0 disables)
 static int cache_enabled() {
