@@ -146,6 +146,15 @@ int mmadmm_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, doub
 int mmadmm_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int btype,
                            int compact_mask, mmadmm_mesh* out);
 /* hexagonal disc of radius r centred (cx, cy): 3N(N+1)+1 nodes, 6N^2 triangles, rim FIXED */
+/* setUpShoulderExperiment (main.cpp:403-630): rect mesh minus the upper (x, y[, z]) quadrant's
+ * simplices, re-marked boundary, interior vertices moved by up to h/10 in a random direction drawn with
+ * glibc rand() (seed it as main.cpp:785 does: srand(69)) and Eigen 3.4 Random() semantics (Eigen is
+ * un-vendored in the reference: version unpinned).  The unmoved positions (the CompMesh reference
+ * Vc) come from mmadmm_mesh_reference_points. */
+int mmadmm_mesh_shoulder(int dim, int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za,
+                         double zb, int btype, mmadmm_mesh* out);
+/* Vc of a mesh (the unmoved positions of a Shoulder mesh; Vp for the other generators) */
+int mmadmm_mesh_reference_points(mmadmm_mesh h, double* Xc);
 int mmadmm_mesh_hexdisc(int N, double r, double cx, double cy, int btype, mmadmm_mesh* out);
 int mmadmm_mesh_read(int dim, const char* tri, const char* pnts, const char* mask, mmadmm_mesh* out);
 int mmadmm_mesh_sizes(mmadmm_mesh m, int* dim, int* nP, int* nF, int* mask_len);

@@ -74,6 +74,7 @@ struct MeshBuf {
   std::vector<double> Vp;
   std::vector<int32_t> F;
   std::vector<int32_t> mask;
+  std::vector<double> Vc;  // reference positions when they differ from Vp (Shoulder), else empty
   int nP() const { return (int)(Vp.size() / dim); }
   int nF() const { return (int)(F.size() / (dim + 1)); }
 };

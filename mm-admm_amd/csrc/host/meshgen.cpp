@@ -6,11 +6,18 @@
 //                           main.cpp:33-40); the O(nP*nF) remap loop (510-518) is replaced by an
 //                           O(N) ascending-rank compaction with the same result
 //   mmadmm_mesh_hexdisc     a well-shaped disc mesh (not in the reference)
+//   mmadmm_mesh_shoulder    setUpShoulderExperiment's mesh (main.cpp:403-630): the rect mesh without
+//                           the simplices whose centroid lies in the upper (x, y[, z]) quadrant, its
+//                           boundary re-marking, and the interior vertices moved by up to h/10 in a
+//                           random direction -- glibc rand() (the caller seeds it; main.cpp:785 does
+//                           srand(69)) and Eigen 3.4's Random() (x + (y - x) rand() / RAND_MAX, in
+//                           [-1, 1], coefficient order); Eigen is un-vendored (its version unpinned)
 //   mmadmm_mesh_read        utils::readTriangles (src/MeshUtils.h:669-733)
 //   mmadmm_write_points / mmadmm_write_simplices: Mesh::outputPoints / outputSimplices
 //                           (src/Mesh.cpp:1067-1095), default ostream formatting (%.6g)
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -229,6 +236,69 @@ void hexdisc(int N, double r, double cx, double cy, int bType, MeshBuf& m) {
     }
 }
 
+void shoulder(int dim, int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za, double zb,
+              int bType, MeshBuf& m) {
+  if (dim == 2)
+    rect2d(nx, ny, (int)xa, (int)xb, (int)ya, (int)yb, bType, m);
+  else
+    rect3d(nx, ny, nz, (int)xa, (int)xb, (int)ya, (int)yb, (int)za, (int)zb, bType, m);
+  const int D = dim, V = D + 1;
+  const double cx = (xa + xb) / 2.0, cy = (ya + yb) / 2.0, cz = (za + zb) / 2.0;
+  const double EPS = 1e-16;
+  const std::vector<double>& X = m.Vp;  // Vc: not yet perturbed
+  std::vector<char> removed(m.nF(), 0);
+  for (int i = 0; i < m.nF(); i++) {
+    double x[4][3] = {{0}};
+    for (int n = 0; n < V; ++n)
+      for (int d = 0; d < D; ++d) x[n][d] = X[(size_t)m.F[(size_t)i * V + n] * D + d];
+    double c[3];
+    for (int d = 0; d < D; ++d)  // (1/3)(x0 + x1 + x2) / (1/4)(x0 + x1 + x2 + x3), Eigen order
+      c[d] = (D == 2) ? (1.0 / 3.0) * ((x[0][d] + x[1][d]) + x[2][d])
+                      : (1.0 / 4.0) * (((x[0][d] + x[1][d]) + x[2][d]) + x[3][d]);
+    const bool inQuad = (D == 2) ? (c[0] > cx && c[1] > cy) : (c[0] > cx && c[1] > cy && c[2] > cz);
+    if (!inQuad) continue;
+    removed[i] = 1;
+    for (int n = 0; n < V; ++n) {
+      const double* p = x[n];
+      bool fixed;
+      if (D == 2) {
+        fixed = (std::fabs(p[0] - cx) < EPS && std::fabs(p[1] - cy) < EPS) ||
+                (std::fabs(p[0] - cx) < EPS && std::fabs(p[1] - yb) < EPS) ||
+                (std::fabs(p[0] - xb) < EPS && std::fabs(p[1] - cy) < EPS);
+      } else {
+        fixed = (std::fabs(p[0] - cx) < EPS && std::fabs(p[2] - cz) < EPS) ||
+                (std::fabs(p[0] - cx) < EPS && std::fabs(p[2] - zb) < EPS) ||
+                (std::fabs(p[0] - xb) < EPS && std::fabs(p[2] - cz) < EPS) ||
+                (std::fabs(p[1] - ya) < EPS && std::fabs(p[2] - cz) < EPS) ||
+                (std::fabs(p[1] - yb) < EPS && std::fabs(p[2] - cz) < EPS) ||
+                (std::fabs(p[0] - cx) < EPS && std::fabs(p[1] - ya) < EPS) ||
+                (std::fabs(p[0] - cx) < EPS && std::fabs(p[1] - yb) < EPS);
+      }
+      m.mask[m.F[(size_t)i * V + n]] = fixed ? kFixed : bType;
+    }
+  }
+  // utils::removeRow in descending id order == keeping the others in order
+  std::vector<int32_t> F2;
+  F2.reserve(m.F.size());
+  for (int i = 0; i < m.nF(); ++i)
+    if (!removed[i]) F2.insert(F2.end(), m.F.begin() + (size_t)i * V, m.F.begin() + (size_t)(i + 1) * V);
+  m.F.swap(F2);
+  m.Vc = m.Vp;
+  const double hx = (xb - xa) / ((double)nx), hy = (yb - ya) / ((double)ny);
+  const double hz = (D == 3) ? (zb - za) / ((double)nz) : 0;
+  const double h = sqrt(hx * hx + hy * hy + hz * hz);
+  for (int i = 0; i < m.nP(); i++) {
+    if (m.mask[i] != kInterior) continue;
+    double dir[3], sq = 0.0;
+    for (int d = 0; d < D; ++d) dir[d] = -1.0 + (1.0 - (-1.0)) * (double)rand() / (double)RAND_MAX;
+    for (int d = 0; d < D; ++d) sq = (d == 0) ? dir[d] * dir[d] : sq + dir[d] * dir[d];
+    const double nrm = sqrt(sq);
+    for (int d = 0; d < D; ++d) dir[d] /= nrm;
+    const double r = (h / 10.0) * static_cast<double>(rand()) / static_cast<double>(RAND_MAX);
+    for (int d = 0; d < D; ++d) m.Vp[(size_t)i * D + d] += r * dir[d];
+  }
+}
+
 void readMesh(int dim, const char* tri, const char* pnts, const char* mask, MeshBuf& m) {
   m.dim = dim;
   std::string line, word;
@@ -286,6 +356,26 @@ int mmadmm_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, doub
     auto* m = new MeshBuf();
     mmx::levelset2d(nx, ny, xa, xb, ya, yb, btype, compact_mask != 0, *m);
     *out = reinterpret_cast<mmadmm_mesh>(m);
+  });
+}
+
+int mmadmm_mesh_shoulder(int dim, int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za,
+                         double zb, int btype, mmadmm_mesh* out) {
+  return guarded([&] {
+    if (!out || (dim != 2 && dim != 3) || nx < 1 || ny < 1 || (dim == 3 && nz < 1))
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_shoulder: bad arguments");
+    auto* m = new MeshBuf();
+    mmx::shoulder(dim, nx, ny, nz, xa, xb, ya, yb, za, zb, btype, *m);
+    *out = reinterpret_cast<mmadmm_mesh>(m);
+  });
+}
+
+int mmadmm_mesh_reference_points(mmadmm_mesh h, double* Xc) {
+  return guarded([&] {
+    auto* m = reinterpret_cast<MeshBuf*>(h);
+    if (!m || !Xc) throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_reference_points: null argument");
+    const std::vector<double>& src = m->Vc.empty() ? m->Vp : m->Vc;
+    std::copy(src.begin(), src.end(), Xc);
   });
 }
 

@@ -99,6 +99,9 @@ def lib():
         ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.mmadmm_mesh_hexdisc.argtypes = [ctypes.c_int] + [ctypes.c_double] * 3 + [ctypes.c_int,
                                                                                ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_mesh_shoulder.argtypes = [ctypes.c_int] * 4 + [ctypes.c_double] * 6 + [ctypes.c_int,
+                                                                                     ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_mesh_reference_points.argtypes = [ctypes.c_void_p, c_double_p]
     L.mmadmm_mesh_read.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                    ctypes.POINTER(ctypes.c_void_p)]
     L.mmadmm_mesh_sizes.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 4
@@ -169,8 +172,21 @@ class MeshData:
         F = np.zeros((nF.value, d.value + 1), dtype=np.int32)
         mask = np.zeros(ml.value, dtype=np.int32)
         _check(L.mmadmm_mesh_copy(h, _dp(Xp), _ip(F), _ip(mask)))
+        Xc = np.zeros_like(Xp)
+        _check(L.mmadmm_mesh_reference_points(h, _dp(Xc)))
         L.mmadmm_mesh_free(h)
-        return MeshData(d.value, Xp, F, mask)
+        m = MeshData(d.value, Xp, F, mask)
+        m.Xc = Xc  # reference positions (CompMesh): equal to Xp except for Shoulder meshes
+        return m
+
+    @staticmethod
+    def shoulder(dim, n, xa=0, xb=1, ya=0, yb=1, za=0, zb=1, btype=BOUNDARY_FIXED):
+        """setUpShoulderExperiment's mesh (main.cpp:403-630); draws from the C library's rand()
+        (seed with srand(69) for the reference's sequence, main.cpp:785)."""
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_mesh_shoulder(dim, n, n, n if dim == 3 else 0, xa, xb, ya, yb, za, zb, btype,
+                                          ctypes.byref(h)))
+        return MeshData._take(h)
 
     @staticmethod
     def rect(dim, n, xa=0, xb=1, ya=0, yb=1, za=0, zb=1, btype=BOUNDARY_FIXED):

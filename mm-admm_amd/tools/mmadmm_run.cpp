@@ -5,9 +5,9 @@
 // exactly as main.cpp's main/runAlgo (main.cpp:132-255, 633-907) do, on the MI355X engine through
 // the C-ABI of include/mmadmm.h.
 //
-// Supported: TestType FromFile, SquareGrid, LevelSet (2D); Method 0 (ADMM), 1 (explicit Euler)
-// and 2 (backward Euler: Newton + ILU(0) CG-STAB).  Shoulder (glibc rand + Eigen Random point
-// clouds) exits with a message.  Extra options: --root DIR (instead of the current directory), --device N,
+// Supported: TestType FromFile, SquareGrid, LevelSet (2D), Shoulder (glibc rand after srand(69) as
+// main.cpp:785, Eigen 3.4 Random semantics); Method 0 (ADMM), 1 (explicit Euler) and 2 (backward
+// Euler: Newton + ILU(0) CG-STAB).  3D LevelSet exits with a message.  Extra options: --root DIR (instead of the current directory), --device N,
 // --dry-run (parse and build the mesh on the host only; no GPU).
 #include <sys/stat.h>
 #include <time.h>
@@ -169,6 +169,7 @@ double now() {
 }  // namespace
 
 int main(int argc, char** argv) {
+  srand(69);  // main.cpp:785 (the Shoulder experiment's random perturbation)
   std::vector<std::string> pos;
   std::string root = ".";
   int device = 0;
@@ -213,6 +214,7 @@ int main(int argc, char** argv) {
     const int admmIter = cfg.integer("AdmmIter");
     const double dtTol = cfg.num("DtTol");
     const int nSteps = cfg.integer("nSteps");
+    bool shoulder = false;
     const double dt = cfg.num("dt"), tau = cfg.num("tau"), rho = cfg.num("rho");
     std::cout << "testName " << testName << " TestType " << testType << " Dim " << D << " Method " << methodType
               << std::endl;
@@ -236,6 +238,13 @@ int main(int argc, char** argv) {
       check(mmadmm_mesh_rect(D, nx, ny, nz, cfg.num("xa"), cfg.num("xb"), cfg.num("ya"), cfg.num("yb"), za, zb,
                              btype, &mesh),
             "generateUniformRectMesh");
+    } else if (testType == "Shoulder") {  // setUpShoulderExperiment (main.cpp:403-630)
+      const int nx = cfg.integer("nx"), ny = cfg.integer("ny"), nz = D == 3 ? cfg.integer("nz") : 0;
+      const double za = D == 3 ? cfg.num("za") : 0.0, zb = D == 3 ? cfg.num("zb") : 0.0;
+      check(mmadmm_mesh_shoulder(D, nx, ny, nz, cfg.num("xa"), cfg.num("xb"), cfg.num("ya"), cfg.num("yb"), za, zb,
+                                 btype, &mesh),
+            "setUpShoulderExperiment");
+      shoulder = true;
     } else if (testType == "LevelSet" && D == 2) {  // setUpLevelSetExperiment (main.cpp:258-402)
       check(mmadmm_mesh_levelset2d(cfg.integer("nx"), cfg.integer("ny"), cfg.num("xa"), cfg.num("xb"), cfg.num("ya"),
                                    cfg.num("yb"), btype, 0, &mesh),
@@ -250,6 +259,8 @@ int main(int argc, char** argv) {
     std::vector<double> Xp((size_t)nP * D);
     std::vector<int32_t> F((size_t)nF * (D + 1)), mask(maskLen);
     check(mmadmm_mesh_copy(mesh, Xp.data(), F.data(), mask.data()), "mesh copy");
+    std::vector<double> Xc(Xp);  // CompMesh reference: the initial Vp, or Shoulder's unmoved Vc
+    if (shoulder) check(mmadmm_mesh_reference_points(mesh, Xc.data()), "mesh reference points");
     mmadmm_mesh_free(mesh);
     std::cout << "size of Vp " << nP << ", " << D << std::endl;
     std::cout << "size of F " << nF << ", " << D + 1 << std::endl;
@@ -268,8 +279,8 @@ int main(int argc, char** argv) {
     p.rank = 0;
     p.nranks = 1;
     mmadmm_handle h = nullptr;
-    // CompMesh: Vc is a copy of the initial Vp in both set-ups (main.cpp:727, 778)
-    check(mmadmm_create(D, nP, Xp.data(), compMesh ? Xp.data() : nullptr, nF, F.data(), mask.data(), &p, fn, user,
+    // CompMesh: Vc is a copy of the initial Vp (main.cpp:727, 778) or Shoulder's unmoved mesh (main.cpp:479-491)
+    check(mmadmm_create(D, nP, Xp.data(), compMesh ? Xc.data() : nullptr, nF, F.data(), mask.data(), &p, fn, user,
                         &h),
           "Mesh/MeshIntegrator");
 
