@@ -61,9 +61,17 @@ def test_dry_run_from_file(tmp_path):
     assert "size of F 4015, 3" in r.stdout
 
 
-def test_unsupported_is_reported(tmp_path):
+def test_dry_run_shoulder(tmp_path):
+    """Shoulder (main.cpp:403-630): the 10x10 rect mesh without its upper-right quadrant."""
     cfg = dict(MONITOR210, TestType="Shoulder")
     r = _run(_root(tmp_path, "Sh", cfg), "Sh", "0", "1", "--dry-run")
+    assert r.returncode == 0, r.stderr
+    assert "size of Vp 221, 2" in r.stdout and "size of F 300, 3" in r.stdout
+
+
+def test_unsupported_is_reported(tmp_path):
+    cfg = dict(MONITOR210, TestType="LevelSet", Dim=3, nz=10, za=0, zb=1)
+    r = _run(_root(tmp_path, "Ls3", cfg), "Ls3", "0", "1", "--dry-run")
     assert r.returncode == 2 and "not available" in r.stderr
     r = _run(_root(tmp_path / "m3", "Monitor210", MONITOR210), "Monitor210", "3", "1", "--dry-run")
     assert r.returncode == 2 and "unknown Method" in r.stderr
