@@ -178,6 +178,21 @@ class Engine final : public EngineBase {
     interior_.upload(interior.data(), interior.size(), st_);
     incPtr_.upload(plan_.incPtr.data(), plan_.incPtr.size(), st_);
     incOff_.upload(plan_.incSrc.data(), plan_.incSrc.size(), st_);
+    {  // x-update order: nodes by their first incident (local) simplex, then id -- locality of the
+       // slot gathers when the node numbering is not simplex-ordered (e.g. cell centres numbered last)
+      std::vector<long long> key(nl);
+      for (int v = 0; v < nl; ++v) {
+        long long k = (long long)nF_;
+        for (int t = plan_.incPtr[v]; t < plan_.incPtr[v + 1]; ++t)
+          if (plan_.incSrc[t] >= 0) k = std::min<long long>(k, plan_.incSrc[t] / K);
+        key[v] = k;
+      }
+      std::vector<int32_t> ord(nl);
+      for (int v = 0; v < nl; ++v) ord[v] = v;
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key[a] < key[b]; });
+      nodeOrder_.upload(ord.data(), std::max<size_t>(ord.size(), 1), st_);
+      MMX_HIP(hipStreamSynchronize(st_));
+    }
     invdiag_.upload(invdiag.data(), invdiag.size(), st_);
     if (compMesh_) Vc_.upload(Vcl.data(), Vcl.size(), st_);
     gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
@@ -765,6 +780,7 @@ class Engine final : public EngineBase {
     m.gcache = gcache_.p;
     m.tieList = tieList_.p;
     m.tieCount = tieCount_.p;
+    m.nodeOrder = nodeOrder_.p;
     {
       const char* ft = getenv("MMX_FORCE_TIE");
       m.forceTie = ft ? atoi(ft) : 0;
@@ -844,7 +860,7 @@ class Engine final : public EngineBase {
   DevBuf<uint8_t> sbits_, interior_;
   DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_, gpad_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
-  DevBuf<int32_t> expOff_, tieList_;
+  DevBuf<int32_t> expOff_, tieList_, nodeOrder_;
   DevBuf<unsigned> tieCount_;
   PartitionPlan plan_;
   Comm* comm_ = nullptr;

@@ -24,6 +24,7 @@ struct DeviceMesh {
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
   int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
+  const int* nodeOrder;   // x-update processing order (nodes by first incident simplex) or nullptr
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)
   const double* Vc;       // nP x D reference positions (CompMesh) or nullptr
   // monitor grid

@@ -216,9 +216,11 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
                                                      double* __restrict__ partials, int xcd) {
   constexpr int CH = 8;
   const int lb = logical_block(xcd);
-  const int v = lb * kBlock + threadIdx.x;
+  const int idx = lb * kBlock + threadIdx.x;
   double pv[3] = {0, 0, 0};
-  if (v < m.nP) {
+  if (idx < m.nP) {
+    // processing order: nodes by first incident simplex, so a workgroup's nodes share simplices
+    const int v = m.nodeOrder ? m.nodeOrder[idx] : idx;
     double acc[D];
 #pragma unroll
     for (int c = 0; c < D; ++c) acc[c] = 0.0;
