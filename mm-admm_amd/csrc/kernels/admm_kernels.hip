@@ -693,10 +693,11 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   double* zs = zg + (size_t)s * K;
   double* us = ug + (size_t)s * K;
   double* gc = m.gcache + (size_t)s * (K + 1);
-  double z[K], dx[K], gcv[K + 1];
+  double z[K], z0[K], dx[K], gcv[K + 1];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     z[i] = zs[i];
+    z0[i] = z[i];  // the entry z, for ||z - zPrev||^2 (no reload at the end)
     dx[i] = us[i];
   }
   if (useCache) {
@@ -743,7 +744,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      const double d = z[i] - zs[i];
+      const double d = z[i] - z0[i];
       dual2 += d * d;
     }
 #if defined(MMX_EXP_NOGRAD) || defined(MMX_EXP_NOB)
