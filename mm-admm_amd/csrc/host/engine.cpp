@@ -232,6 +232,7 @@ class Engine final : public EngineBase {
     }
     // prox workgroups can be 64 lanes; node kernels pad their grid to a multiple of 8 (XCD map)
     const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 63) / 64, (nP_ + 255) / 256 + 8));
+    maxBlocks_ = maxBlocks;
     partA_.alloc(maxBlocks * kNumPartials);
     partB_.alloc(maxBlocks * kNumPartials);
     resultsCap_ = 0;
@@ -283,15 +284,22 @@ class Engine final : public EngineBase {
     const bool early = tol >= 0;
     int done = 0;
     double primal = 0, dual = 0;
+    // early exit off: every iteration's prox partials kept in their own slice and reduced in one
+    // launch after the loop (no reduction launch inside the loop)
+    const bool deferRed = !early && nIters <= kDeferMax;
+    const size_t slice = maxBlocks_ * kNumPartials;
+    if (deferRed && partA_.n < slice * nIters) partA_.alloc(slice * std::max(nIters, 10));
+    int firstDeferred = 0;  // first iteration of the batched reduction
     for (int i = 0; i < nIters; ++i) {
       hipEvent_t a0 = nullptr, a1 = nullptr, b1 = nullptr;
       if (timing) {
         a0 = nextEvent();
         MMX_HIP(hipEventRecord(a0, st_));
       }
+      const bool firstProx = !hessComputed_;          // another kernel, another partial count
       const bool swapB = (D == 3) && hessComputed_;  // 3D steady state: B_ -> B2_, then swap
       launch_prox<D>(m_, !hessComputed_, gcacheValid_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p,
-                     swapB ? B2_.p : B_.p, partA_.p, &nbp, st_);
+                     swapB ? B2_.p : B_.p, partA_.p + (deferRed ? slice * i : 0), &nbp, st_);
       if (swapB) std::swap(B_.p, B2_.p);
       gcacheValid_ = true;  // the prox's last blockGrad left the gradient at the final z
       if (timing) {
@@ -310,11 +318,21 @@ class Engine final : public EngineBase {
         MMX_HIP(hipEventRecord(b1, st_));
         timed_.push_back({a0, a1, b1});
       }
-      if (resid)
+      if (deferRed) {
+        if (firstProx && i < nIters - 1) {  // reduced at once: the batch below assumes one partial count
+          launch_reduce_partials(partA_.p + slice * i, nbp, results_.p + (size_t)i * 2 * kNumPartials, st_);
+          firstDeferred = i + 1;
+        } else if (i == nIters - 1) {
+          const int i0 = firstProx ? i : firstDeferred;
+          launch_reduce_steps(partA_.p + slice * i0, slice, nbp, partB_.p, nbx, nIters - i0,
+                              results_.p + (size_t)i0 * 2 * kNumPartials, st_);
+        }
+      } else if (resid) {
         launch_reduce_partials2(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, partB_.p, nbx,
                                 results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
-      else
+      } else {
         launch_reduce_partials(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, st_);
+      }
       done = i + 1;
       if (early) {
         std::vector<double> rv;
@@ -878,6 +896,8 @@ class Engine final : public EngineBase {
   DevBuf<int32_t> jia_, jja_;
   DevBuf<double> jval_, dv_, xn_, rhs_, dx_;
   int stepsTaken_ = 0;
+  size_t maxBlocks_ = 1;                 // partial-sum rows per launch (upper bound)
+  static constexpr int kDeferMax = 64;   // deferred reductions up to this many ADMM iterations
   bool timing_ = false;
   std::vector<hipEvent_t> evPool_;
   size_t evUsed_ = 0;

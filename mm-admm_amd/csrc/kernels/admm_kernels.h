@@ -73,6 +73,10 @@ template <int D>
 void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
                         hipStream_t st);
 void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st);
+// a step's reductions at once: results[i*2*kNumPartials ..] from partA slice i (i < n), the x-update's
+// set into the second half of row n-1
+void launch_reduce_steps(const double* partA, size_t stride, int nbA, const double* partB, int nbB, int n,
+                         double* results, hipStream_t st);
 // two reductions in one launch (one workgroup each)
 void launch_reduce_partials2(const double* partials, int nblocks, double* out, const double* partials2, int nblocks2,
                              double* out2, hipStream_t st);

@@ -1064,14 +1064,30 @@ __global__ void __launch_bounds__(kBlock) k_pack_export(int mode, int nExp, cons
 }
 
 constexpr int kRed = 1024;
+__device__ void reduce_set(const double* __restrict__ partials, int nblocks, double* __restrict__ out);
+
 __global__ void __launch_bounds__(kRed) k_reduce_partials(const double* __restrict__ partials, int nblocks,
                                                            double* __restrict__ out, const double* __restrict__ partials2,
                                                            int nblocks2, double* __restrict__ out2) {
-  if (blockIdx.x == 1) {  // second set in the same launch
-    partials = partials2;
-    nblocks = nblocks2;
-    out = out2;
-  }
+  if (blockIdx.x == 1)  // second set in the same launch
+    reduce_set(partials2, nblocks2, out2);
+  else
+    reduce_set(partials, nblocks, out);
+}
+
+// a whole step's reductions in one launch (early exit off): workgroup i < n reduces the prox
+// partials of iteration i (slices of `stride` doubles), workgroup n the last x-update's
+__global__ void __launch_bounds__(kRed) k_reduce_steps(const double* __restrict__ partA, size_t stride, int nbA,
+                                                        const double* __restrict__ partB, int nbB, int n,
+                                                        double* __restrict__ results) {
+  const int i = blockIdx.x;
+  if (i < n)
+    reduce_set(partA + (size_t)i * stride, nbA, results + (size_t)i * 2 * kNumPartials);
+  else
+    reduce_set(partB, nbB, results + (size_t)(n - 1) * 2 * kNumPartials + kNumPartials);
+}
+
+__device__ void reduce_set(const double* __restrict__ partials, int nblocks, double* __restrict__ out) {
   // one workgroup of 1024: lane-strided sums in a fixed order (four rows requested at a time),
   // then the wavefront butterflies and the 16 wavefront results in order -- a fixed shape
   __shared__ double red[kRed / 64][kNumPartials];
@@ -1280,6 +1296,10 @@ void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, dou
 }
 void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st) {
   hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kRed), 0, st, partials, nblocks, out, partials, nblocks, out);
+}
+void launch_reduce_steps(const double* partA, size_t stride, int nbA, const double* partB, int nbB, int n,
+                         double* results, hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce_steps, dim3(n + 1), dim3(kRed), 0, st, partA, stride, nbA, partB, nbB, n, results);
 }
 void launch_reduce_partials2(const double* partials, int nblocks, double* out, const double* partials2, int nblocks2,
                              double* out2, hipStream_t st) {
