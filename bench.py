@@ -526,6 +526,15 @@ def main():
         result["cpu_baseline"] = cpu_baseline(mesh, args.admm_iter, threads)
     for f in DEFERRED:  # the sections' CPU baselines, after every GPU measurement
         f()
+    # the GPU speed-up against the CPU path on all cores and on one (reported, not a target)
+    cb = result.get("cpu_baseline")
+    if cb and cb.get("value"):
+        cb["gpu_speedup"] = round(result["value"] / cb["value"], 1)
+        if cb.get("value_1thread"):
+            cb["gpu_speedup_1thread"] = round(result["value"] / cb["value_1thread"], 1)
+    c4r = result.get("c4_3d", {})
+    if c4r.get("cpu_baseline", {}).get("value"):
+        c4r["cpu_baseline"]["gpu_speedup"] = round(c4r["value"] / c4r["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
