@@ -184,3 +184,22 @@ def test_device_division_by_reciprocal_is_correctly_rounded(seed):
     out = mx.devmath(5, pairs)[:n]
     ref = x / c
     assert np.array_equal(out.view(np.int64), ref.view(np.int64))
+
+
+@pytest.mark.parametrize("dim,tol", [(2, -1.0), (2, 1e-3), (3, -1.0)])
+def test_long_run_bitwise(dim, tol):
+    """Many steps on a mid-size mesh: no drift between the device and the oracle.
+
+    tol < 0 runs the deferred-reduction path (one k_reduce_steps per step), tol > 0 the
+    per-iteration early-exit check (reference MeshIntegrator::step, early exit on
+    ||x - z|| / ||z - zPrev|| < tol). The meshes move by ~1e-2 over the run."""
+    if dim == 2:
+        mesh, mon, rho, nsteps = _hexdisc(40), 2, 100.0, 20
+    else:
+        mesh, mon, rho, nsteps = oracle_py.Mesh.rect(3, 10), 6, 2000.0, 8
+    O, G = make_pair(mesh, mon, 0.025, 0.5, rho, False, 1, 1)
+    for _ in range(nsteps):
+        O.step(5, tol)
+        G.step(5, tol)
+    np.testing.assert_array_equal(G.get("x"), O.get("x"))
+    np.testing.assert_array_equal(G.get("z"), O.get("z"))
