@@ -346,7 +346,7 @@ __device__ void invertK(double* A) {
 // called after each BFGS update (the global accessor then reads what it wrote).
 template <int K>
 struct RegB {
-  static constexpr bool kRowFence = false;
+  static constexpr bool kRowFence = false, kPipe = false;
   double* b;
   __device__ __forceinline__ double get(int i, int j) const { return b[i * K + j]; }
   __device__ __forceinline__ void set(int i, int j, double v) const { b[i * K + j] = v; }
@@ -357,7 +357,7 @@ struct RegB {
 // scheduler hoists all K*K reads and the kernel spills)
 template <int K, int STRIDE = kLdsStride>
 struct LdsB {
-  static constexpr bool kRowFence = true;
+  static constexpr bool kRowFence = true, kPipe = false;
   double* base;  // &lds[tid], entries strided by STRIDE
   __device__ __forceinline__ double get(int i, int j) const { return base[(i * K + j) * STRIDE]; }
   __device__ __forceinline__ void set(int i, int j, double v) const { base[(i * K + j) * STRIDE] = v; }
@@ -368,6 +368,9 @@ struct LdsB {
 // address-space-qualified pointers: they keep global (and LDS) accesses as global_/ds_ instructions
 // through the pointer laundering below (a plain pointer out of an asm operand becomes flat)
 typedef __attribute__((address_space(1))) double gdouble;
+#ifndef MMX_ROW_PIPE
+#define MMX_ROW_PIPE 1  // global Bkinv rows: request row i+1 before working on row i
+#endif
 typedef __attribute__((address_space(3))) double ldouble;
 
 // Global, wave-interleaved (entry ij of simplex s at ((s/64)*K*K + ij)*64 + s%64: a wavefront's
@@ -376,7 +379,7 @@ typedef __attribute__((address_space(3))) double ldouble;
 // so `rd` stays intact for an exact recomputation of the block.
 template <int K>
 struct WaveB {
-  static constexpr bool kRowFence = true;
+  static constexpr bool kRowFence = true, kPipe = MMX_ROW_PIPE;
   const gdouble* rd;
   gdouble* wr;
   __device__ __forceinline__ double get(int i, int j) const { return rd[(i * K + j) * 64]; }
@@ -393,7 +396,7 @@ struct WaveB {
 // indices are compile-time in the unrolled passes, so every get/set resolves to one of the two.
 template <int K, int RL>
 struct HybB {
-  static constexpr bool kRowFence = true;
+  static constexpr bool kRowFence = true, kPipe = false;
   const gdouble* rd;
   gdouble* wr;
   ldouble* lds;  // &ldsRows[lane], entries strided by 64
@@ -410,6 +413,24 @@ struct HybB {
   __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
 };
 
+// 3D with one wavefront per SIMD: the first H rows of the lane's Bkinv held in registers for the
+// whole prox (the VGPR budget of one wave per SIMD has room), the rest streamed as in WaveB --
+// passes 2 and 3 of each BFGS update then re-read only K - H rows from L2/HBM.
+template <int K, int H>
+struct HoldB {
+  static constexpr bool kRowFence = true, kPipe = MMX_ROW_PIPE;
+  const gdouble* rd;
+  gdouble* wr;
+  double hold[H * K];
+  __device__ __forceinline__ double get(int i, int j) const { return (i < H) ? hold[i * K + j] : rd[(i * K + j) * 64]; }
+  __device__ __forceinline__ void set(int i, int j, double v) {
+    if (i < H) hold[i * K + j] = v;
+    wr[(i * K + j) * 64] = v;
+  }
+  __device__ __forceinline__ void advance() { rd = wr; }
+  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
+};
+
 // index of Bkinv entry ij of simplex s: 2D simplex-major (the LDS kernel's chunks), 3D
 // wave-interleaved (WaveB)
 template <int D>
@@ -422,6 +443,23 @@ __device__ __forceinline__ size_t bidx(int s, int ij) {
 #define MMX_ROW_FENCE(BA) \
   if constexpr (BA::kRowFence) __builtin_amdgcn_sched_barrier(0)
 
+template <int K, class BA>
+__device__ __forceinline__ void load_row(const BA& B, int i, double (&r)[K]) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) r[j] = B.get(i, j);
+}
+// row i of a pass: PIPE takes it from rn (requested one row earlier) and requests row i+1 into rn
+template <int K, bool PIPE, class BA>
+__device__ __forceinline__ void next_row(const BA& B, int i, double (&row)[K], double (&rn)[K]) {
+  if constexpr (PIPE) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) row[j] = rn[j];
+    if (i + 1 < K) load_row<K>(B, i + 1, rn);
+  } else {
+    load_row<K>(B, i, row);
+  }
+}
+
 // Mesh<D>::bfgsOptSimplex iteration loop (src/Mesh.cpp:827-856): inverse-BFGS without line
 // search, <= 50 iterations, stop when ||grad||_1 < tol.  Returns the iteration count.
 // EXACT = false: the fast path; a power near a rounding midpoint raises *tie (the caller then
@@ -432,16 +470,21 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
                                                unsigned fixedBits, double tol, bool& bad, double* gcache,
                                                bool* tie = nullptr) {
   constexpr int K = D * (D + 1);
+  constexpr bool kPipe = BA::kPipe;
   int iter;
   for (iter = 0; iter < 50; iter++) {
     B.fresh();
     double pk[K];
+    double rn[K];  // kPipe: row i+1 is requested before row i is used (latency under the row's work)
+    if constexpr (kPipe) load_row<K>(B, 0, rn);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
-      double sacc = (-B.get(i, 0)) * G[0];
+      double row[K];
+      next_row<K, kPipe>(B, i, row, rn);
+      double sacc = (-row[0]) * G[0];
 #pragma unroll
-      for (int j = 1; j < K; ++j) sacc += (-B.get(i, j)) * G[j];
+      for (int j = 1; j < K; ++j) sacc += (-row[j]) * G[j];
       pk[i] = sacc;
     }
     MMX_ROW_FENCE(BA);
@@ -473,12 +516,12 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.fresh();
     // one pass over B: By_i = sum_j B_ij y_j, yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij
     double yBy = 0.0, yB[K];
+    if constexpr (kPipe) load_row<K>(B, 0, rn);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
       double row[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j) row[j] = B.get(i, j);
+      next_row<K, kPipe>(B, i, row, rn);
       double by = row[0] * yk[0];
 #pragma unroll
       for (int j = 1; j < K; ++j) by += row[j] * yk[j];
@@ -493,12 +536,12 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
 #endif
     B.fresh();
     // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
+    if constexpr (kPipe) load_row<K>(B, 0, rn);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
       double row[K], nrow[K], ykr[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j) row[j] = B.get(i, j);
+      next_row<K, kPipe>(B, i, row, rn);
       // 3D: (y p^T)_qj is formed again for every row -- laundering y per row stops the compiler
       // from keeping all K*K = 144 products live across the rows (they spilled); 2D keeps its 36
 #pragma unroll
@@ -803,6 +846,10 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
 #define MMX_HYB_RL 0
 #endif
   constexpr int RL = MMX_HYB_RL;  // Bkinv rows held in LDS for the whole prox (0: all streamed)
+#ifndef MMX_HOLD_RL
+#define MMX_HOLD_RL 4  // measured (C4, MonType 6): 2 -2.3%, 3 -1.8%, 4 -4.0%, 5 +22%, 6 +19% (prox time)
+#endif
+  constexpr int HL = MMX_HOLD_RL;  // Bkinv rows held in registers for the whole prox (HoldB)
   __shared__ double ldsRows[(RL > 0 ? RL : 1) * K * 64];
   const int tid = threadIdx.x;
   const int s0 = blockIdx.x * 64;
@@ -851,6 +898,14 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
       HybB<K, RL> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsRows + tid)};
       its = tie ? 0
                 : bfgs_iterations<D, HybB<K, RL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+    } else if constexpr (HL > 0) {
+      HoldB<K, HL> Bacc;
+      Bacc.rd = (const gdouble*)(Bin + gb);
+      Bacc.wr = (gdouble*)(Bout + gb);
+#pragma unroll
+      for (int e = 0; e < HL * K; ++e) Bacc.hold[e] = Bin[gb + (size_t)e * 64];
+      its = tie ? 0
+                : bfgs_iterations<D, HoldB<K, HL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     } else {
       WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb)};
       its = tie ? 0
