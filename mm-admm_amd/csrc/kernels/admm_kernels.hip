@@ -346,7 +346,8 @@ __device__ void invertK(double* A) {
 // called after each BFGS update (the global accessor then reads what it wrote).
 template <int K>
 struct RegB {
-  static constexpr bool kRowFence = false, kPipe = false;
+  static constexpr bool kRowFence = false;
+  static constexpr int kPipe = 0;
   double* b;
   __device__ __forceinline__ double get(int i, int j) const { return b[i * K + j]; }
   __device__ __forceinline__ void set(int i, int j, double v) const { b[i * K + j] = v; }
@@ -357,7 +358,8 @@ struct RegB {
 // scheduler hoists all K*K reads and the kernel spills)
 template <int K, int STRIDE = kLdsStride>
 struct LdsB {
-  static constexpr bool kRowFence = true, kPipe = false;
+  static constexpr bool kRowFence = true;
+  static constexpr int kPipe = 0;
   double* base;  // &lds[tid], entries strided by STRIDE
   __device__ __forceinline__ double get(int i, int j) const { return base[(i * K + j) * STRIDE]; }
   __device__ __forceinline__ void set(int i, int j, double v) const { base[(i * K + j) * STRIDE] = v; }
@@ -369,7 +371,7 @@ struct LdsB {
 // through the pointer laundering below (a plain pointer out of an asm operand becomes flat)
 typedef __attribute__((address_space(1))) double gdouble;
 #ifndef MMX_ROW_PIPE
-#define MMX_ROW_PIPE 1  // global Bkinv rows: request row i+1 before working on row i
+#define MMX_ROW_PIPE 2  // global Bkinv rows: request row i+2 before working on row i (C4: 1 -> 2 rows -1.6%, 3 spills)
 #endif
 typedef __attribute__((address_space(3))) double ldouble;
 
@@ -379,7 +381,8 @@ typedef __attribute__((address_space(3))) double ldouble;
 // so `rd` stays intact for an exact recomputation of the block.
 template <int K>
 struct WaveB {
-  static constexpr bool kRowFence = true, kPipe = MMX_ROW_PIPE;
+  static constexpr bool kRowFence = true;
+  static constexpr int kPipe = MMX_ROW_PIPE;
   const gdouble* rd;
   gdouble* wr;
   __device__ __forceinline__ double get(int i, int j) const { return rd[(i * K + j) * 64]; }
@@ -396,7 +399,8 @@ struct WaveB {
 // indices are compile-time in the unrolled passes, so every get/set resolves to one of the two.
 template <int K, int RL>
 struct HybB {
-  static constexpr bool kRowFence = true, kPipe = false;
+  static constexpr bool kRowFence = true;
+  static constexpr int kPipe = 0;
   const gdouble* rd;
   gdouble* wr;
   ldouble* lds;  // &ldsRows[lane], entries strided by 64
@@ -416,15 +420,20 @@ struct HybB {
 // 3D with one wavefront per SIMD: the first H rows of the lane's Bkinv held in registers for the
 // whole prox (the VGPR budget of one wave per SIMD has room), the rest streamed as in WaveB --
 // passes 2 and 3 of each BFGS update then re-read only K - H rows from L2/HBM.
-template <int K, int H>
+template <int K, int H, int L = 0>
 struct HoldB {
-  static constexpr bool kRowFence = true, kPipe = MMX_ROW_PIPE;
+  static constexpr bool kRowFence = true;
+  static constexpr int kPipe = MMX_ROW_PIPE;
   const gdouble* rd;
   gdouble* wr;
+  ldouble* lds;  // rows H..H+L-1: &ldsRows[lane], entries strided by 64
   double hold[H * K];
-  __device__ __forceinline__ double get(int i, int j) const { return (i < H) ? hold[i * K + j] : rd[(i * K + j) * 64]; }
+  __device__ __forceinline__ double get(int i, int j) const {
+    return (i < H) ? hold[i * K + j] : (i < H + L) ? lds[((i - H) * K + j) * 64] : rd[(i * K + j) * 64];
+  }
   __device__ __forceinline__ void set(int i, int j, double v) {
     if (i < H) hold[i * K + j] = v;
+    else if (i < H + L) lds[((i - H) * K + j) * 64] = v;
     wr[(i * K + j) * 64] = v;
   }
   __device__ __forceinline__ void advance() { rd = wr; }
@@ -448,16 +457,27 @@ __device__ __forceinline__ void load_row(const BA& B, int i, double (&r)[K]) {
 #pragma unroll
   for (int j = 0; j < K; ++j) r[j] = B.get(i, j);
 }
-// row i of a pass: PIPE takes it from rn (requested one row earlier) and requests row i+1 into rn
-template <int K, bool PIPE, class BA>
-__device__ __forceinline__ void next_row(const BA& B, int i, double (&row)[K], double (&rn)[K]) {
-  if constexpr (PIPE) {
+// row i of a pass: PIPE > 0 takes it from rn[0] (requested PIPE rows earlier), shifts the queue and
+// requests row i+PIPE
+template <int K, int PIPE, class BA>
+__device__ __forceinline__ void next_row(const BA& B, int i, double (&row)[K], double (&rn)[PIPE > 0 ? PIPE : 1][K]) {
+  if constexpr (PIPE > 0) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) row[j] = rn[j];
-    if (i + 1 < K) load_row<K>(B, i + 1, rn);
+    for (int j = 0; j < K; ++j) row[j] = rn[0][j];
+#pragma unroll
+    for (int d = 0; d + 1 < PIPE; ++d)
+#pragma unroll
+      for (int j = 0; j < K; ++j) rn[d][j] = rn[d + 1][j];
+    if (i + PIPE < K) load_row<K>(B, i + PIPE, rn[PIPE - 1]);
   } else {
     load_row<K>(B, i, row);
   }
+}
+// the first PIPE rows of a pass
+template <int K, int PIPE, class BA>
+__device__ __forceinline__ void start_rows(const BA& B, double (&rn)[PIPE > 0 ? PIPE : 1][K]) {
+#pragma unroll
+  for (int d = 0; d < PIPE; ++d) load_row<K>(B, d, rn[d]);
 }
 
 // Mesh<D>::bfgsOptSimplex iteration loop (src/Mesh.cpp:827-856): inverse-BFGS without line
@@ -470,13 +490,13 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
                                                unsigned fixedBits, double tol, bool& bad, double* gcache,
                                                bool* tie = nullptr) {
   constexpr int K = D * (D + 1);
-  constexpr bool kPipe = BA::kPipe;
+  constexpr int kPipe = BA::kPipe;
   int iter;
   for (iter = 0; iter < 50; iter++) {
     B.fresh();
     double pk[K];
-    double rn[K];  // kPipe: row i+1 is requested before row i is used (latency under the row's work)
-    if constexpr (kPipe) load_row<K>(B, 0, rn);
+    double rn[kPipe > 0 ? kPipe : 1][K];  // kPipe rows requested ahead of the row being worked on
+    start_rows<K, kPipe>(B, rn);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
@@ -516,7 +536,7 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.fresh();
     // one pass over B: By_i = sum_j B_ij y_j, yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij
     double yBy = 0.0, yB[K];
-    if constexpr (kPipe) load_row<K>(B, 0, rn);
+    start_rows<K, kPipe>(B, rn);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
@@ -536,7 +556,7 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
 #endif
     B.fresh();
     // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
-    if constexpr (kPipe) load_row<K>(B, 0, rn);
+    start_rows<K, kPipe>(B, rn);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
@@ -850,6 +870,11 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
 #define MMX_HOLD_RL 4  // measured (C4, MonType 6): 2 -2.3%, 3 -1.8%, 4 -4.0%, 5 +22%, 6 +19% (prox time)
 #endif
   constexpr int HL = MMX_HOLD_RL;  // Bkinv rows held in registers for the whole prox (HoldB)
+#ifndef MMX_HOLD_LDS
+#define MMX_HOLD_LDS 0  // measured: 2, 4 or 6 more rows in LDS change the C4 prox by < 1%: not traffic-bound any more
+#endif
+  constexpr int LL = MMX_HOLD_LDS;  // the next LL rows held in LDS (HoldB)
+  __shared__ double ldsHold[(LL > 0 ? LL : 1) * K * 64];
   __shared__ double ldsRows[(RL > 0 ? RL : 1) * K * 64];
   const int tid = threadIdx.x;
   const int s0 = blockIdx.x * 64;
@@ -899,13 +924,16 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
       its = tie ? 0
                 : bfgs_iterations<D, HybB<K, RL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     } else if constexpr (HL > 0) {
-      HoldB<K, HL> Bacc;
+      HoldB<K, HL, LL> Bacc;
       Bacc.rd = (const gdouble*)(Bin + gb);
       Bacc.wr = (gdouble*)(Bout + gb);
+      Bacc.lds = (ldouble*)(ldsHold + tid);
 #pragma unroll
       for (int e = 0; e < HL * K; ++e) Bacc.hold[e] = Bin[gb + (size_t)e * 64];
+#pragma unroll 4
+      for (int e = 0; e < LL * K; ++e) ldsHold[e * 64 + tid] = Bin[gb + (size_t)(HL * K + e) * 64];
       its = tie ? 0
-                : bfgs_iterations<D, HoldB<K, HL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+                : bfgs_iterations<D, HoldB<K, HL, LL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     } else {
       WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb)};
       its = tie ? 0
