@@ -127,3 +127,19 @@ def test_partitioned_regrid_equals_single(mx, mon, dim, nranks):
     for e in parts:
         e.close()
     comm.close()
+
+
+def test_rccl_communicator_single_rank(mx):
+    """The RCCL communicator bench.py uses for N > 1 (ncclGetUniqueId, ncclCommInitRank,
+    ncclAllGather on the engine's stream), driven at one rank: the partitioned engine over it
+    equals the plain engine bit for bit. Ranks on several GPUs are left to the multi-GPU run."""
+    mesh = mx.MeshData.rect(2, 12)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 3), rho=1000.0, tau=0.5, device=0)
+    ref = mx.Engine(M, 0.025)
+    comm = mx.Comm.rccl(1, 0, mx.Comm.unique_id(), 0)
+    part = mx.Engine(M, 0.025, rank=0, nranks=1, comm=comm)
+    for _ in range(3):
+        ref.step(5, -1.0)
+        part.step(5, -1.0)
+    ids = part.local_nodes()
+    assert np.array_equal(part.get("x").reshape(-1, 2), ref.get("x").reshape(-1, 2)[ids])
