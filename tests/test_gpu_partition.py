@@ -143,3 +143,29 @@ def test_rccl_communicator_single_rank(mx):
         part.step(5, -1.0)
     ids = part.local_nodes()
     assert np.array_equal(part.get("x").reshape(-1, 2), ref.get("x").reshape(-1, 2)[ids])
+
+
+def test_partitioned_early_exit_equals_single(mx):
+    """Early exit (tol > 0) on a partition: the residual norms are summed over ranks, so every rank
+    stops at the same iteration as the single-GPU engine (bench.py's early-exit run at N > 1)."""
+    mesh = mx.MeshData.hexdisc(10, 0.5, 0.5, 0.5)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5, device=0)
+    ref = mx.Engine(M, 0.055)
+    nranks = 2
+    comm = mx.Comm.loopback(nranks)
+    parts = [mx.Engine(M, 0.055, rank=r, nranks=nranks, comm=comm) for r in range(nranks)]
+    for _ in range(3):
+        ref.step(10, 1e-3)
+
+    def run(r):
+        def f():
+            for _ in range(3):
+                parts[r].step(10, 1e-3)
+        return f
+
+    _run_parallel([run(r) for r in range(nranks)])
+    xr = ref.get("x").reshape(-1, 2)
+    n_ref = ref.stats()["n_prox"]
+    for e in parts:
+        assert np.array_equal(e.get("x").reshape(-1, 2), xr[e.local_nodes()])
+        assert e.stats()["n_prox"] == n_ref
