@@ -38,8 +38,8 @@ DEFERRED = []
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--admm-iter", type=int, default=10)
     ap.add_argument("--disc-n", type=int, default=577)
     ap.add_argument("--no-cpu-baseline", action="store_true")
