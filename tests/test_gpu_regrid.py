@@ -55,3 +55,17 @@ def test_regrid_at_setup_positions_equals_host_setup(dim, maker):
         G.regrid(0.0)
         np.testing.assert_array_equal(G.get("grid"), host)
         G.close()
+
+
+@pytest.mark.parametrize("dim,n,nsteps", [(2, 40, 20), (3, 8, 10)])
+def test_regrid_long_run_bitwise(dim, n, nsteps):
+    """The moving bump (MonType 7) over a full revolution (t = 0 .. 1 at dt 0.05 in 2D): grid and
+    positions stay identical to the oracle across every device regrid."""
+    mesh = oracle_py.Mesh.rect(dim, n)
+    O, G = pair(mesh, 7, 0.05, 0.5, 200.0)
+    for _ in range(nsteps):
+        O.step(5, -1.0)
+        G.step(5, -1.0)
+    np.testing.assert_array_equal(G.get("grid"), O.get("grid"))
+    np.testing.assert_array_equal(G.get("x"), O.get("x"))
+    assert G.stats()["regrids"] == nsteps
