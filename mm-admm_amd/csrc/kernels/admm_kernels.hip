@@ -60,6 +60,12 @@ __device__ __forceinline__ int logical_block(int xcd) {
   return xcd ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
 }
 
+// any grid size: XCD x (= blockIdx % 8) takes a contiguous range of q or q + 1 logical blocks
+__device__ __forceinline__ int logical_block_any() {
+  const int g = (int)gridDim.x, q = g / 8, r = g % 8, x = (int)(blockIdx.x % 8);
+  return x * q + min(x, r) + (int)(blockIdx.x / 8);
+}
+
 template <int D>
 __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   GridView<D> g;
@@ -745,7 +751,11 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   constexpr int K = D * (D + 1), KK = K * K;
   __shared__ __attribute__((aligned(16))) double lds[KK * (BS + 1)];
   const int tid = threadIdx.x;
-  const int s0 = blockIdx.x * BS;
+#ifndef MMX_LDS_XCD
+#define MMX_LDS_XCD 0  // measured C3: no gain (2D blocks already share lines within one workgroup)
+#endif
+  const int lb = MMX_LDS_XCD ? logical_block_any() : (int)blockIdx.x;
+  const int s0 = lb * BS;
   const int nIn = min(BS, m.nF - s0);
   const bool act = tid < nIn;
   const int s = act ? s0 + tid : s0;  // inactive lanes shadow the first simplex, store nothing
@@ -819,9 +829,9 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     pv[4] = bad ? 1.0 : 0.0;
     pv[5] = (double)its;
   }
-  if (m.forceTie > 0 && tid == 0 && (int)(blockIdx.x % (unsigned)m.forceTie) == 0) tie = true;
+  if (m.forceTie > 0 && tid == 0 && (int)((unsigned)lb % (unsigned)m.forceTie) == 0) tie = true;
   if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to k_prox_fix
-    if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = (int)blockIdx.x;
+    if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = lb;
     return;
   }
   if (act) {
@@ -844,7 +854,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     if (v.x == 12345.0) chunk[e] = v.y;  // keep the LDS reads alive
 #endif
   }
-  block_partials<6, BS>(pv, partials);
+  block_partials<6, BS>(pv, partials, lb);
 }
 
 // Steady-state 3D prox: one wavefront per workgroup, one lane per tetrahedron, Bkinv (144
@@ -877,7 +887,11 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
   __shared__ double ldsHold[(LL > 0 ? LL : 1) * K * 64];
   __shared__ double ldsRows[(RL > 0 ? RL : 1) * K * 64];
   const int tid = threadIdx.x;
-  const int s0 = blockIdx.x * 64;
+#ifndef MMX_WAVE_XCD
+#define MMX_WAVE_XCD 1  // measured C4: prox 3.42 -> 3.29 ms (neighbouring tets share x and monitor-grid lines in one L2)
+#endif
+  const int lb = MMX_WAVE_XCD ? logical_block_any() : (int)blockIdx.x;  // XCD-contiguous tet ranges
+  const int s0 = lb * 64;
   const bool act = s0 + tid < m.nF;
   const int s = act ? s0 + tid : s0;
   int f[D + 1];
@@ -915,7 +929,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     entry_grad<D, false>(g, fc, z, xi, dx, gcv, useCache != 0, G, Igt, bad, &tie);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
-    const size_t gb = (size_t)blockIdx.x * KK * 64 + tid;
+    const size_t gb = (size_t)lb * KK * 64 + tid;
     int its;
     if constexpr (RL > 0) {
 #pragma unroll 8
@@ -954,9 +968,9 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     pv[4] = bad ? 1.0 : 0.0;
     pv[5] = (double)its;
   }
-  if (m.forceTie > 0 && tid == 0 && (int)(blockIdx.x % (unsigned)m.forceTie) == 0) tie = true;
+  if (m.forceTie > 0 && tid == 0 && (int)((unsigned)lb % (unsigned)m.forceTie) == 0) tie = true;
   if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to k_prox_fix
-    if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = (int)blockIdx.x;
+    if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = lb;
     return;
   }
   if (act) {
@@ -966,7 +980,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
       us[i] = dx[i] - z[i];  // uBar = DXpU - z
     }
   }
-  block_partials<6, 64>(pv, partials);
+  block_partials<6, 64>(pv, partials, lb);
 }
 
 // Mesh::computeEnergy (src/Mesh.cpp:496-530) on positions x
