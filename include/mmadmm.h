@@ -96,8 +96,8 @@ typedef struct mmadmm_stats {
  * mmadmm_regrid rebuilds the smoothed monitor grid on the device from the current mesh positions,
  * the monitor evaluated at time t (built-in MonType 7 on the device; any other monitor through its
  * host callback at the current vertices); bit-identical to the host set-up.  mmadmm_set_regrid(h, 1)
- * does that at the start of every mmadmm_step with t = steps taken * dt.  Single-rank engines only
- * (MMADMM_ERR_INVALID on a partition: the grid needs every vertex). */
+ * does that at the start of every mmadmm_step with t = steps taken * dt.  On an element partition
+ * every rank all-gathers the positions of the vertices it owns and rebuilds the same global grid. */
 int mmadmm_regrid(mmadmm_handle h, double t);
 int mmadmm_set_regrid(mmadmm_handle h, int every_step);
 
@@ -111,6 +111,16 @@ int mmadmm_version(void);
  * lam1 = 1 + sech(50 (|x - c| - 0.3)^2), 1/lam1 across n; MEx2.h's construction around a
  * sphere) with no reference counterpart (BASELINE config 4) */
 int mmadmm_builtin_monitor(int dim, int mon_type, mmadmm_monitor_fn* fn, void** user);
+/* The smoothed monitor grid the set-up builds from the positions Xp (nP x dim) and the monitor
+ * (MeshInterpolator<D>::updateMesh + interpolateMonitor, src/MeshInterpolator.cpp:68-130, 166-259,
+ * 366-404): host only, no device needed.  *rows = grid rows; vals (rows x dim*dim, row-major
+ * tensors) is filled unless NULL. */
+int mmadmm_monitor_grid(int dim, int nP, const double* Xp, mmadmm_monitor_fn fn, void* user, int* rows,
+                        double* vals);
+
+/* Mesh::reOrientElements (src/Mesh.cpp:243-260) alone, in place on F (host only): the ordering
+ * mmadmm_create applies and mmadmm_get_simplices returns. */
+int mmadmm_mesh_reorient(int dim, int nP, const double* Xp, int nF, int32_t* F);
 
 /* Mesh<D> + MeshIntegrator<D>.  Xp: nP x dim row-major; Xc: reference positions (CompMesh)
  * or NULL; F: nF x (dim+1); mask: nP node types.  F is re-oriented (src/Mesh.cpp:243-260)

@@ -56,6 +56,27 @@ struct EngineBase {
   virtual void debugBlockGrad(int s, const double* z, const double* dx, int flags, double* out) = 0;
 };
 
+// Mesh::reOrientElements (src/Mesh.cpp:243-260): swap F(i,1), F(i,2) when det(E) < 0, E the
+// edge vectors from vertex 0 as columns, Eigen's 2x2 / 3x3 determinant
+void reorient_simplices(int D, const double* Vp, int nF, int32_t* F) {
+  for (int s = 0; s < nF; ++s) {
+    double E[3][3] = {{0}};
+    const int32_t* f = F + (size_t)s * (D + 1);
+    for (int j = 0; j < D; ++j)
+      for (int r = 0; r < D; ++r) E[r][j] = Vp[(size_t)f[j + 1] * D + r] - Vp[(size_t)f[0] * D + r];
+    double det;
+    if (D == 2) {
+      det = E[0][0] * E[1][1] - E[1][0] * E[0][1];
+    } else {
+      const double h0 = E[0][0] * (E[1][1] * E[2][2] - E[1][2] * E[2][1]);
+      const double h1 = E[0][1] * (E[1][0] * E[2][2] - E[1][2] * E[2][0]);
+      const double h2 = E[0][2] * (E[1][0] * E[2][1] - E[1][1] * E[2][0]);
+      det = h0 - h1 + h2;
+    }
+    if (det < 0) std::swap(F[(size_t)s * (D + 1) + 1], F[(size_t)s * (D + 1) + 2]);
+  }
+}
+
 template <int D>
 class Engine final : public EngineBase {
  public:
@@ -77,14 +98,7 @@ class Engine final : public EngineBase {
     for (int i = 0; i < nF * (D + 1); ++i)
       if (Fh_[i] < 0 || Fh_[i] >= nP) throw Error(MMADMM_ERR_INVALID, "simplex vertex id out of range");
     maskH_.assign(mask, mask + nP);
-    // Mesh::reOrientElements (src/Mesh.cpp:243-260): swap F(i,1), F(i,2) when det(E) < 0
-    for (int s = 0; s < nF; ++s) {
-      double E[3][3];
-      for (int j = 0; j < D; ++j)
-        for (int r = 0; r < D; ++r)
-          E[r][j] = Vp[(size_t)Fh_[(size_t)s * (D + 1) + j + 1] * D + r] - Vp[(size_t)Fh_[(size_t)s * (D + 1)] * D + r];
-      if (hostDet(E) < 0) std::swap(Fh_[(size_t)s * (D + 1) + 1], Fh_[(size_t)s * (D + 1) + 2]);
-    }
+    reorient_simplices(D, Vp.data(), nF, Fh_.data());
     // monitor grid (MeshInterpolator set-up), once per run on the initial vertices
     build_monitor_grid(D, Vp.data(), nP, fn, user, grid_);
     monFn_ = fn;
@@ -224,10 +238,9 @@ class Engine final : public EngineBase {
       // hessInvs = I (src/Mesh.cpp:456-464).  2D: simplex-major; 3D: wave-interleaved and
       // double-buffered (k_prox_wave), padded to whole groups of 64 simplices
       const size_t nB = (D == 2) ? (size_t)nF_ * K * K : (size_t)((nF_ + 63) / 64) * 64 * K * K;
-      std::vector<double> eye(nB, 0.0);
-      for (int s = 0; s < nF_; ++s)
-        for (int i = 0; i < K; ++i) eye[bIndex(s, i * K + i)] = 1.0;
-      B_.upload(eye.data(), eye.size(), st_);
+      B_.alloc(nB);
+      MMX_HIP(hipMemsetAsync(B_.p, 0, nB * sizeof(double), st_));
+      launch_bkinv_identity<D>(nF_, B_.p, st_);
       if (D == 3) B2_.alloc(nB);
     }
     // prox workgroups can be 64 lanes; node kernels pad their grid to a multiple of 8 (XCD map)
@@ -340,8 +353,9 @@ class Engine final : public EngineBase {
         const double* r = rv.data();
         primal = sqrt(r[kNumPartials + 2]);
         dual = sqrt(r[1]);
-        if (r[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element in prox (reference: assert(Edet > 0))");
-        if (primal < tol && dual < tol) break;
+        // an inverted element ends the loop; it is reported below, after the step's bookkeeping
+        // (Vp, timers, counters), exactly like one found without the early exit
+        if (r[4] > 0 || (primal < tol && dual < tol)) break;
       }
     }
     // Mesh::updateAfterStep: Vp = x
@@ -924,6 +938,16 @@ extern "C" {
 
 const char* mmadmm_last_error(void) { return mmx::g_last_error.c_str(); }
 int mmadmm_version(void) { return 100; }
+
+int mmadmm_mesh_reorient(int dim, int nP, const double* Xp, int nF, int32_t* F) {
+  return guarded([&] {
+    if ((dim != 2 && dim != 3) || nP < 1 || nF < 0 || !Xp || (nF > 0 && !F))
+      throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_reorient: bad arguments");
+    for (long long i = 0; i < (long long)nF * (dim + 1); ++i)
+      if (F[i] < 0 || F[i] >= nP) throw Error(MMADMM_ERR_INVALID, "simplex vertex id out of range");
+    mmx::reorient_simplices(dim, Xp, nF, F);
+  });
+}
 
 int mmadmm_create(int dim, int nP, const double* Xp, const double* Xc, int nF, const int32_t* F, const int32_t* mask,
                   const mmadmm_params* p, mmadmm_monitor_fn fn, void* user, mmadmm_handle* out) {

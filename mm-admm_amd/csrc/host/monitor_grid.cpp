@@ -210,3 +210,15 @@ void build_monitor_grid(int dim, const double* X, int nP, mmadmm_monitor_fn fn, 
 }
 
 }  // namespace mmx
+
+extern "C" int mmadmm_monitor_grid(int dim, int nP, const double* Xp, mmadmm_monitor_fn fn, void* user, int* rows,
+                                   double* vals) {
+  return mmx::guarded([&] {
+    if ((dim != 2 && dim != 3) || nP < 1 || !Xp || !fn || !rows)
+      throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_monitor_grid: bad arguments");
+    mmx::HostGrid g;
+    mmx::build_monitor_grid(dim, Xp, nP, fn, user, g);
+    *rows = (int)(g.vals.size() / ((size_t)dim * dim));
+    if (vals) std::copy(g.vals.begin(), g.vals.end(), vals);
+  });
+}

@@ -158,10 +158,6 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     mv.m[1][0] = c0 * a1.x + c1 * b1.x + c2 * e1.x + c3 * f1.x;
     mv.m[1][1] = c0 * a1.y + c1 * b1.y + c2 * e1.y + c3 * f1.y;
   } else {
-#ifdef MMX_EXP_NOMON  // timing experiment: no grid gathers (numerics meaningless)
-    for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = (n % 4 == 0) ? 1.0 + 1e-3 * pnt[n / 3] : 0.0;
-    return;
-#endif
     const int zInd = findLimInf(pnt[2], g.az, g.nz + 1, g.hz, g.rhz);
     const double x0 = g.gx[xInd], x1 = g.gx[xInd + 1];
     const double y0 = g.gy[yInd], y1 = g.gy[yInd + 1];

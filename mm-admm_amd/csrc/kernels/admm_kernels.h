@@ -62,6 +62,9 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
 // gradient in m.gcache; the entry blockGrad then reduces to adding the regulariser.
 // 3D: pad[r 10 + n] = vals[r 9 + n], pad[r 10 + 9] = 0 (rebuilt whenever vals changes)
 void launch_pad_rows(const double* vals, long long rows, double* pad, hipStream_t st);
+// diagonal entries of the identity Bkinv of nF simplices in the bidx<D> layout (buffer zeroed before)
+template <int D>
+void launch_bkinv_identity(int nF, double* B, hipStream_t st);
 
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z,

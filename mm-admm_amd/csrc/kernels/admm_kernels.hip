@@ -517,15 +517,10 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
 #pragma unroll
     for (int i = 0; i < K; ++i) z[i] += pk[i];
     double G1[K], Igt;
-#ifdef MMX_EXP_NOGRAD  // experiment: no blockGrad in the loop (measures memory + B algebra)
-#pragma unroll
-    for (int i = 0; i < K; ++i) G1[i] = G[i] * 0.5;
-#else
     {
       const double e = blockGrad<D, true, true, EXACT>(g, fc, z, xi, dx, G1, Igt, gcache, tie);
       bad |= (e != e);
     }
-#endif
     if constexpr (!EXACT) {
       if (*tie) break;
     }
@@ -593,9 +588,6 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.advance();
 #pragma unroll
     for (int i = 0; i < K; ++i) G[i] = G1[i];
-#ifdef MMX_EXP_ONEITER  // experiment: exactly one BFGS iteration
-    break;
-#endif
     if (Ix < tol) break;
   }
   return (iter == 50) ? 50 : iter + 1;
@@ -781,12 +773,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   const int tot = nIn * KK;  // even: K*K is even
 #pragma unroll 4
   for (int e = tid * 2; e < tot; e += BS * 2) {
-#ifdef MMX_EXP_NOB  // experiment: no Bkinv traffic (identity), measures everything else
-    const int ea = e / KK, eb = (e + 1) / KK;
-    const double2 v = make_double2(((e - ea * KK) % (K + 1)) == 0 ? 1.0 : 0.0, ((e + 1 - eb * KK) % (K + 1)) == 0 ? 1.0 : 0.0);
-#else
     const double2 v = *reinterpret_cast<const double2*>(chunk + e);
-#endif
     const int sa = e / KK, ka = e - sa * KK;
     const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
     lds[ka * (BS + 1) + sa] = v.x;
@@ -820,9 +807,6 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
       const double d = z[i] - z0[i];
       dual2 += d * d;
     }
-#if defined(MMX_EXP_NOGRAD) || defined(MMX_EXP_NOB)
-    bad = false;  // timing experiments: the numerics are meaningless
-#endif
     pv[0] = Ihsave;
     pv[1] = dual2;
     pv[3] = (double)its;
@@ -848,11 +832,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     double2 v;
     v.x = lds[ka * (BS + 1) + sa];
     v.y = lds[kb * (BS + 1) + sb];
-#ifndef MMX_EXP_NOB
     *reinterpret_cast<double2*>(chunk + e) = v;
-#else
-    if (v.x == 12345.0) chunk[e] = v.y;  // keep the LDS reads alive
-#endif
   }
   block_partials<6, BS>(pv, partials, lb);
 }
@@ -959,9 +939,6 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
       const double d = z[i] - zs[i];
       dual2 += d * d;
     }
-#if defined(MMX_EXP_NOGRAD)
-    bad = false;  // timing experiments: the numerics are meaningless
-#endif
     pv[0] = Ihsave;
     pv[1] = dual2;
     pv[3] = (double)its;
@@ -1330,6 +1307,24 @@ __global__ void __launch_bounds__(kBlock) k_pad_rows(const double* __restrict__ 
 void launch_pad_rows(const double* vals, long long rows, double* pad, hipStream_t st) {
   if (rows > 0) hipLaunchKernelGGL(k_pad_rows, dim3((unsigned)((rows + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vals, rows, pad);
 }
+// hessInvs = I (src/Mesh.cpp:456-464) on the device, in the layout of bidx<D> (the caller zeroes
+// the buffer first): one lane per (simplex, diagonal entry)
+template <int D>
+__global__ void k_bkinv_identity(int nF, double* B) {
+  constexpr int K = D * (D + 1);
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)nF * K) return;
+  const int s = (int)(t / K), i = (int)(t % K);
+  B[bidx<D>(s, i * K + i)] = 1.0;
+}
+template <int D>
+void launch_bkinv_identity(int nF, double* B, hipStream_t st) {
+  constexpr int K = D * (D + 1);
+  const long long n = (long long)nF * K;
+  if (n > 0) hipLaunchKernelGGL(k_bkinv_identity<D>, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, nF, B);
+}
+template void launch_bkinv_identity<2>(int, double*, hipStream_t);
+template void launch_bkinv_identity<3>(int, double*, hipStream_t);
 // reuse of the previous prox's last gradient at the prox entry (MMX_GRAD_CACHE=0 disables)
 static int cache_enabled() {
   static int v = [] {

@@ -129,6 +129,15 @@ def lib():
     return L
 
 
+def _close_at_exit(obj):
+    """__del__ of a handle owner: close it, unless the interpreter is tearing down (module globals
+    such as the ctypes library may already be gone; the process exit releases the device)."""
+    try:
+        obj.close()
+    except (TypeError, AttributeError, NameError):
+        pass
+
+
 def _check(rc):
     if rc != MMADMM_OK:
         msg = lib().mmadmm_last_error().decode(errors="replace")
@@ -313,7 +322,8 @@ class Comm:
             lib().mmadmm_comm_destroy(self.h)
             self.h = None
 
-    __del__ = close
+    def __del__(self):
+        _close_at_exit(self)
 
 
 def partition_plan(dim, nP, F, nranks, rank):
@@ -375,7 +385,8 @@ class Engine:
             lib().mmadmm_destroy(self.h)
             self.h = None
 
-    __del__ = close
+    def __del__(self):
+        _close_at_exit(self)
 
     def step(self, nIters, tol=1e-3):
         Ih = ctypes.c_double()

@@ -1,0 +1,182 @@
+"""BASELINE.json's configurations at their stated sizes on the GPU, against the oracle.
+
+SURVEY.md §8 sizes: C2 SquareGrid n = 223 (99,905 nodes), C3 the 1,000,519-node disc of the
+headline bench, C4 3D SquareGrid n = 63 (512,191 nodes, 3,000,564 tetrahedra), C5 3D n = 136
+(5,086,809 nodes, 30,185,472 tetrahedra, time-varying monitor).  The size-dependent code paths
+meet the oracle here: the deferred per-iteration reduction slices (maxBlocks), the XCD block
+ranges of the prox, the LDS chunk tail of the 2D prox and 64-bit Bkinv indexing.
+
+* C2, C3, C4: bit-identical device state (x, z, u, Bkinv) to the oracle with correctly rounded pow
+  and the exact diagonal solve, fixed iteration counts (the oracle runs on OMP_NUM_THREADS host
+  cores); C2 also at reference semantics (glibc pow, Jacobi-CG, early exit on): same ADMM iteration
+  counts and <= 1e-10 relative node-position error.
+* C4 partitioned over two ranks (loopback communicator, one GPU) equals one GPU bit for bit.
+* C5 (too large for the oracle in a test): one GPU equals a three-rank partition bit for bit.  On
+  one GPU the Bkinv offsets of the last tetrahedra exceed 2^32 doubles; on the partition every
+  rank's offsets stay below 2^31, so equality checks the 64-bit index path.  Plus properties: no
+  inverted element, one grid rebuild per step, finite energies.
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import mmadmm_amd as mx
+import oracle_py
+
+pytestmark = pytest.mark.gpu
+
+POS_TOL = 1e-10
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+
+
+@pytest.fixture(autouse=True)
+def _pow_mode_reset():
+    yield
+    oracle_py.set_pow_mode(0)
+
+
+def _pair(m, mon, dt, tau, rho, pow_mode=1, cg_mode=1):
+    oracle_py.set_pow_mode(pow_mode)
+    om = oracle_py.Mesh(m.dim, m.Xp, m.F, m.mask)
+    O = oracle_py.Integrator(om, mon, dt, tau, rho, nthreads=_threads(), cgMode=cg_mode)
+    G = mx.Engine(mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(m.dim, mon), rho=rho, tau=tau), dt)
+    return O, G
+
+
+def _bitwise(O, G, fields=("x", "z", "u", "hess")):
+    for f in fields:
+        a, b = G.get(f), O.get(f)
+        assert np.array_equal(a, b), f"{f}: {np.count_nonzero(a != b)} of {a.size} entries differ"
+
+
+def _run_parallel(fns):
+    errs = []
+
+    def wrap(f):
+        try:
+            f()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=wrap, args=(f,)) for f in fns]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    if errs:
+        raise errs[0]
+
+
+def _partitioned(M, dt, nranks, steps, iters, regrid=False):
+    comm = mx.Comm.loopback(nranks)
+    parts = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm) for r in range(nranks)]
+    ih = [[None] * steps for _ in range(nranks)]
+    for e in parts:
+        if regrid:
+            e.set_regrid(True)
+
+    def run(r):
+        def f():
+            for k in range(steps):
+                ih[r][k] = parts[r].step(iters, -1.0)[0]
+        return f
+
+    _run_parallel([run(r) for r in range(nranks)])
+    return comm, parts, ih
+
+
+def test_c2_square_grid_bitwise():
+    """C2: SquareGrid n = 223, MEx1, Monitor2320-family parameters; 2 steps x 10 iterations."""
+    m = mx.MeshData.rect(2, 223)
+    assert (m.nP, m.nF) == (99905, 198916)
+    O, G = _pair(m, 1, 0.055, 0.5, 50.0)
+    for s in range(2):
+        ih_o = O.step(10, -1.0)[0]
+        ih_g = G.step(10, -1.0)[0]
+        assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
+    _bitwise(O, G)
+    assert G.stats()["bfgs_iters"] == O.bfgs_iters()
+
+
+def test_c2_square_grid_reference_semantics():
+    """C2 with the reference's arithmetic (glibc pow, Jacobi-CG) and its early exit (tol 1e-3)."""
+    m = mx.MeshData.rect(2, 223)
+    O, G = _pair(m, 1, 0.055, 0.5, 50.0, pow_mode=0, cg_mode=0)
+    for s in range(3):
+        ih_o, it_o = O.step(10, 1e-3)[:2]
+        ih_g, it_g = G.step(10, 1e-3)
+        assert it_o == it_g, f"ADMM iteration count differs at step {s}"
+        assert abs(ih_o - ih_g) <= 1e-11 * abs(ih_o)
+    xo, xg = O.get("x"), G.get("x")
+    assert np.abs(xo - xg).max() / np.abs(xo).max() <= POS_TOL
+
+
+def test_c3_disc_bitwise():
+    """C3: the bench's 1,000,519-node disc, MEx1, dt 0.055 tau 0.5 rho 50; 2 steps x 10 iterations
+    (the first with the FD-Hessian prox and the gradient predictor)."""
+    m = mx.MeshData.hexdisc(577, 0.5, 0.5, 0.5)
+    assert m.nP == 1000519
+    O, G = _pair(m, 1, 0.055, 0.5, 50.0)
+    for s in range(2):
+        ih_o = O.step(10, -1.0)[0]
+        ih_g = G.step(10, -1.0)[0]
+        assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
+    _bitwise(O, G)
+    assert G.stats()["bfgs_iters"] == O.bfgs_iters()
+
+
+def test_c4_cube_bitwise_and_partitioned():
+    """C4: 3D SquareGrid n = 63, anisotropic shell monitor (MonType 6), dt 0.025 tau 0.5 rho 2000;
+    1 step x 10 iterations bit-identical to the oracle, then the same step on a two-rank
+    element partition bit-identical to one GPU."""
+    m = mx.MeshData.rect(3, 63)
+    assert (m.nP, m.nF) == (512191, 3000564)
+    O, G = _pair(m, 6, 0.025, 0.5, 2000.0)
+    ih_o = O.step(10, -1.0)[0]
+    ih_g = G.step(10, -1.0)[0]
+    assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
+    _bitwise(O, G)
+    assert G.stats()["bfgs_iters"] == O.bfgs_iters()
+    del O
+    M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 6), rho=2000.0, tau=0.5)
+    comm, parts, ih = _partitioned(M, 0.025, 2, 1, 10)
+    xr = G.get("x").reshape(-1, 3)
+    for r, e in enumerate(parts):
+        assert np.array_equal(e.get("x").reshape(-1, 3), xr[e.local_nodes()]), f"rank {r}"
+        assert abs(ih[r][0] - ih_g) <= 1e-12 * abs(ih_g)
+        e.close()
+    comm.close()
+    G.close()
+
+
+def test_c5_cube_partition_equals_single():
+    """C5: 3D n = 136, time-varying monitor (MonType 7, grid rebuilt on the device every step),
+    dt 0.025 tau 0.5 rho 2000; 1 step x 3 iterations on one GPU and on a three-rank partition."""
+    m = mx.MeshData.rect(3, 136)
+    assert (m.nP, m.nF) == (5086809, 30185472)
+    assert m.nF * 144 > 2 ** 32  # one GPU: Bkinv offsets beyond 32 bits
+    assert (m.nF // 3 + 64) * 144 < 2 ** 31  # partition: every rank's offsets within 31 bits
+    M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 7), rho=2000.0, tau=0.5)
+    G = mx.Engine(M, 0.025)
+    G.set_regrid(True)
+    e0 = G.energy()
+    ih_g, it_g = G.step(3, -1.0)
+    assert it_g == 3 and np.isfinite(ih_g) and np.isfinite(e0)
+    st = G.stats()
+    assert st["regrids"] == 1 and st["steps"] == 1
+    assert st["bfgs_iters"] > 0
+    xg = G.get("x").reshape(-1, 3)
+    assert np.isfinite(xg).all()
+    assert np.isfinite(G.energy())
+    G.close()
+    comm, parts, ih = _partitioned(M, 0.025, 3, 1, 3, regrid=True)
+    for r, e in enumerate(parts):
+        assert np.array_equal(e.get("x").reshape(-1, 3), xg[e.local_nodes()]), f"rank {r}"
+        assert abs(ih[r][0] - ih_g) <= 1e-12 * abs(ih_g)
+        e.close()
+    comm.close()
