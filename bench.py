@@ -11,7 +11,8 @@ first warm-up step (finite-difference Hessians) is reported separately.
   python bench.py [--gpus N] [--steps K] [--warmup W]
 For N > 1 launch with torch.distributed.run: the global mesh grows with N (hexagonal disc of
 N_disc = 577*sqrt(N), ~N million nodes) and is element-partitioned across the ranks, one per GPU,
-exchanging interface-slot values with RCCL all-gathers (weak scaling).
+exchanging interface-slot values with their neighbouring ranks over RCCL send/recv (recursive
+coordinate bisection of the simplex centroids; weak scaling).
 value = ADMM iterations per second x (global nodes / 1,000,519): whole-job throughput in units of
 C3-sized meshes.
 
@@ -46,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-spmv", action="store_true")
     ap.add_argument("--no-be", action="store_true", help="skip the backward-Euler (method 2) section")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 (2D unit square, 99,905 nodes) section")
     ap.add_argument("--no-3d", action="store_true", help="skip the 3D (BASELINE config 4) section")
     ap.add_argument("--c5", action="store_true",
                     help="add BASELINE config 5 on one GPU: 3D 5.09M-node mesh, time-varying monitor")
@@ -175,6 +177,47 @@ def be_bench(mx, with_cpu):
     return out
 
 
+def c2_bench(mx, with_cpu, threads, admm_iter, steps=20):
+    """BASELINE config 2 / SURVEY C2 on one GPU: 2D SquareGrid n = 223 (99,905 nodes, 198,916
+    triangles), MEx1 (static Gaussian bump), dt 0.055 tau 0.5 rho 50, admm_iter ADMM iterations per
+    step with the early exit off; the CPU path on the same mesh beside it."""
+    mesh = mx.MeshData.rect(2, 223)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5)
+    E = mx.Engine(M, 0.055)
+    t0 = time.perf_counter()
+    E.step(admm_iter, -1.0)
+    E.sync()
+    first = time.perf_counter() - t0
+    for _ in range(2):
+        E.step(admm_iter, -1.0)
+    E.set_timing(True)
+    E.reset_stats()
+    E.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        E.step(admm_iter, -1.0)
+    E.sync()
+    el = time.perf_counter() - t0
+    st = E.stats()
+    prox_ms = st["t_prox_ms"] / max(st["n_prox"], 1)
+    prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
+    out = {"workload": "C2: 2D SquareGrid n=223, %d nodes, %d triangles, MEx1, dt 0.055 tau 0.5 rho 50, %d ADMM "
+                       "iterations per step" % (mesh.nP, mesh.nF, admm_iter),
+           "value": round(steps * admm_iter / el, 3), "unit": "ADMM it/s", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 3), "first_step_ms": round(first * 1e3, 1),
+           "kernels": {"k_prox_ms": round(prox_ms, 4)},
+           "roofline": {"bound": "hbm", "kernel": "k_prox_lds<2, 128>", "achieved": round(prox_gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
+                        "bytes_per_launch": st["prox_bytes"], "avg_launch_ms": round(prox_ms, 4)}}
+    E.close()
+
+    def _cpu():
+        out["cpu_baseline"] = cpu_baseline(mesh, admm_iter, threads, label="C2")
+    if with_cpu:  # CPU baselines run after every GPU measurement (main)
+        DEFERRED.append(_cpu)
+    return out
+
+
 def c4_bench(mx, with_cpu, threads, admm_iter):
     """BASELINE config 4 / SURVEY C4 on one GPU: 3D SquareGrid n = 63 (512,191 nodes, 3,000,564
     tetrahedra), the anisotropic shell monitor (MonType 6), dt 0.025 tau 0.5 (the 3DMonitor2x0
@@ -222,11 +265,14 @@ def c4_bench(mx, with_cpu, threads, admm_iter):
         O = oracle_py.Integrator(om, 6, 0.025, 0.5, 2000.0, nthreads=threads)
         O.step(1, -1.0)
         t0 = time.perf_counter()
-        O.step(1, -1.0)
-        cdt = time.perf_counter() - t0
+        for _ in range(CPU_STEPS):
+            O.step(1, -1.0)
+        cdt = (time.perf_counter() - t0) / CPU_STEPS
         out["cpu_baseline"] = {"value": round(1.0 / cdt, 3), "unit": "ADMM it/s", "cores": threads, "kind": "port",
-                               "sample": "C4 mesh, 1 timed step of 1 ADMM iteration after set-up and the FD-Hessian "
-                                         "step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, %d threads)" % threads}
+                               "host": host_info(threads),
+                               "sample": "C4 mesh, %d timed steps of 1 ADMM iteration after set-up and the FD-Hessian "
+                                         "step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, %d threads)"
+                                         % (CPU_STEPS, threads)}
     if with_cpu:  # CPU baselines run after every GPU measurement (main)
         DEFERRED.append(_cpu)
     return out
@@ -295,35 +341,82 @@ def pmc_traffic(kernel):
     return d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_raw_per_launch")
 
 
-def cpu_baseline(mesh, admm_iter, threads):
+def host_info(threads):
+    """The GPU box's host as the CPU baseline saw it: nproc, the CPUs this job may run
+    on, the lscpu model and physical core count, and the threads the baseline used."""
+    info = {"threads_used": threads, "nproc": os.cpu_count(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = dict((a.strip(), b.strip()) for a, b in (ln.split(":", 1) for ln in out.splitlines() if ":" in ln))
+        info["model"] = kv.get("Model name")
+        if kv.get("Core(s) per socket") and kv.get("Socket(s)"):
+            info["physical_cores"] = int(kv["Core(s) per socket"]) * int(kv["Socket(s)"])
+        info["threads_per_core"] = kv.get("Thread(s) per core")
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def cpu_threads(args):
+    """Threads of the CPU baseline: --cpu-threads, else every CPU the job is granted (the harness's
+    CPU share: OMP_NUM_THREADS when it sets one, else the affinity mask)."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env:
+        return env
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+CPU_STEPS = 5  # SURVEY §8d: >= 5 timed steps
+
+
+def cpu_baseline(mesh, admm_iter, threads, mon=1, dt=0.055, tau=0.5, rho=50.0, label="C3"):
     """Reference-equivalent CPU path (the oracle: CPU restatement of the reference, OpenMP prox,
     serial consensus algebra, -O3 -msse2) on the same mesh; bounded sample: set-up and the
-    FD-Hessian step untimed, then one timed step of admm_iter iterations."""
+    FD-Hessian step untimed, then CPU_STEPS timed steps of admm_iter iterations on `threads`
+    threads, and CPU_STEPS further steps of one iteration on one thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py
 
-    om = oracle_py.Mesh(2, mesh.Xp, mesh.F, mesh.mask)
-    O = oracle_py.Integrator(om, 1, 0.055, 0.5, 50.0, nthreads=threads)
+    om = oracle_py.Mesh(mesh.dim, mesh.Xp, mesh.F, mesh.mask)
+    O = oracle_py.Integrator(om, mon, dt, tau, rho, nthreads=threads)
     O.step(admm_iter, -1.0)
     t0 = time.perf_counter()
-    O.step(admm_iter, -1.0)
-    dt = time.perf_counter() - t0
+    for _ in range(CPU_STEPS):
+        O.step(admm_iter, -1.0)
+    el = time.perf_counter() - t0
     oracle_py.set_threads(1)  # SURVEY §8d: all cores and 1 thread
     t0 = time.perf_counter()
-    O.step(1, -1.0)
-    dt1 = time.perf_counter() - t0
-    return {"value": round(admm_iter / dt, 3), "unit": "ADMM it/s", "cores": threads, "kind": "port",
-            "value_1thread": round(1.0 / dt1, 3),
-            "sample": f"C3 mesh, 1 timed step of {admm_iter} ADMM iterations after set-up and the "
+    for _ in range(CPU_STEPS):
+        O.step(1, -1.0)
+    el1 = time.perf_counter() - t0
+    return {"value": round(CPU_STEPS * admm_iter / el, 3), "unit": "ADMM it/s", "cores": threads, "kind": "port",
+            "value_1thread": round(CPU_STEPS / el1, 3), "host": host_info(threads),
+            "sample": f"{label} mesh, {CPU_STEPS} timed steps of {admm_iter} ADMM iterations after set-up and the "
                       f"FD-Hessian step (oracle/oracle.cpp, g++ -O3 -msse2 -fopenmp, {threads} threads); "
-                      f"value_1thread: one further step of 1 ADMM iteration on 1 thread"}
+                      f"value_1thread: {CPU_STEPS} further steps of 1 ADMM iteration on 1 thread"}
 
 
-def stream_copy_ceiling(torch):
-    """Measured HBM ceiling on this box: 1 GiB device-to-device copy (read + write bytes / time)."""
+def stream_copy_ceiling(torch, la):
+    """Measured HBM ceiling on this box: a 1 GiB device-to-device copy (read + write bytes / time)
+    with the library's 16-B-per-lane streaming kernels (the fastest of its variants), and with
+    torch's copy_ for comparison."""
     n = 1 << 27  # doubles
     x = torch.ones(n, dtype=torch.float64, device="cuda")
     y = torch.empty_like(x)
+    torch.cuda.synchronize()
+    dev = torch.cuda.current_device()
+    ms = min(la.stream_copy_ms(x.data_ptr(), y.data_ptr(), n, reps=20, device=dev, variant=v) for v in (0, 1, 2))
+    kern = 2 * 8 * n / (ms * 1e-3) / 1e9
     for _ in range(3):
         y.copy_(x)
     torch.cuda.synchronize()
@@ -334,9 +427,9 @@ def stream_copy_ceiling(torch):
         y.copy_(x)
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    tms = e0.elapsed_time(e1) / reps
     del x, y
-    return round(2 * 8 * n / (ms * 1e-3) / 1e9, 1)
+    return round(kern, 1), round(2 * 8 * n / (tms * 1e-3) / 1e9, 1)
 
 
 def pmc_flops(kernel):
@@ -395,7 +488,7 @@ def main():
             dist.broadcast_object_list(uid, src=0)
             comm = mx.Comm.rccl(world, rank, uid[0], local)
             eng = mx.Engine(M, dt, rank=rank, nranks=world, comm=comm)
-            parallelism = f"element-partition x{world} (RCCL all-gather of interface slots)"
+            parallelism = f"element-partition x{world} (RCB, RCCL halo send/recv of interface slots)"
         except mx.MMADMMError as e:  # report, and measure independent replicas instead
             log(f"partitioned engine unavailable ({e}); running replicas")
             mesh, M = make_mesh(1)
@@ -505,14 +598,20 @@ def main():
                                "source": "rocprofv3 SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes "
                                          "(profiles/pmc_summary.json); peak: AMD MI355X fp64 vector spec"}
     if rank == 0 and world == 1:
-        result["roofline"]["measured_copy_ceiling_GBs"] = stream_copy_ceiling(torch)
+        cc, tc = stream_copy_ceiling(torch, la)
+        result["roofline"]["measured_copy_ceiling_GBs"] = cc
+        result["roofline"]["torch_copy_GBs"] = tc
+        result["roofline"]["frac_of_copy_ceiling"] = round(prox_gbs / cc, 4)
     if not args.no_spmv and not c4:
         log("spmv microbenchmark")
         result["spmv"] = spmv_bench(torch, la, mx, with_cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
     if not args.no_be and world == 1 and not c4:
         log("backward Euler")
         result["backward_euler"] = be_bench(mx, with_cpu=not args.no_cpu_baseline)
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count(), 16)
+    threads = cpu_threads(args)
+    if not args.no_c2 and world == 1 and not c4:
+        log("C2 square grid")
+        result["c2"] = c2_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
     if not args.no_3d and world == 1 and not c4:
         log("3D C4")
         result["c4_3d"] = c4_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
@@ -533,6 +632,9 @@ def main():
         if cb.get("value_1thread"):
             cb["gpu_speedup_1thread"] = round(result["value"] / cb["value_1thread"], 1)
     c4r = result.get("c4_3d", {})
+    c2r = result.get("c2", {})
+    if c2r.get("cpu_baseline", {}).get("value"):
+        c2r["cpu_baseline"]["gpu_speedup"] = round(c2r["value"] / c2r["cpu_baseline"]["value"], 1)
     if c4r.get("cpu_baseline", {}).get("value"):
         c4r["cpu_baseline"]["gpu_speedup"] = round(c4r["value"] / c4r["cpu_baseline"]["value"], 1)
     if rank == 0:

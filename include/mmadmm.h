@@ -64,6 +64,7 @@ typedef struct mmadmm_params {
   int device;     /* HIP device ordinal, -1 = current device */
   int rank;       /* element-partitioned run: this rank (0 for single GPU) */
   int nranks;     /* number of ranks (1 for single GPU) */
+  int partition;  /* element partition: MMADMM_PART_RCB (0, default) or MMADMM_PART_RANGES */
 } mmadmm_params;
 
 typedef struct mmadmm_stats {
@@ -180,10 +181,15 @@ int mmadmm_debug_blockgrad(mmadmm_handle h, int s, const double* z, const double
                            double* out);
 
 /* ---- element partition across ranks (one process per GPU)
- * Rank r owns simplices [r*nF/nranks, (r+1)*nF/nranks) and the nodes they touch; interface
- * nodes are replicated and their x-update / predictor sums take the other ranks' slot values
- * from an all-gather, summed in ascending global simplex order: node positions are bit-identical
- * to a single-GPU run.  No reference counterpart (the reference is single-process OpenMP). */
+ * Every simplex has one owner rank -- MMADMM_PART_RCB: recursive coordinate bisection of the
+ * simplex centroids (compact parts, short interfaces); MMADMM_PART_RANGES: contiguous ranges
+ * [r*nF/nranks, (r+1)*nF/nranks) of global ids -- and a rank holds the nodes its simplices touch;
+ * interface nodes are replicated.  Their x-update / predictor sums take the other ranks' slot
+ * values from a halo exchange with the neighbouring ranks only (RCCL send/recv), summed in
+ * ascending global simplex order: node positions are bit-identical to a single-GPU run.  At most
+ * 64 ranks.  No reference counterpart (the reference is single-process OpenMP). */
+#define MMADMM_PART_RCB 0
+#define MMADMM_PART_RANGES 1
 #define MMADMM_UNIQUE_ID_BYTES 128
 typedef struct mmadmm_comm_s* mmadmm_comm;
 typedef struct mmadmm_plan_s* mmadmm_plan;
@@ -200,12 +206,18 @@ int mmadmm_create_partitioned(int dim, int nP, const double* Xp, const double* X
                               const int32_t* mask, const mmadmm_params* p, mmadmm_monitor_fn fn, void* user,
                               mmadmm_comm comm, mmadmm_handle* out);
 int mmadmm_local_nodes(mmadmm_handle h, int* n_local, int32_t* global_ids);
-/* the partition plan alone (host only): local nodes, per-node slot sources (>= 0 local slot
- * offset s*K+n*D, < 0 row -1-src of the gathered buffer), exported slot offsets */
-int mmadmm_plan_create(int dim, int nP, int nF, const int32_t* F, int nranks, int rank, mmadmm_plan* out);
-int mmadmm_plan_sizes(mmadmm_plan h, int* nLocalNodes, int* nLocalSimplices, int* simplexBegin, int* nSources,
-                      int* nExport, int* maxExport);
-int mmadmm_plan_get(mmadmm_plan h, int32_t* localNodes, int32_t* incPtr, int32_t* incSrc, int32_t* exportOff);
+/* the partition plan alone (host only).  Xp (nP x dim) is needed by MMADMM_PART_RCB.  Sizes: local
+ * nodes and simplices, incident-slot sources, rows sent / received, neighbour ranks, interface nodes
+ * (local nodes another rank also touches).  Arrays: local node and simplex global ids (ascending),
+ * per-node slot sources (incPtr/incSrc: >= 0 local slot offset s*K+n*D, < 0 row -1-src of the
+ * receive buffer), the local slot offsets sent (per peer, peers ascending), and per peer
+ * {rank, rows sent, rows received} (the receive buffer holds the peers' rows in that order). */
+int mmadmm_plan_create(int dim, int nP, const double* Xp, int nF, const int32_t* F, int nranks, int rank, int method,
+                       mmadmm_plan* out);
+int mmadmm_plan_sizes(mmadmm_plan h, int* nLocalNodes, int* nLocalSimplices, int* nSources, int* nSend, int* nRecv,
+                      int* nPeers, int* nInterface);
+int mmadmm_plan_get(mmadmm_plan h, int32_t* localNodes, int32_t* localSimplices, int32_t* incPtr, int32_t* incSrc,
+                    int32_t* sendOff, int32_t* peers);
 int mmadmm_plan_destroy(mmadmm_plan h);
 
 /* device math self-test (correctly rounded powers): op 0 sqrt, 1 x^1.5, 2 x^-0.5, 3 x^2.25,

@@ -126,6 +126,12 @@ int mmx_ilu_symbolic(int n, const int32_t* ia, const int32_t* ja, int level, lon
 int mmx_matrix_chain_prof(mmx_matrix m, unsigned long long* out, int reset);
 int mmx_sweep_schedule_info(int n, const int32_t* ia, const int32_t* ja, int level, int fwd, long long* info);
 
+/* Measurement utility (no reference counterpart): the achievable HBM ceiling.  Copies n doubles
+ * (n even, device pointers, 16-byte aligned) reps times with a 16-B-per-lane streaming kernel
+ * (variant 0: grid-stride, nontemporal; 1: one element per lane; 2: four per lane) on a private
+ * stream; *ms = average milliseconds per copy (bytes moved per copy: 16 n). */
+int mmx_stream_copy(int device, const double* d_src, double* d_dst, long long n, int reps, int variant, double* ms);
+
 #ifdef __cplusplus
 }
 #endif

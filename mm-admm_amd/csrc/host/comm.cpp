@@ -33,6 +33,18 @@ struct RcclComm final : Comm {
   void allgather(int, const double* dsend, double* drecv, size_t count, hipStream_t st) override {
     MMX_NCCL(ncclAllGather(dsend, drecv, count, ncclDouble, comm, st));
   }
+  void exchange(int, const double* dsend, double* drecv, const std::vector<HaloPeer>& peers, int rowLen,
+                hipStream_t st) override {
+    if (peers.empty()) return;
+    MMX_NCCL(ncclGroupStart());
+    for (const HaloPeer& p : peers) {
+      if (p.sendCount)
+        MMX_NCCL(ncclSend(dsend + (size_t)p.sendOff * rowLen, (size_t)p.sendCount * rowLen, ncclDouble, p.rank, comm, st));
+      if (p.recvCount)
+        MMX_NCCL(ncclRecv(drecv + (size_t)p.recvOff * rowLen, (size_t)p.recvCount * rowLen, ncclDouble, p.rank, comm, st));
+    }
+    MMX_NCCL(ncclGroupEnd());
+  }
 };
 
 // Threads of one process, one per rank, all on the same or on different devices.
@@ -42,7 +54,8 @@ struct LoopbackComm final : Comm {
   int arrived = 0;
   long long generation = 0;
   std::vector<std::vector<double>> slots;
-  explicit LoopbackComm(int n) : slots(n) { nranks = n; }
+  std::vector<std::vector<std::vector<double>>> mail;  // mail[from][to]
+  explicit LoopbackComm(int n) : slots(n), mail(n, std::vector<std::vector<double>>(n)) { nranks = n; }
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     const long long g = generation;
@@ -63,6 +76,27 @@ struct LoopbackComm final : Comm {
       if (count)
         MMX_HIP(hipMemcpyAsync(drecv + (size_t)q * count, slots[q].data(), count * sizeof(double),
                                hipMemcpyHostToDevice, st));
+    MMX_HIP(hipStreamSynchronize(st));
+    barrier();
+  }
+  void exchange(int rank, const double* dsend, double* drecv, const std::vector<HaloPeer>& peers, int rowLen,
+                hipStream_t st) override {
+    for (const HaloPeer& p : peers) {
+      auto& box = mail[rank][p.rank];
+      box.resize((size_t)p.sendCount * rowLen);
+      if (!box.empty())
+        MMX_HIP(hipMemcpyAsync(box.data(), dsend + (size_t)p.sendOff * rowLen, box.size() * sizeof(double),
+                               hipMemcpyDeviceToHost, st));
+    }
+    MMX_HIP(hipStreamSynchronize(st));
+    barrier();
+    for (const HaloPeer& p : peers) {
+      const auto& box = mail[p.rank][rank];
+      if (box.size() != (size_t)p.recvCount * rowLen) throw Error(MMADMM_ERR_INVALID, "loopback exchange: size mismatch");
+      if (!box.empty())
+        MMX_HIP(hipMemcpyAsync(drecv + (size_t)p.recvOff * rowLen, box.data(), box.size() * sizeof(double),
+                               hipMemcpyHostToDevice, st));
+    }
     MMX_HIP(hipStreamSynchronize(st));
     barrier();
   }

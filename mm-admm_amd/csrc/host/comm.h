@@ -1,13 +1,17 @@
-// comm.h -- the one collective the element-partitioned ADMM path needs: an all-gather of
-// fixed-size fp64 blocks (interface-slot values, per-iteration scalar partials).  RCCL over xGMI
-// between processes (one per GPU); a host-staged loopback between threads of one process, which
-// lets the partitioned path be tested on a single GPU.
+// comm.h -- the communication the element-partitioned ADMM path needs: a halo exchange of
+// interface-slot values with the neighbouring ranks (x-update and predictor sums, once per ADMM
+// iteration), and an all-gather of small fixed-size fp64 blocks (per-step scalar partials; the
+// vertex positions of a time-varying monitor's grid rebuild).  RCCL over xGMI between processes
+// (one per GPU); a host-staged loopback between threads of one process, which lets the
+// partitioned path be tested on a single GPU.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
 #include <mutex>
 #include <vector>
+
+#include "partition.h"
 
 namespace mmx {
 
@@ -16,6 +20,11 @@ struct Comm {
   virtual ~Comm() = default;
   // recv[q*count .. (q+1)*count) = rank q's send block (device pointers, stream-ordered)
   virtual void allgather(int rank, const double* dsend, double* drecv, size_t count, hipStream_t st) = 0;
+  // for every peer p: send rows [p.sendOff, p.sendOff + p.sendCount) of dsend to p.rank, receive
+  // p.recvCount rows from p.rank into drecv at row p.recvOff (rows of rowLen doubles, device
+  // pointers, stream-ordered)
+  virtual void exchange(int rank, const double* dsend, double* drecv, const std::vector<HaloPeer>& peers, int rowLen,
+                        hipStream_t st) = 0;
 };
 
 Comm* make_rccl_comm(int nranks, int rank, const void* uid, int device);

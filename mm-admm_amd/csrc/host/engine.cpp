@@ -130,22 +130,12 @@ class Engine final : public EngineBase {
     powd_ = pow(d, d * pp / 2.0);
     // element partition (a single rank owns everything); node -> incident slots in ascending
     // global simplex id (column-major D^T order), other ranks' slots from the gathered buffer
-    plan_ = make_partition_plan(D, nP, nF, Fh_.data(), nranks_, rank_);
+    plan_ = make_partition_plan(D, nP, Vp.data(), nF, Fh_.data(), nranks_, rank_, p.partition);
     nP_ = (int)plan_.localNodes.size();
-    nF_ = plan_.s1 - plan_.s0;
+    nF_ = (int)plan_.localSimplices.size();
     if (nranks_ > 1) {  // vertex owners for the partitioned regrid: the rank of the lowest incident simplex
-      std::vector<long long> minS(nP, (long long)nF);
-      for (long long sI = 0; sI < nF; ++sI)
-        for (int n = 0; n < D + 1; ++n) {
-          const int v = Fh_[(size_t)sI * (D + 1) + n];
-          if (sI < minS[v]) minS[v] = sI;
-        }
       std::vector<std::vector<int>> owned(nranks_);
-      for (int v = 0; v < nP; ++v) {
-        int q = 0;  // isolated vertices: rank 0 (as the plan places them)
-        if (minS[v] < nF) q = (int)(std::upper_bound(plan_.sbeg.begin(), plan_.sbeg.end(), minS[v]) - plan_.sbeg.begin()) - 1;
-        owned[q].push_back(v);
-      }
+      for (int v = 0; v < nP; ++v) owned[plan_.nodeOwner[v]].push_back(v);
       size_t mx = 1;
       for (auto& o : owned) mx = std::max(mx, o.size());
       maxOwned_ = (int)mx;
@@ -222,9 +212,9 @@ class Engine final : public EngineBase {
     xPrev_.upload(Vl.data(), Vl.size(), st_);
     xBar_.upload(Vl.data(), Vl.size(), st_);
     if (nranks_ > 1) {
-      expOff_.upload(plan_.exportOff.data(), std::max<size_t>(plan_.exportOff.size(), 1), st_);
-      export_.alloc((size_t)std::max(plan_.maxExport, 1) * D);
-      remote_.alloc((size_t)nranks_ * std::max(plan_.maxExport, 1) * D);
+      expOff_.upload(plan_.sendOff.data(), std::max<size_t>(plan_.sendOff.size(), 1), st_);
+      export_.alloc((size_t)std::max<size_t>(plan_.sendOff.size(), 1) * D);
+      remote_.alloc((size_t)std::max(plan_.recvRows, 1) * D);
     }
     z_.alloc((size_t)nF_ * K);
     gcache_.alloc((size_t)nF_ * (K + 1));
@@ -664,11 +654,12 @@ class Engine final : public EngineBase {
     return h0 - h1 + h2;
   }
 
-  // all-gather of this rank's interface-slot values: mode 0 x-update terms, 1 simplex gradients
+  // halo exchange of interface-slot values with the neighbouring ranks: mode 0 x-update terms,
+  // 1 simplex gradients
   void exchange(int mode) {
     if (nranks_ == 1) return;
-    launch_pack_export<D>(mode, (int)plan_.exportOff.size(), expOff_.p, z_.p, u_.p, gs_.p, w_, export_.p, st_);
-    comm_->allgather(rank_, export_.p, remote_.p, (size_t)std::max(plan_.maxExport, 1) * D, st_);
+    launch_pack_export<D>(mode, (int)plan_.sendOff.size(), expOff_.p, z_.p, u_.p, gs_.p, w_, export_.p, st_);
+    comm_->exchange(rank_, export_.p, remote_.p, plan_.peers, D, st_);
   }
 
   // rows x 2*kNumPartials scalar records on the device -> combined over ranks on the host

@@ -966,6 +966,26 @@ int mmx_sweep_schedule_info(int n, const int32_t* ia, const int32_t* ja, int lev
   });
 }
 
+int mmx_stream_copy(int device, const double* d_src, double* d_dst, long long n, int reps, int variant, double* ms) {
+  return guarded([&] {
+    if (!d_src || !d_dst || n <= 0 || (n & 1) || reps <= 0 || !ms) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    MMX_HIP(hipSetDevice(device));
+    hipStream_t st;
+    MMX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    mmx::Timer t;
+    t.init();
+    mmx::launch_stream_copy(variant, n / 2, d_src, d_dst, st);  // warm-up
+    MMX_HIP(hipEventRecord(t.a, st));
+    for (int r = 0; r < reps; ++r) mmx::launch_stream_copy(variant, n / 2, d_src, d_dst, st);
+    MMX_HIP(hipEventRecord(t.b, st));
+    MMX_HIP(hipEventSynchronize(t.b));
+    float el = 0.f;
+    MMX_HIP(hipEventElapsedTime(&el, t.a, t.b));
+    MMX_HIP(hipStreamDestroy(st));
+    *ms = (double)el / reps;
+  });
+}
+
 int mmx_matrix_destroy(mmx_matrix m) {
   if (!m) return MMADMM_OK;
   delete m->m;

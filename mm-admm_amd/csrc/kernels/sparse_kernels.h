@@ -96,4 +96,8 @@ void launch_cgs_update(int n, const double* vbar, const double* z, const double*
 // Scalar finalisers (one workgroup).  mode 0 init, 1 alpha, 2 omega, 3 update.
 void launch_cgs_fin(int mode, const double* partials, int nblk, CgsScalars* sc, hipStream_t st);
 
+// Measurement utility: dst = src over n2 16-byte elements (streaming copy ceiling; variants in
+// sparse_kernels.hip).
+void launch_stream_copy(int variant, long long n2, const double* src, double* dst, hipStream_t st);
+
 }  // namespace mmx

@@ -669,4 +669,48 @@ void launch_cgs_fin(int mode, const double* partials, int nblk, CgsScalars* sc, 
   }
 }
 
+// Streaming copy (measurement utility: the achievable HBM ceiling the bench reports beside the
+// 8 TB/s spec), 16 B per lane per access.  Variant 0: grid-stride, 4 accesses in flight per lane,
+// nontemporal hints, 8 workgroups per CU; 1: one 16-B element per lane, one pass (n2/256
+// workgroups), default policy; 2: 4 consecutive-by-stride elements per lane, one pass, default
+// policy.
+template <int VAR>
+__global__ void __launch_bounds__(256) k_stream_copy(long long n2, const v2d_t* __restrict__ src,
+                                                     v2d_t* __restrict__ dst) {
+  if constexpr (VAR == 0) {
+    const long long stride = (long long)gridDim.x * 256;
+    long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n2; i += 4 * stride) {
+      v2d_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+    }
+    for (; i < n2; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  } else if constexpr (VAR == 1) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n2) dst[i] = src[i];
+  } else {
+    const long long base = (long long)blockIdx.x * 1024 + threadIdx.x;
+    v2d_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256 < n2) v[u] = src[base + u * 256];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256 < n2) dst[base + u * 256] = v[u];
+  }
+}
+
+void launch_stream_copy(int variant, long long n2, const double* src, double* dst, hipStream_t st) {
+  const v2d_t* s2 = reinterpret_cast<const v2d_t*>(src);
+  v2d_t* d2 = reinterpret_cast<v2d_t*>(dst);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL(k_stream_copy<0>, dim3(256 * 8), dim3(256), 0, st, n2, s2, d2); break;
+    case 1: hipLaunchKernelGGL(k_stream_copy<1>, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
+    default: hipLaunchKernelGGL(k_stream_copy<2>, dim3((unsigned)((n2 + 1023) / 1024)), dim3(256), 0, st, n2, s2, d2); break;
+  }
+}
+
 }  // namespace mmx

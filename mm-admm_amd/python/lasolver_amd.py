@@ -90,6 +90,7 @@ def lib():
     L.mmx_matrix_stats_get.argtypes = [vp, ctypes.POINTER(SparseStats)]
     L.mmx_matrix_stats_reset.argtypes = [vp]
     L.mmx_matrix_destroy.argtypes = [vp]
+    L.mmx_stream_copy.argtypes = [i, vp, vp, ll, i, i, ctypes.POINTER(ctypes.c_double)]
     L.mmx_ilu_symbolic.argtypes = [i, c_int_p, c_int_p, i, ctypes.POINTER(ll), c_int_p, c_int_p, c_int_p]
     _cfg = True
     return L
@@ -287,9 +288,18 @@ def ilu_symbolic(ia, ja, level):
     return iaf, jaf, dg
 
 
+def stream_copy_ms(src_ptr, dst_ptr, n, reps=20, device=0, variant=0):
+    """Average ms of a 16-B-per-lane streaming copy of n doubles between two device buffers (the
+    achievable HBM ceiling; 16 n bytes moved per copy)."""
+    ms = ctypes.c_double()
+    _check(lib().mmx_stream_copy(int(device), ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr), int(n), int(reps),
+                                 int(variant), ctypes.byref(ms)))
+    return ms.value
+
+
 def matmult(A, x):
     """accel_class.cpp's matmult(xin, xout, n, a, ia, ja) on the GPU."""
     return A.matmult(x)
 
 
-__all__ = ["ParamIter", "MatrixStruc", "MatrixIter", "matmult", "ilu_symbolic", "MMADMMError"]
+__all__ = ["ParamIter", "MatrixStruc", "MatrixIter", "matmult", "ilu_symbolic", "stream_copy_ms", "MMADMMError"]

@@ -29,7 +29,10 @@ MONITOR_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, c_double_p, c_double_p, ctypes
 class mmadmm_params(ctypes.Structure):
     _fields_ = [("dt", ctypes.c_double), ("tau", ctypes.c_double), ("rho", ctypes.c_double),
                 ("grad_use", ctypes.c_int), ("device", ctypes.c_int), ("rank", ctypes.c_int),
-                ("nranks", ctypes.c_int)]
+                ("nranks", ctypes.c_int), ("partition", ctypes.c_int)]
+
+
+PARTITION = {"rcb": 0, "ranges": 1}  # MMADMM_PART_RCB / MMADMM_PART_RANGES
 
 
 class mmadmm_stats(ctypes.Structure):
@@ -121,9 +124,10 @@ def lib():
                                             c_int_p, ctypes.POINTER(mmadmm_params), MONITOR_FN, vp, vp,
                                             ctypes.POINTER(vp)]
     L.mmadmm_local_nodes.argtypes = [vp, ctypes.POINTER(ctypes.c_int), c_int_p]
-    L.mmadmm_plan_create.argtypes = [ctypes.c_int] * 3 + [c_int_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
-    L.mmadmm_plan_sizes.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int)] * 6
-    L.mmadmm_plan_get.argtypes = [vp, c_int_p, c_int_p, c_int_p, c_int_p]
+    L.mmadmm_plan_create.argtypes = [ctypes.c_int, ctypes.c_int, c_double_p, ctypes.c_int, c_int_p, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.mmadmm_plan_sizes.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int)] * 7
+    L.mmadmm_plan_get.argtypes = [vp] + [c_int_p] * 6
     L.mmadmm_plan_destroy.argtypes = [vp]
     _lib = L
     return L
@@ -326,21 +330,28 @@ class Comm:
         _close_at_exit(self)
 
 
-def partition_plan(dim, nP, F, nranks, rank):
-    """The element partition of rank `rank` (host only) -> dict of numpy arrays."""
+def partition_plan(dim, Xp, F, nranks, rank, method="rcb"):
+    """The element partition of rank `rank` (host only) -> dict of numpy arrays: localNodes,
+    localSimplices (global ids, ascending), incPtr/incSrc (per local node its incident slot sources
+    in ascending global simplex order: >= 0 local slot offset, < 0 row -1-src of the receive
+    buffer), sendOff (local slot offsets sent, per peer), peers (rows: rank, rows sent, rows
+    received), recvRows, interfaceNodes."""
     L = lib()
+    Xp = np.ascontiguousarray(Xp, dtype=np.float64).reshape(-1, dim)
     F = np.ascontiguousarray(F, dtype=np.int32)
     h = ctypes.c_void_p()
-    _check(L.mmadmm_plan_create(int(dim), int(nP), len(F), _ip(F), int(nranks), int(rank), ctypes.byref(h)))
+    _check(L.mmadmm_plan_create(int(dim), Xp.shape[0], _dp(Xp), len(F), _ip(F), int(nranks), int(rank),
+                                PARTITION[method], ctypes.byref(h)))
     try:
-        v = [ctypes.c_int() for _ in range(6)]
+        v = [ctypes.c_int() for _ in range(7)]
         _check(L.mmadmm_plan_sizes(h, *[ctypes.byref(x) for x in v]))
-        nl, nfl, s0, ns, ne, mx = [x.value for x in v]
-        out = dict(localNodes=np.zeros(nl, np.int32), incPtr=np.zeros(nl + 1, np.int32),
-                   incSrc=np.zeros(ns, np.int32), exportOff=np.zeros(ne, np.int32))
-        _check(L.mmadmm_plan_get(h, _ip(out["localNodes"]), _ip(out["incPtr"]), _ip(out["incSrc"]),
-                                 _ip(out["exportOff"])))
-        out.update(nLocalSimplices=nfl, simplexBegin=s0, maxExport=mx)
+        nl, nfl, ns, nsend, nrecv, npeers, nif = [x.value for x in v]
+        out = dict(localNodes=np.zeros(nl, np.int32), localSimplices=np.zeros(nfl, np.int32),
+                   incPtr=np.zeros(nl + 1, np.int32), incSrc=np.zeros(ns, np.int32), sendOff=np.zeros(nsend, np.int32),
+                   peers=np.zeros((npeers, 3), np.int32))
+        _check(L.mmadmm_plan_get(h, *[_ip(out[k]) for k in ("localNodes", "localSimplices", "incPtr", "incSrc",
+                                                             "sendOff", "peers")]))
+        out.update(recvRows=nrecv, interfaceNodes=nif)
         return out
     finally:
         L.mmadmm_plan_destroy(h)
@@ -349,12 +360,13 @@ def partition_plan(dim, nP, F, nranks, rank):
 class Engine:
     """Direct handle on one libmmadmm integrator (what MeshIntegrator wraps)."""
 
-    def __init__(self, mesh, dt, rank=0, nranks=1, comm=None):
+    def __init__(self, mesh, dt, rank=0, nranks=1, comm=None, partition="rcb"):
         """rank/nranks/comm: element-partitioned run (include/mmadmm.h); `mesh` is the global mesh
-        on every rank and this engine owns simplices [rank*nF/nranks, (rank+1)*nF/nranks)."""
+        on every rank and this engine owns the simplices the partition ("rcb": recursive coordinate
+        bisection of the centroids; "ranges": contiguous id ranges) gives rank `rank`."""
         L = lib()
         p = mmadmm_params(dt=float(dt), tau=mesh.tau, rho=mesh.rho, grad_use=int(mesh.gradUse),
-                          device=mesh.device, rank=int(rank), nranks=int(nranks))
+                          device=mesh.device, rank=int(rank), nranks=int(nranks), partition=PARTITION[partition])
         fn, user = mesh.Mon._cfunc()
         self._fn = fn
         h = ctypes.c_void_p()

@@ -40,20 +40,23 @@ def _run_parallel(fns):
 
 
 CASES = [
-    ("rect2d", lambda mx: mx.MeshData.rect(2, 12), 2, 3, 1000.0, 0.5, 0.025, 2),
-    ("rect2d_3ranks", lambda mx: mx.MeshData.rect(2, 14), 2, 5, 50.0, 0.5, 0.05, 3),
-    ("hexdisc", lambda mx: mx.MeshData.hexdisc(10, 0.5, 0.5, 0.5), 2, 1, 50.0, 0.5, 0.055, 2),
-    ("rect3d", lambda mx: mx.MeshData.rect(3, 3), 3, 1, 20.0, 0.5, 0.05, 2),
+    ("rect2d", lambda mx: mx.MeshData.rect(2, 12), 2, 3, 1000.0, 0.5, 0.025, 2, "rcb"),
+    ("rect2d_3ranks", lambda mx: mx.MeshData.rect(2, 14), 2, 5, 50.0, 0.5, 0.05, 3, "rcb"),
+    ("hexdisc", lambda mx: mx.MeshData.hexdisc(10, 0.5, 0.5, 0.5), 2, 1, 50.0, 0.5, 0.055, 2, "rcb"),
+    ("hexdisc_4ranks", lambda mx: mx.MeshData.hexdisc(14, 0.5, 0.5, 0.5), 2, 1, 50.0, 0.5, 0.055, 4, "rcb"),
+    ("hexdisc_ranges", lambda mx: mx.MeshData.hexdisc(10, 0.5, 0.5, 0.5), 2, 1, 50.0, 0.5, 0.055, 3, "ranges"),
+    ("rect3d", lambda mx: mx.MeshData.rect(3, 3), 3, 1, 20.0, 0.5, 0.05, 2, "rcb"),
+    ("rect3d_4ranks", lambda mx: mx.MeshData.rect(3, 4), 3, 6, 2000.0, 0.5, 0.025, 4, "rcb"),
 ]
 
 
-@pytest.mark.parametrize("name,gen,dim,mon,rho,tau,dt,nranks", CASES, ids=[c[0] for c in CASES])
-def test_partitioned_equals_single(mx, name, gen, dim, mon, rho, tau, dt, nranks):
+@pytest.mark.parametrize("name,gen,dim,mon,rho,tau,dt,nranks,method", CASES, ids=[c[0] for c in CASES])
+def test_partitioned_equals_single(mx, name, gen, dim, mon, rho, tau, dt, nranks, method):
     mesh = gen(mx)
     M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, mon), rho=rho, tau=tau, device=0)
     ref = mx.Engine(M, dt)
     comm = mx.Comm.loopback(nranks)
-    parts = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm) for r in range(nranks)]
+    parts = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm, partition=method) for r in range(nranks)]
     steps, iters = 4, 6
     ih_ref = [ref.step(iters, -1.0)[0] for _ in range(steps)]
     ih = [[None] * steps for _ in range(nranks)]
@@ -79,7 +82,7 @@ def test_partitioned_equals_single(mx, name, gen, dim, mon, rho, tau, dt, nranks
     assert covered.all()
     # the early-exit path agrees too (same iteration decisions)
     ref2 = mx.Engine(M, dt)
-    parts2 = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm) for r in range(nranks)]
+    parts2 = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm, partition=method) for r in range(nranks)]
     it_ref = ref2.step(50, 1e-3)[1]
     its = [None] * nranks
 

@@ -1,7 +1,8 @@
 """Element partition of the ADMM consensus step on CPU ranks (torch.distributed, gloo): the
-exchange plan of libmmadmm (host-only mmadmm_plan_*) plus an all-gather of interface-slot values
-reproduces, bit for bit, the single-process per-node sums over incident slots in ascending
-global simplex order -- the sums k_xupdate / k_predict form on each GPU."""
+exchange plan of libmmadmm (host-only mmadmm_plan_*) plus a halo exchange with the neighbouring
+ranks only (point-to-point send/recv of interface-slot values, as the engine does over RCCL)
+reproduces, bit for bit, the single-process per-node sums over incident slots in ascending global
+simplex order -- the sums k_xupdate / k_predict form on each GPU."""
 import os
 import sys
 
@@ -13,6 +14,12 @@ import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mm-admm_amd", "python"))
+
+
+def _mesh(mx, kind, dim, n):
+    if kind == "disc":
+        return mx.MeshData.hexdisc(n, 0.5, 0.5, 0.5)
+    return mx.MeshData.rect(dim, n)
 
 
 def _expected_sums(F, nP, D, T):
@@ -27,53 +34,65 @@ def _expected_sums(F, nP, D, T):
     return np.array(acc)
 
 
-def _rank_main(rank, world, port, dim, n, out):
+def _rank_main(rank, world, port, kind, dim, n, method, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import mmadmm_amd as mx
-        mesh = mx.MeshData.rect(dim, n)
+        mesh = _mesh(mx, kind, dim, n)
         D, K = dim, dim * (dim + 1)
         F = mesh.F
         T = np.random.default_rng(5).standard_normal(len(F) * K) * np.exp(np.random.default_rng(6).uniform(-20, 20, len(F) * K))
-        plan = mx.partition_plan(dim, mesh.nP, F, world, rank)
-        s0 = plan["simplexBegin"]
-        mxe = max(plan["maxExport"], 1)
-        send = np.zeros((mxe, D))
-        for e, off in enumerate(plan["exportOff"]):
-            send[e] = T[s0 * K + off: s0 * K + off + D]
-        gathered = [torch.zeros(mxe * D, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(gathered, torch.from_numpy(send.reshape(-1)))
-        remote = torch.cat(gathered).numpy().reshape(-1, D)
+        plan = mx.partition_plan(dim, mesh.Xp, F, world, rank, method)
+        ls = plan["localSimplices"]
+        Tl = T.reshape(-1, K)[ls].reshape(-1)  # this rank's slot values, local simplex order
+        send = np.zeros((max(len(plan["sendOff"]), 1), D))
+        for e, off in enumerate(plan["sendOff"]):
+            send[e] = Tl[off: off + D]
+        recv = torch.zeros(max(plan["recvRows"], 1) * D, dtype=torch.float64)
+        reqs, so, ro = [], 0, 0
+        sendt = torch.from_numpy(send.reshape(-1))
+        for q, ns, nr in plan["peers"]:
+            reqs.append(dist.isend(sendt[so * D:(so + ns) * D].clone(), int(q)))
+            reqs.append(dist.irecv(recv[ro * D:(ro + nr) * D], int(q)))
+            so, ro = so + ns, ro + nr
+        for r in reqs:
+            r.wait()
+        remote = recv.numpy().reshape(-1, D)
         nodes = plan["localNodes"]
         sums = np.zeros((len(nodes), D))
         for l in range(len(nodes)):
             acc = [0.0] * D
             for t in range(plan["incPtr"][l], plan["incPtr"][l + 1]):
                 src = int(plan["incSrc"][t])
-                vals = T[s0 * K + src: s0 * K + src + D] if src >= 0 else remote[-1 - src]
+                vals = Tl[src: src + D] if src >= 0 else remote[-1 - src]
                 for c in range(D):
                     acc[c] = acc[c] + float(vals[c])
             sums[l] = acc
         exp = _expected_sums(F, mesh.nP, D, T)[nodes]
-        out[rank] = bool(np.array_equal(sums, exp)) and len(nodes) > 0
-        # every simplex is owned by exactly one rank
-        cnt = torch.tensor([plan["nLocalSimplices"]], dtype=torch.int64)
+        ok = bool(np.array_equal(sums, exp)) and len(nodes) > 0
+        # every simplex is owned by exactly one rank; neighbours only (no rank talks to itself)
+        cnt = torch.tensor([len(ls)], dtype=torch.int64)
         dist.all_reduce(cnt)
-        out[rank] = out[rank] and int(cnt.item()) == len(F)
+        ok = ok and int(cnt.item()) == len(F) and all(int(q) != rank for q in plan["peers"][:, 0])
+        out[rank] = ok
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dim,n", [(2, 2, 8), (3, 2, 7), (2, 3, 3)])
-def test_partition_exchange_gloo(world, dim, n):
+CASES = [(2, "rect", 2, 8, "rcb"), (3, "rect", 2, 7, "rcb"), (2, "rect", 3, 3, "rcb"), (4, "disc", 2, 9, "rcb"),
+         (4, "disc", 2, 9, "ranges"), (4, "rect", 3, 4, "rcb")]
+
+
+@pytest.mark.parametrize("world,kind,dim,n,method", CASES)
+def test_partition_exchange_gloo(world, kind, dim, n, method):
     pytest.importorskip("mmadmm_amd")
-    port = 29500 + world * 10 + dim * 100 + n
+    port = 29500 + world * 10 + dim * 100 + n + (500 if method == "ranges" else 0) + (1000 if kind == "disc" else 0)
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     out = mgr.dict()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, dim, n, out)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, kind, dim, n, method, out)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -85,6 +104,56 @@ def test_partition_exchange_gloo(world, dim, n):
 def test_single_rank_plan_is_the_full_incidence():
     import mmadmm_amd as mx
     mesh = mx.MeshData.rect(2, 5)
-    plan = mx.partition_plan(2, mesh.nP, mesh.F, 1, 0)
-    assert np.array_equal(plan["localNodes"], np.arange(mesh.nP)) and plan["maxExport"] == 0
-    assert (plan["incSrc"] >= 0).all() and plan["nLocalSimplices"] == len(mesh.F)
+    plan = mx.partition_plan(2, mesh.Xp, mesh.F, 1, 0)
+    assert np.array_equal(plan["localNodes"], np.arange(mesh.nP)) and len(plan["peers"]) == 0
+    assert (plan["incSrc"] >= 0).all() and np.array_equal(plan["localSimplices"], np.arange(len(mesh.F)))
+
+
+def _interface(mx, mesh, world, method):
+    plans = [mx.partition_plan(mesh.dim, mesh.Xp, mesh.F, world, r, method) for r in range(world)]
+    return plans, sum(p["interfaceNodes"] for p in plans)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_rcb_disc_cuts_are_short(world):
+    """The headline disc numbers its simplices ring by ring, so contiguous id ranges cut it into
+    annuli (each cut a whole circle); RCB cuts it into sectors/strips with short interfaces, and
+    balances the simplices to within 2% per cut (the plane snaps to the best nearby vertex
+    coordinate)."""
+    import mmadmm_amd as mx
+    mesh = mx.MeshData.hexdisc(60, 0.5, 0.5, 0.5)
+    plans, rcb = _interface(mx, mesh, world, "rcb")
+    _, ranges = _interface(mx, mesh, world, "ranges")
+    sizes = [len(p["localSimplices"]) for p in plans]
+    assert max(sizes) <= 1.06 * len(mesh.F) / world and sum(sizes) == len(mesh.F)
+    assert rcb < 0.5 * ranges, (rcb, ranges)
+    assert max(len(p["peers"]) for p in plans) <= min(world - 1, 6)
+
+
+def test_rcb_cuts_a_structured_cube_between_cell_layers():
+    """An odd number of cell layers: the proportional cut falls inside the middle layer; the plane
+    snaps to a layer boundary (one layer is within the 2% balance tolerance at n = 51), so the
+    interface is one plane of (n+1)^2 nodes, not three."""
+    import mmadmm_amd as mx
+    n = 51
+    mesh = mx.MeshData.rect(3, n)
+    plans, total = _interface(mx, mesh, 2, "rcb")
+    assert [p["interfaceNodes"] for p in plans] == [(n + 1) ** 2] * 2
+    sizes = [len(p["localSimplices"]) for p in plans]
+    assert abs(sizes[0] - sizes[1]) == len(mesh.F) // n  # one layer of cells off the half
+
+
+def test_rcb_is_deterministic_and_rank_consistent():
+    """Every rank derives the same owners: the simplex sets of all ranks tile the mesh, and what
+    rank q sends to rank r is exactly what r expects from q (row counts agree pairwise)."""
+    import mmadmm_amd as mx
+    mesh = mx.MeshData.rect(3, 5)
+    world = 5
+    plans = [mx.partition_plan(3, mesh.Xp, mesh.F, world, r) for r in range(world)]
+    own = np.concatenate([p["localSimplices"] for p in plans])
+    assert np.array_equal(np.sort(own), np.arange(len(mesh.F)))
+    cnt = {(r, int(q)): (int(s), int(v)) for r, p in enumerate(plans) for q, s, v in p["peers"]}
+    for (r, q), (s, v) in cnt.items():
+        assert cnt[(q, r)] == (v, s)
+    again = mx.partition_plan(3, mesh.Xp, mesh.F, world, 2)
+    assert np.array_equal(again["localSimplices"], plans[2]["localSimplices"])
