@@ -176,6 +176,9 @@ struct SparseMatrix {
   std::vector<int> iaf, jaf, dgRel;
   DevBuf<int> d_iaf, d_jaf, d_dg, d_amap, d_permf, d_permb;
   DevBuf<int2> d_piv;
+  DevBuf<int> d_toff;           // factor in LDS: per lower entry, its offset into d_tgt
+  DevBuf<signed char> d_tgt;    // per (lower entry, pivot-row upper entry): position updated in the row, or -1
+  bool facLds = false;
   int nchf = 0, nchb = 0, nlevf = 0, nlevb = 0;
   DevBuf<double> d_af;
   DevBuf<unsigned> d_flags, d_ctl;  // ctl: 8 tickets, err, pad (16-byte multiple)
@@ -293,6 +296,38 @@ struct SparseMatrix {
         for (int k = iaf[i]; k < dg[i]; ++k) pv[k] = make_int2(dg[jaf[k]], iaf[jaf[k] + 1]);
       d_piv.upload(pv.data(), pv.size(), st);
     }
+    {  // update positions for the LDS-row factor (rows of at most kFacW entries)
+      int maxW = 0;
+      for (int i = 0; i < n; ++i) maxW = std::max(maxW, iaf[i + 1] - iaf[i]);
+      std::vector<long long> off(std::max<size_t>(jaf.size(), 1), 0);
+      long long tot = 0;
+      for (int i = 0; i < n; ++i)
+        for (int k = iaf[i]; k < dg[i]; ++k) {
+          off[k] = tot;
+          tot += iaf[jaf[k] + 1] - dg[jaf[k]] - 1;
+        }
+      const char* fm = getenv("MMX_FACTOR");
+      facLds = maxW <= kFacW && tot < (1ll << 31) && !(fm && std::strcmp(fm, "global") == 0);
+      if (facLds) {
+        std::vector<int> toff(off.size());
+        std::vector<signed char> tg(std::max<long long>(tot, 1), -1);
+#pragma omp parallel for schedule(dynamic, 4096)
+        for (int i = 0; i < n; ++i) {
+          const int* rb = jaf.data() + iaf[i];
+          const int* re = jaf.data() + iaf[i + 1];
+          for (int k = iaf[i]; k < dg[i]; ++k) {
+            toff[k] = (int)off[k];
+            const int id = jaf[k];
+            for (int pp = dg[id] + 1; pp < iaf[id + 1]; ++pp) {
+              const int* f = std::lower_bound(rb, re, jaf[pp]);
+              tg[off[k] + (pp - dg[id] - 1)] = (f != re && *f == jaf[pp]) ? (signed char)(f - rb) : (signed char)-1;
+            }
+          }
+        }
+        d_toff.upload(toff.data(), toff.size(), st);
+        d_tgt.upload(tg.data(), tg.size(), st);
+      }
+    }
     // level schedules of the lower (forward sweep, factor) and upper (backward sweep) factor
     std::vector<int> lev(n);
     auto schedule = [&](bool fwd, DevBuf<int>& out, int& nch, int& nlev) {
@@ -409,8 +444,12 @@ struct SparseMatrix {
       fepoch = 1;
     }
     begin(2);
-    launch_ilu_factor(d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_permf.p, nchf, d_af.p,
-                      d_flags.p, fepoch, tickets(), errw(), st);
+    if (facLds)
+      launch_ilu_factor_lds(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_toff.p, d_tgt.p, d_permf.p, nchf,
+                            d_af.p, d_flags.p, fepoch, tickets(), errw(), st);
+    else
+      launch_ilu_factor(d_ia.p, d_ja.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_permf.p, nchf, d_af.p,
+                        d_flags.p, fepoch, tickets(), errw(), st);
     if (useChain) {  // the sweeps read the factor's entries in schedule order
       launch_chain_fill(chf.nent, chf.src.p, d_af.p, chf.val.p, 0.0, st);
       launch_chain_fill(chb.nent, chb.src.p, d_af.p, chb.val.p, 0.0, st);

@@ -47,6 +47,14 @@ void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int*
                        const int* dg, const int2* piv, const int* perm, int nchunks, double* af, unsigned* flags,
                        unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
 
+// The same factor with each lane's row in LDS (rows of at most kFacW entries): toff[k] for a lower
+// entry k indexes tgt[], which holds for each upper entry of k's pivot row (after the diagonal)
+// the position in row i it updates, or -1.
+constexpr int kFacW = 127;
+void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, const int* iaf, const int* jaf, const int* dg,
+                           const int2* piv, const int* toff, const signed char* tgt, const int* perm, int nchunks,
+                           double* af, unsigned* flags, unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
+
 // Sweep over the rows of perm (forward or backward level order).  Forward: unit L into granules
 // gout, right-hand side per pro (0: src; 1: p = res + beta (p - omega avbar); 2: s = res - alpha
 // avbar, stored to p).  Backward: U from the forward granules gin into out and granules gout.

@@ -388,6 +388,120 @@ __global__ void __launch_bounds__(kSweepRows) k_ilu_factor(const int* __restrict
   }
 }
 
+// The same factor with the lane's row held in LDS and the dependency waits batched.  Row i's
+// kFacBatch next lower entries have their flags polled together (one round trip); for the ready
+// prefix, every pivot and the first kFacU upper values of every pivot row are requested together
+// (a second round trip), with the host-built positions tgt[] in row i that each upper value updates
+// (-1: row i does not hold that column) -- no merge search.  Then the eliminations run in ascending
+// order on the LDS image of the row (same operations, same order as k_ilu_factor: bit-identical).
+// A 2D mesh row (<= 7 lower entries) waits two round trips instead of two per lower entry.
+template <int B, int U>
+__global__ void __launch_bounds__(kSweepRows) k_ilu_factor_lds(const int* __restrict__ ia, const double* __restrict__ a,
+                                                              const int* __restrict__ amap, const int* __restrict__ iaf,
+                                                              const int* __restrict__ jaf, const int* __restrict__ dg,
+                                                              const int2* __restrict__ piv, const int* __restrict__ toff,
+                                                              const signed char* __restrict__ tgt,
+                                                              const int* __restrict__ perm, int nchunks, double* af,
+                                                              unsigned* flags, unsigned epoch, unsigned* ticket,
+                                                              unsigned* err) {
+  __shared__ double rowv[kFacW * kSweepRows];
+  const int lane = (int)threadIdx.x;
+  double* my = rowv + lane;  // entry e of the lane's row at my[e * 64]
+  bool give_up = false;
+  while (!give_up) {
+    const int t = take_ticket(ticket);
+    if (t >= nchunks) break;
+    const int i = perm[(size_t)t * kSweepRows + lane];
+    const bool valid = i >= 0;
+    int kb = 0, kd = 0, ke = 0;
+    if (valid) {
+      kb = iaf[i];
+      kd = dg[i];
+      ke = iaf[i + 1];
+      for (int e = 0; e < ke - kb; ++e) my[e * kSweepRows] = 0.0;
+      for (int ii = ia[i]; ii < ia[i + 1]; ++ii) my[(amap[ii] - kb) * kSweepRows] = a[ii];
+    }
+    int kk = kb;
+    bool done = !valid;
+    unsigned spins = 0;
+    while (true) {
+      bool fin = false, prog = false;
+      if (!done && kk < kd) {
+        const int nb = (kd - kk < B) ? kd - kk : B;
+        int id[B], to[B];
+        int2 pv[B];
+        unsigned fl[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+          if (q < nb) {
+            id[q] = jaf[kk + q];
+            pv[q] = piv[kk + q];
+            to[q] = toff[kk + q];
+          }
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+          if (q < nb) fl[q] = __hip_atomic_load(&flags[id[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int r = 0;
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+          if (q < nb && r == q && fl[q] == epoch) r = q + 1;
+        if (r > 0) {
+          prog = true;
+          double pvt[B], uu[B][U];
+          signed char tg[B][U];
+#pragma unroll
+          for (int q = 0; q < B; ++q)
+            if (q < r) {
+              pvt[q] = ld_agent(&af[pv[q].x]);
+              const int m = pv[q].y - pv[q].x - 1;
+#pragma unroll
+              for (int u = 0; u < U; ++u)
+                if (u < m) {
+                  uu[q][u] = ld_agent(&af[pv[q].x + 1 + u]);
+                  tg[q][u] = tgt[to[q] + u];
+                }
+            }
+#pragma unroll
+          for (int q = 0; q < B; ++q)
+            if (q < r) {
+              const int e0 = kk + q - kb;
+              const double mult = my[e0 * kSweepRows] / pvt[q];
+              my[e0 * kSweepRows] = mult;
+              const int m = pv[q].y - pv[q].x - 1;
+#pragma unroll
+              for (int u = 0; u < U; ++u)
+                if (u < m && tg[q][u] >= 0) my[tg[q][u] * kSweepRows] = my[tg[q][u] * kSweepRows] - mult * uu[q][u];
+              for (int c0 = U; c0 < m; c0 += U) {  // long pivot rows
+                double uc[U];
+                signed char tc[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                  if (c0 + u < m) {
+                    uc[u] = ld_agent(&af[pv[q].x + 1 + c0 + u]);
+                    tc[u] = tgt[to[q] + c0 + u];
+                  }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                  if (c0 + u < m && tc[u] >= 0) my[tc[u] * kSweepRows] = my[tc[u] * kSweepRows] - mult * uc[u];
+              }
+            }
+          kk += r;
+        }
+      }
+      if (!done && kk == kd) {  // publish: agent-scope (write-through) stores, drained, then the flag
+        for (int e = 0; e < ke - kb; ++e) st_agent(&af[kb + e], my[e * kSweepRows]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&flags[i], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        done = true;
+        fin = true;
+      }
+      if (__all(done)) break;
+      backoff(spins, __ballot(fin || prog) != 0, err, 1u, give_up);
+      if (give_up) break;
+    }
+  }
+}
+
 // Triangular sweeps (scaler_ILU::solve, ILU_class.cpp:470-499).  Forward (unit L):
 // y_i = b_i - sum_{k<diag} af_k y_jk; backward (U): x_i = (y_i - sum_{k>diag} af_k x_jk) / af_diag;
 // the terms are subtracted one at a time in ascending column order.  The forward sweep fuses the
@@ -611,6 +725,15 @@ void launch_spmv2(int epi, int nblk, const int4* desc, const int* ia, const int*
     hipLaunchKernelGGL(k_spmv2<1>, g, bl, 0, st, desc, nblk, ia, ja, a, x, y, e1, partials);
   else
     hipLaunchKernelGGL(k_spmv2<2>, g, bl, 0, st, desc, nblk, ia, ja, a, x, y, e1, partials);
+}
+
+void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, const int* iaf, const int* jaf, const int* dg,
+                           const int2* piv, const int* toff, const signed char* tgt, const int* perm, int nchunks,
+                           double* af, unsigned* flags, unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st) {
+  if (nchunks <= 0) return;
+  const int grid = nchunks < sweep_grid() ? nchunks : sweep_grid();
+  hipLaunchKernelGGL((k_ilu_factor_lds<8, 8>), dim3(grid), dim3(kSweepRows), 0, st, ia, a, amap, iaf, jaf, dg, piv, toff,
+                     tgt, perm, nchunks, af, flags, epoch, ticket, err);
 }
 
 void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
