@@ -81,6 +81,10 @@ public:
         stepsTaken++;
         return Ih;
     }
+    // the reference's commented Mesh<D>::setUp hook (src/Mesh.cpp:1006-1014): rebuild the monitor
+    // grid from the current mesh at the start of every step (no reference counterpart; off by default)
+    void setTimeVarying(bool on) { mmadmm_cxx::check(mmadmm_set_regrid(h_, on ? 1 : 0)); }
+
     double getEnergy() {
         double E = 0;
         mmadmm_cxx::check(mmadmm_energy(h_, &E));
