@@ -180,6 +180,9 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
       return true;
     };
     while (!fits(RI) && RI < kChainImpMax) RI *= 2;
+    // the importer runs at most RI imports ahead of the compute wave: take the whole ring (a
+    // band importing hundreds of values per iteration needs many iterations of run-ahead)
+    RI = kChainImpMax;
     if (!fits(RI)) {
       S.why = "import ring too small for band " + std::to_string(b);
       return S;

@@ -22,7 +22,7 @@ namespace mmx {
 
 constexpr int kChainLanes = 64;
 constexpr int kChainRingMax = 32;    // LDS ring slots per lane (doubles) -- chain_sweep.hip kRingMax
-constexpr int kChainImpMax = 1024;   // LDS import slots (16-byte granules) -- chain_sweep.hip kImpMax
+constexpr int kChainImpMax = 2048;   // LDS import slots (16-byte granules) -- chain_sweep.hip kImpMax
 constexpr int kChainPad = -2147483647 - 1;  // empty entry slot (schedule building only)
 
 struct ChainSchedule {

@@ -26,7 +26,11 @@ namespace {
 
 constexpr int kPad = -2147483647 - 1;
 constexpr int kRingMax = 32;    // = kChainRingMax (host/chain_sched.h)
-constexpr int kImpMax = 1024;   // = kChainImpMax
+constexpr int kImpMax = 2048;   // = kChainImpMax
+#ifndef MMX_IMP_Q
+#define MMX_IMP_Q 4
+#endif
+constexpr int kImpQ = MMX_IMP_Q;  // imports each importer lane polls per round
 constexpr unsigned kChainSpinMax = 1u << 22;
 
 template <typename T>
@@ -347,29 +351,50 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       }
     } else {
       // ---------------- importer ----------------
-      // lane l delivers imports l, l + 64, l + 128, ... in order; the published count is the
-      // lowest import still pending over the lanes (all below it are in their slots)
+      // lane l delivers imports l, l + 64, l + 128, ... in order, polling its next kImpQ at once:
+      // a band of long chains below the cell-centre rows imports ~4 values per row (256 per
+      // iteration), so one import per lane per round trip would set the pace; the published count
+      // is the lowest import still pending over the lanes (all below it are in their slots)
+      constexpr int Q = kImpQ;
       const int ib = ca.bandImp[b], ni = ca.bandNImp[b];
       const unsigned long long m0 = ca.prof ? clk() : 0;
       int k = lane;
-      int need = (k < ni && k >= RI) ? ca.impFree[ib + k - RI] : -1;
-      int j = k < ni ? ca.impRow[ib + k] : 0;
       int published = 0;
       unsigned spins = 0;
+      int jq[Q], nq[Q];
+      bool fresh = true;
       while (ni > 0) {
-        bool prog = false;
-        if (k < ni && lds_read(&s_prog) > need) {  // slot free: its previous import is no longer read
-          const uint64_t lo = __hip_atomic_load(gout + 2 * (size_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint64_t hi = __hip_atomic_load(gout + 2 * (size_t)j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(lo >> 32) == epoch && (unsigned)(hi >> 32) == epoch) {
-            s_dep[impBase + (k & (RI - 1))] = join_words((uint32_t)lo, (uint32_t)hi);
-            k += 64;
-            prog = true;
-            if (k < ni) {
-              need = k >= RI ? ca.impFree[ib + k - RI] : -1;
-              j = ca.impRow[ib + k];
-            }
+        if (fresh) {  // the rows and slot-free iterations of the lane's next Q imports
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            const int kq = k + 64 * q;
+            jq[q] = kq < ni ? ca.impRow[ib + kq] : 0;
+            nq[q] = (kq < ni && kq >= RI) ? ca.impFree[ib + kq - RI] : -1;
           }
+          fresh = false;
+        }
+        const int progNow = (k < ni) ? lds_read(&s_prog) : 0;
+        uint64_t lo[Q], hi[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {  // a slot is free once its previous import is no longer read
+          lo[q] = hi[q] = 0;
+          if (k + 64 * q < ni && progNow > nq[q]) {
+            lo[q] = __hip_atomic_load(gout + 2 * (size_t)jq[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[q] = __hip_atomic_load(gout + 2 * (size_t)jq[q] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        int d = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {  // the ready prefix, in order
+          if (d == q && k + 64 * q < ni && (unsigned)(lo[q] >> 32) == epoch && (unsigned)(hi[q] >> 32) == epoch) {
+            s_dep[impBase + ((k + 64 * q) & (RI - 1))] = join_words((uint32_t)lo[q], (uint32_t)hi[q]);
+            d = q + 1;
+          }
+        }
+        const bool prog = d > 0;
+        if (prog) {
+          k += 64 * d;
+          fresh = true;
         }
         int low = k < ni ? k : ni;
 #pragma unroll
