@@ -2,6 +2,7 @@
 #include "chain_sched.h"
 
 #include <algorithm>
+#include <queue>
 #include <cstdint>
 
 namespace mmx {
@@ -112,6 +113,7 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   std::vector<int> impOf(n, -1), first, last, rows;
   std::vector<long long> doneAt(n, 0);  // iteration (band-relative + offset) a row is published
   std::vector<long long> offset(S.nbands, 0);
+  std::vector<std::vector<int>> srcBands(S.nbands);  // bands each band imports from
   int RI = 256;
   for (int b = 0; b < S.nbands; ++b) {
     const int c0 = b * L, nl = std::min(L, C - c0);
@@ -189,6 +191,9 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
     }
     S.bandImp[b] = (int)S.impRow.size();
     S.bandNImp[b] = (int)ord.size();
+    for (int j : rows) srcBands[b].push_back(chainOf[j] / L);
+    std::sort(srcBands[b].begin(), srcBands[b].end());
+    srcBands[b].erase(std::unique(srcBands[b].begin(), srcBands[b].end()), srcBands[b].end());
     long long off = 0;
     for (size_t q = 0; q < ord.size(); ++q) {
       const int id = ord[q];
@@ -208,6 +213,36 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   }
   S.RI = RI;
   S.nImports = (long long)S.impRow.size();
+  // ticket order: a band becomes available once every band it imports from has a ticket; among the
+  // available bands the longest (most iterations) goes first, then the lowest index.  The long
+  // bands carry the critical path (in the backward sweep they come last by index, behind thousands
+  // of one-iteration bands they barely depend on).
+  {
+    std::vector<std::vector<int>> users(S.nbands);
+    std::vector<int> pending(S.nbands, 0);
+    for (int b = 0; b < S.nbands; ++b)
+      for (int a : srcBands[b])
+        if (a != b) {
+          users[a].push_back(b);
+          ++pending[b];
+        }
+    auto later = [&](int a, int c) { return S.bandT[a] != S.bandT[c] ? S.bandT[a] < S.bandT[c] : a > c; };
+    std::priority_queue<int, std::vector<int>, decltype(later)> avail(later);
+    for (int b = 0; b < S.nbands; ++b)
+      if (pending[b] == 0) avail.push(b);
+    S.bandOrder.clear();
+    while (!avail.empty()) {
+      const int b = avail.top();
+      avail.pop();
+      S.bandOrder.push_back(b);
+      for (int c : users[b])
+        if (--pending[c] == 0) avail.push(c);
+    }
+    if ((int)S.bandOrder.size() != S.nbands) {
+      S.why = "band import cycle";
+      return S;
+    }
+  }
   // codes -> LDS indices: 0 zero cell, 1 + ring index, 1 + 64 (R + 1) + import slot
   const int impBase = 1 + L * (R + 1);
   for (int& c : S.code) c = (c == kChainPad) ? 0 : (c >= 0 ? 1 + c : impBase + ((-c - 1) & (RI - 1)));
@@ -238,6 +273,20 @@ std::string validate_chain_schedule(const ChainSchedule& S, int n, const std::ve
     }
   for (int i = 0; i < n; ++i)
     if (bandOf[i] < 0) return "row " + std::to_string(i) + " never scheduled";
+  // tickets: every band once, after every band it imports from (the importers never wait on a band
+  // that has no workgroup yet)
+  if ((int)S.bandOrder.size() != S.nbands) return "band order size";
+  std::vector<int> ticketOf(S.nbands, -1);
+  for (int q = 0; q < S.nbands; ++q) {
+    const int b = S.bandOrder[q];
+    if (b < 0 || b >= S.nbands || ticketOf[b] >= 0) return "band order is not a permutation";
+    ticketOf[b] = q;
+  }
+  for (int b = 0; b < S.nbands; ++b)
+    for (int q = 0; q < S.bandNImp[b]; ++q) {
+      const int j = S.impRow[(size_t)S.bandImp[b] + q];
+      if (bandOf[j] != b && ticketOf[bandOf[j]] > ticketOf[b]) return "band imports from a later ticket";
+    }
   for (int i = 0; i < n; ++i) {
     const int b = bandOf[i], l = laneOf[i], t = iterOf[i];
     const size_t base = ((size_t)(S.bandSlot[b] + t) * E) * L + l;

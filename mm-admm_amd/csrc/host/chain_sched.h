@@ -44,6 +44,8 @@ struct ChainSchedule {
   std::vector<int> impRow, impFree;  // per import: producer row; last iteration it is read
   std::vector<int> impNeed;          // per slot: highest import index read at that iteration (-1)
   std::vector<int> bandE;            // per band: entry slots in use (multiple of 4, <= E)
+  std::vector<int> bandOrder;        // per ticket: the band taken (every band after the bands it
+                                     // imports from; long bands as early as their sources allow)
 };
 
 // fwd: unit-lower sweep over the entries [iaf[i], dg[i]); !fwd: upper sweep over (dg[i], iaf[i+1]).

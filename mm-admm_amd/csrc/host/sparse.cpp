@@ -189,7 +189,7 @@ struct SparseMatrix {
   struct ChainDir {
     int E = 0;
     long long nent = 0, nslot = 0;
-    DevBuf<int> bandSlot, bandT, bandImp, bandNImp, bandE, laneStart, laneLen, laneSkew, code, src, dsrc, impRow,
+    DevBuf<int> bandSlot, bandT, bandImp, bandNImp, bandE, bandOrder, laneStart, laneLen, laneSkew, code, src, dsrc, impRow,
         impFree, impNeed;
     DevBuf<double> val, dval;
     ChainArgs args{};
@@ -394,6 +394,7 @@ struct SparseMatrix {
     up(c.impFree, S.impFree);
     up(c.impNeed, S.impNeed);
     up(c.bandE, S.bandE);
+    up(c.bandOrder, S.bandOrder);
     c.E = S.E;
     c.nent = (long long)S.code.size();
     c.nslot = (long long)S.dsrc.size();
@@ -405,7 +406,8 @@ struct SparseMatrix {
       MMX_HIP(hipMemsetAsync(d_cprof.p, 0, 1024 * sizeof(unsigned long long), st));
     }
     c.args = ChainArgs{c.bandSlot.p, c.bandT.p, c.bandImp.p, c.bandNImp.p, c.laneStart.p, c.laneLen.p, c.laneSkew.p,
-                       c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impFree.p, c.impNeed.p, S.nbands, S.R, S.RI,
+                       c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impFree.p, c.impNeed.p, c.bandOrder.p,
+                       S.nbands, S.R, S.RI,
                        d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr, (pe && atoi(pe) >= 2) ? 1 : 0};
   }
 

@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 
   while (true) {
     if (tid == 0) {
-      s_band = (int)atomicAdd(ticket, 1u);
+      const unsigned tk = atomicAdd(ticket, 1u);
+      s_band = tk < (unsigned)ca.nbands ? ca.bandOrder[tk] : ca.nbands;
       s_prog = 0;
       s_impDone = 0;
       s_dep[0] = 0.0;

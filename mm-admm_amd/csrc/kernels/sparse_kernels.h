@@ -80,6 +80,7 @@ struct ChainArgs {
   const int* impRow;
   const int* impFree;
   const int* impNeed;  // per slot: highest import index read at that iteration (-1: none)
+  const int* bandOrder;  // per ticket: the band taken
   int nbands, R, RI;
   unsigned long long* prof;  // optional cycle counters (MMX_CHAIN_PROF), see chain_sweep.hip
   int profIter;              // MMX_CHAIN_PROF=2: also time the waits inside iterations (perturbs them)
