@@ -552,9 +552,12 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     }
     MMX_ROW_FENCE(BA);
     const double c1 = (c2 + yBy) / cr_pow_2(c2);
-#ifdef MMX_BFGS_DIVBY
-    const double rc2 = 1.0 / c2;  // the K*K divisions by c2 below: div_by, bit-identical
-#endif
+    // fast path (EXACT = false): the 2 K^2 divisions by c2 below by Markstein's correction from
+    // one reciprocal (div_mk, bit-identical inside the ranges checked after the pass; outside
+    // them the block is recomputed exactly, as for a near-midpoint power)
+    const double rc2 = 1.0 / c2;
+    unsigned eBy = 0u;  // max of mk_exp(by, 900) over the pass
+    double fin = 0.0;   // stays +0 while every new entry is finite
     B.fresh();
     // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
     start_rows<K, kPipe>(B, rn);
@@ -575,17 +578,28 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
         double by = row[0] * (ykr[0] * pk[j]);
 #pragma unroll
         for (int q = 1; q < K; ++q) by += row[q] * (ykr[q] * pk[j]);
-#ifdef MMX_BFGS_DIVBY
-        nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - div_by(by, c2, rc2)) - div_by(pk[i] * yB[j], c2, rc2));
-#else
-        nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - by / c2) - (pk[i] * yB[j]) / c2);
-#endif
+        if constexpr (EXACT) {
+          nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - by / c2) - (pk[i] * yB[j]) / c2);
+        } else {
+          eBy = max(eBy, mk_exp(by, 900));
+          nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - div_mk(by, c2, rc2)) - div_mk(pk[i] * yB[j], c2, rc2));
+          fin = cr_fma(nrow[j], 0.0, fin);
+        }
       }
 #pragma unroll
       for (int j = 0; j < K; ++j) B.set(i, j, nrow[j]);
     }
     MMX_ROW_FENCE(BA);
     B.advance();
+    if constexpr (!EXACT) {
+      // div_mk's ranges: c2 in [2^-100, 2^100]; by = 0 or in [2^-900, 2^900]; p_i yB_j likewise,
+      // which p and yB = 0 or in [2^-450, 2^450] guarantee; every new entry finite
+      unsigned ePY = 0u;
+#pragma unroll
+      for (int k = 0; k < K; ++k) ePY = max(ePY, max(mk_exp(pk[k], 450), mk_exp(yB[k], 450)));
+      if (!(c2 >= 0x1p-100 && c2 <= 0x1p100) || eBy > 1799u || ePY > 899u || fin != 0.0) *tie = true;
+      if (*tie) break;
+    }
 #pragma unroll
     for (int i = 0; i < K; ++i) G[i] = G1[i];
     if (Ix < tol) break;
@@ -1232,10 +1246,10 @@ __global__ void k_debug_blockgrad(DeviceMesh<D> m, int s, const double* __restri
 __global__ void k_devmath(int op, int n, const double* __restrict__ in, double* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (op == 5) {  // quotient pairs (x, c) -> RN(x/c) by div_by
+  if (op == 5) {  // quotient pairs (x, c) -> RN(x/c) by div_mk (no range check here)
     if (2 * i + 1 < n) {
       const double xx = in[2 * i], c = in[2 * i + 1];
-      out[i] = div_by(xx, c, 1.0 / c);
+      out[i] = div_mk(xx, c, 1.0 / c);
     }
     return;
   }

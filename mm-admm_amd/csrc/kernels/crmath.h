@@ -30,15 +30,31 @@ namespace mmx {
 MMX_HD double cr_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 MMX_HD double cr_sqrt(double x) { return __builtin_sqrt(x); }
 
-// RN(x / c) from rc = RN(1 / c) without a division (Markstein: with rc correctly rounded and
-// q = RN(x rc) within one ulp of x/c, the residual r = x - c q is exact (FMA) and RN(q + r rc) is
-// the correctly rounded quotient).  Zero, tiny, huge and non-finite operands take the division.
-MMX_HD double div_by(double x, double c, double rc) {
+// RN(x / c) from rc = RN(1 / c) without a division, for the BFGS update's divisions by c2
+// (Markstein: with rc correctly rounded and q = RN(x rc) within one ulp of x/c, the residual
+// e = q c - x is exact (FMA) and RN(q - e rc) is the correctly rounded quotient).  Three
+// instructions instead of the ~11 of an IEEE division (one of them a quarter-rate v_rcp_f64).
+// Exact when c > 0 with c in [2^-100, 2^100] and x = +-0 or |x| in [2^-900, 2^900]: the residual
+// cannot underflow and q is normal.  Signed zeros: x = +0 gives +0, x = -0 gives -0 (e = +0,
+// -e * rc = -0).  The CALLER checks the ranges (mk_exp_ok) and takes the exact path otherwise;
+// non-finite x gives NaN (the caller's finiteness check catches it).  Checked against IEEE
+// division on 4e8 random and near-midpoint operand pairs (dev note in DESIGN.md §3).
+MMX_HD double div_mk(double x, double c, double rc) {
   const double q = x * rc;
-  const double aq = std::fabs(q), ac = std::fabs(c);
-  if (!(aq > 0x1p-900 && aq < 0x1p900 && ac > 0x1p-900 && ac < 0x1p900)) return x / c;
-  const double r = cr_fma(-q, c, x);
-  return cr_fma(r, rc, q);
+  const double e = cr_fma(q, c, -x);
+  return cr_fma(-e, rc, q);
+}
+// frexp exponent of x biased so that (unsigned) <= 2*lim - 1 <=> x = 0 or |x| in [2^-lim, 2^lim]
+// (frexp: |x| in [2^(e-1), 2^e); 0 for zero, inf and NaN)
+MMX_HD unsigned mk_exp(double x, int lim) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (unsigned)(__builtin_amdgcn_frexp_exp(x) + (lim - 1));
+#else
+  int e;
+  (void)std::frexp(x, &e);
+  if (!std::isfinite(x)) e = 0;
+  return (unsigned)(e + (lim - 1));
+#endif
 }
 constexpr double kRecip3 = 1.0 / 3.0;  // RN(1/3), for the divisions by D + 1 = 3
 

@@ -164,19 +164,23 @@ def test_inverted_element_reported():
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_device_division_by_reciprocal_is_correctly_rounded(seed):
-    """div_by (crmath.h): RN(x/c) from RN(1/c) + one FMA correction, used for the BFGS update's
-    72 divisions by c2 and the divisions by D+1 and by the grid spacing -- bit-identical to IEEE
-    division on random, wide-range and near-midpoint quotients."""
+    """div_mk (crmath.h): RN(x/c) from RN(1/c) + one FMA correction, used for the BFGS update's
+    2 K^2 divisions by c2 in the fast prox kernels -- bit-identical to IEEE division inside the
+    ranges the kernels check (c in [2^-100, 2^100], c > 0; x = +-0 or |x| in [2^-900, 2^900]) on
+    random, wide-range and near-midpoint quotients, signed zeros included."""
     import mmadmm_amd as mx
     rng = np.random.default_rng(seed)
     n = 1 << 21
-    c = rng.uniform(1, 2, n) * np.exp2(rng.integers(-300, 300, n))
+    c = rng.uniform(1, 2, n) * np.exp2(rng.integers(-100, 100, n))
     c[: n // 4] = rng.uniform(1e-12, 1e-3, n // 4)  # c2 = p.y magnitudes of the prox
-    x = rng.uniform(-2, 2, n) * np.exp2(rng.integers(-300, 300, n))
+    x = rng.uniform(-2, 2, n) * np.exp2(rng.integers(-899, 899, n))
     # near-midpoint quotients: x = RN(c * (q + ulp(q)/2 * (1 + tiny)))
-    q = rng.uniform(1, 2, n // 4)
+    q = rng.uniform(1, 2, n // 4) * np.exp2(rng.integers(-600, 600, n // 4))
     half = np.spacing(q) / 2
-    x[n // 2: n // 2 + n // 4] = c[n // 2: n // 2 + n // 4] * (q + half * (1 + rng.uniform(-1e-6, 1e-6, n // 4)))
+    sl = slice(n // 2, n // 2 + n // 4)
+    x[sl] = c[sl] * (q + half * (1 + rng.uniform(-1e-6, 1e-6, n // 4)))
+    ok = (np.abs(x) >= 2.0 ** -900) & (np.abs(x) <= 2.0 ** 900)
+    x[~ok] = 1.0
     x[-1000:] = 0.0
     x[-500:] = -0.0
     pairs = np.empty(2 * n)
