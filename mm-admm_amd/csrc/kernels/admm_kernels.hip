@@ -353,6 +353,7 @@ __device__ void invertK(double* A) {
 template <int K>
 struct RegB {
   static constexpr bool kRowFence = false;
+  static constexpr bool kRolled = false;
   static constexpr int kPipe = 0;
   double* b;
   __device__ __forceinline__ double get(int i, int j) const { return b[i * K + j]; }
@@ -365,6 +366,7 @@ struct RegB {
 template <int K, int STRIDE = kLdsStride>
 struct LdsB {
   static constexpr bool kRowFence = true;
+  static constexpr bool kRolled = true;  // the update pass one row per trip (code size; 2D: same speed)
   static constexpr int kPipe = 0;
   double* base;  // &lds[tid], entries strided by STRIDE
   __device__ __forceinline__ double get(int i, int j) const { return base[(i * K + j) * STRIDE]; }
@@ -388,6 +390,7 @@ typedef __attribute__((address_space(3))) double ldouble;
 template <int K>
 struct WaveB {
   static constexpr bool kRowFence = true;
+  static constexpr bool kRolled = true;
   static constexpr int kPipe = MMX_ROW_PIPE;
   const gdouble* rd;
   gdouble* wr;
@@ -397,52 +400,6 @@ struct WaveB {
   // a pass over the matrix re-reads it: an opaque pointer stops the compiler from forwarding the
   // previous pass's K*K = 144 loads in registers (3D spilled)
   // the memory clobber keeps the LDS rows in LDS (no store-to-load forwarding into registers)
-  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
-};
-
-// 3D with one wavefront per SIMD: the first RL rows of the lane's Bkinv held in LDS for the whole
-// prox (read from global once, in the prologue), the rest streamed from global as in WaveB.  Row
-// indices are compile-time in the unrolled passes, so every get/set resolves to one of the two.
-template <int K, int RL>
-struct HybB {
-  static constexpr bool kRowFence = true;
-  static constexpr int kPipe = 0;
-  const gdouble* rd;
-  gdouble* wr;
-  ldouble* lds;  // &ldsRows[lane], entries strided by 64
-  __device__ __forceinline__ double get(int i, int j) const {
-    return (i < RL) ? lds[(i * K + j) * 64] : rd[(i * K + j) * 64];
-  }
-  __device__ __forceinline__ void set(int i, int j, double v) const {
-    if (i < RL) lds[(i * K + j) * 64] = v;
-    wr[(i * K + j) * 64] = v;
-  }
-  __device__ __forceinline__ void advance() { rd = wr; }
-  // each pass re-reads: the laundered pointers keep the global rows from being held across passes
-  // the memory clobber keeps the LDS rows in LDS (no store-to-load forwarding into registers)
-  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
-};
-
-// 3D with one wavefront per SIMD: the first H rows of the lane's Bkinv held in registers for the
-// whole prox (the VGPR budget of one wave per SIMD has room), the rest streamed as in WaveB --
-// passes 2 and 3 of each BFGS update then re-read only K - H rows from L2/HBM.
-template <int K, int H, int L = 0>
-struct HoldB {
-  static constexpr bool kRowFence = true;
-  static constexpr int kPipe = MMX_ROW_PIPE;
-  const gdouble* rd;
-  gdouble* wr;
-  ldouble* lds;  // rows H..H+L-1: &ldsRows[lane], entries strided by 64
-  double hold[H * K];
-  __device__ __forceinline__ double get(int i, int j) const {
-    return (i < H) ? hold[i * K + j] : (i < H + L) ? lds[((i - H) * K + j) * 64] : rd[(i * K + j) * 64];
-  }
-  __device__ __forceinline__ void set(int i, int j, double v) {
-    if (i < H) hold[i * K + j] = v;
-    else if (i < H + L) lds[((i - H) * K + j) * 64] = v;
-    wr[(i * K + j) * 64] = v;
-  }
-  __device__ __forceinline__ void advance() { rd = wr; }
   __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
 };
 
@@ -484,6 +441,39 @@ template <int K, int PIPE, class BA>
 __device__ __forceinline__ void start_rows(const BA& B, double (&rn)[PIPE > 0 ? PIPE : 1][K]) {
 #pragma unroll
   for (int d = 0; d < PIPE; ++d) load_row<K>(B, d, rn[d]);
+}
+
+// Row i of the BFGS update (src/Mesh.cpp:848):
+// B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2.  EXACT = false divides by
+// Markstein's correction (div_mk) and folds the range data into eBy / fin for the caller's check.
+template <int D, bool EXACT, class BA, int K, int PIPE>
+__device__ __forceinline__ void bfgs_update_row(BA& B, int i, double pki, double (&rn)[PIPE][K], const double (&yk)[K],
+                                                const double (&pk)[K], const double (&yB)[K], double c1, double c2,
+                                                double rc2, unsigned& eBy, double& fin) {
+  double row[K], nrow[K], ykr[K];
+  next_row<K, BA::kPipe>(B, i, row, rn);
+  // 3D: (y p^T)_qj is formed again for every row -- laundering y per row stops the compiler
+  // from keeping all K*K = 144 products live across the rows (they spilled); 2D keeps its 36
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    ykr[q] = yk[q];
+    if constexpr (D == 3) asm volatile("" : "+v"(ykr[q]));
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    double by = row[0] * (ykr[0] * pk[j]);
+#pragma unroll
+    for (int q = 1; q < K; ++q) by += row[q] * (ykr[q] * pk[j]);
+    if constexpr (EXACT) {
+      nrow[j] = row[j] + (((c1 * (pki * pk[j])) - by / c2) - (pki * yB[j]) / c2);
+    } else {
+      eBy = max(eBy, mk_exp(by, 900));
+      nrow[j] = row[j] + (((c1 * (pki * pk[j])) - div_mk(by, c2, rc2)) - div_mk(pki * yB[j], c2, rc2));
+      fin = cr_fma(nrow[j], 0.0, fin);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) B.set(i, j, nrow[j]);
 }
 
 // Mesh<D>::bfgsOptSimplex iteration loop (src/Mesh.cpp:827-856): inverse-BFGS without line
@@ -561,33 +551,22 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.fresh();
     // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
     start_rows<K, kPipe>(B, rn);
+    if constexpr (BA::kRolled) {
+      // one row per trip (3D: the unrolled pass is ~60 KB of code, more than the instruction
+      // cache; measured C4 prox 3.12 -> 2.93 ms)
+#pragma unroll 1
+      for (int i = 0; i < K; ++i) {
+        double pki = pk[0];
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-      MMX_ROW_FENCE(BA);
-      double row[K], nrow[K], ykr[K];
-      next_row<K, kPipe>(B, i, row, rn);
-      // 3D: (y p^T)_qj is formed again for every row -- laundering y per row stops the compiler
-      // from keeping all K*K = 144 products live across the rows (they spilled); 2D keeps its 36
-#pragma unroll
-      for (int q = 0; q < K; ++q) {
-        ykr[q] = yk[q];
-        if constexpr (D == 3) asm volatile("" : "+v"(ykr[q]));
+        for (int k = 1; k < K; ++k) pki = (i == k) ? pk[k] : pki;
+        bfgs_update_row<D, EXACT>(B, i, pki, rn, yk, pk, yB, c1, c2, rc2, eBy, fin);
       }
+    } else {
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        double by = row[0] * (ykr[0] * pk[j]);
-#pragma unroll
-        for (int q = 1; q < K; ++q) by += row[q] * (ykr[q] * pk[j]);
-        if constexpr (EXACT) {
-          nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - by / c2) - (pk[i] * yB[j]) / c2);
-        } else {
-          eBy = max(eBy, mk_exp(by, 900));
-          nrow[j] = row[j] + (((c1 * (pk[i] * pk[j])) - div_mk(by, c2, rc2)) - div_mk(pk[i] * yB[j], c2, rc2));
-          fin = cr_fma(nrow[j], 0.0, fin);
-        }
+      for (int i = 0; i < K; ++i) {
+        MMX_ROW_FENCE(BA);
+        bfgs_update_row<D, EXACT>(B, i, pk[i], rn, yk, pk, yB, c1, c2, rc2, eBy, fin);
       }
-#pragma unroll
-      for (int j = 0; j < K; ++j) B.set(i, j, nrow[j]);
     }
     MMX_ROW_FENCE(BA);
     B.advance();
@@ -859,27 +838,13 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 // by k_prox_fix from the untouched inputs, as in the 2D kernel.
 template <int D, bool COMP>
 #ifndef MMX_WAVE_OCC
-#define MMX_WAVE_OCC 1  // measured: one wave per SIMD without spills beats two with 75 spilled VGPRs
+#define MMX_WAVE_OCC 1  // measured: one wave per SIMD (310 VGPRs) beats two with 65 spilled VGPRs
 #endif
 __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                      double* __restrict__ zg, double* __restrict__ ug,
                                                      const double* Bin, double* Bout, double* __restrict__ partials,
                                                      int useCache) {
   constexpr int K = D * (D + 1), KK = K * K;
-#ifndef MMX_HYB_RL
-#define MMX_HYB_RL 0
-#endif
-  constexpr int RL = MMX_HYB_RL;  // Bkinv rows held in LDS for the whole prox (0: all streamed)
-#ifndef MMX_HOLD_RL
-#define MMX_HOLD_RL 4  // measured (C4, MonType 6): 2 -2.3%, 3 -1.8%, 4 -4.0%, 5 +22%, 6 +19% (prox time)
-#endif
-  constexpr int HL = MMX_HOLD_RL;  // Bkinv rows held in registers for the whole prox (HoldB)
-#ifndef MMX_HOLD_LDS
-#define MMX_HOLD_LDS 0  // measured: 2, 4 or 6 more rows in LDS change the C4 prox by < 1%: not traffic-bound any more
-#endif
-  constexpr int LL = MMX_HOLD_LDS;  // the next LL rows held in LDS (HoldB)
-  __shared__ double ldsHold[(LL > 0 ? LL : 1) * K * 64];
-  __shared__ double ldsRows[(RL > 0 ? RL : 1) * K * 64];
   const int tid = threadIdx.x;
 #ifndef MMX_WAVE_XCD
 #define MMX_WAVE_XCD 1  // measured C4: prox 3.42 -> 3.29 ms (neighbouring tets share x and monitor-grid lines in one L2)
@@ -925,24 +890,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     const double Ihsave = Igt;
     const size_t gb = (size_t)lb * KK * 64 + tid;
     int its;
-    if constexpr (RL > 0) {
-#pragma unroll 8
-      for (int e = 0; e < RL * K; ++e) ldsRows[e * 64 + tid] = Bin[gb + (size_t)e * 64];
-      HybB<K, RL> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsRows + tid)};
-      its = tie ? 0
-                : bfgs_iterations<D, HybB<K, RL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
-    } else if constexpr (HL > 0) {
-      HoldB<K, HL, LL> Bacc;
-      Bacc.rd = (const gdouble*)(Bin + gb);
-      Bacc.wr = (gdouble*)(Bout + gb);
-      Bacc.lds = (ldouble*)(ldsHold + tid);
-#pragma unroll
-      for (int e = 0; e < HL * K; ++e) Bacc.hold[e] = Bin[gb + (size_t)e * 64];
-#pragma unroll 4
-      for (int e = 0; e < LL * K; ++e) ldsHold[e * 64 + tid] = Bin[gb + (size_t)(HL * K + e) * 64];
-      its = tie ? 0
-                : bfgs_iterations<D, HoldB<K, HL, LL>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
-    } else {
+    {
       WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb)};
       its = tie ? 0
                 : bfgs_iterations<D, WaveB<K>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
