@@ -232,6 +232,15 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
 #pragma unroll
       for (int c = 0; c < D; ++c) Msum.m[r][c] = ((i == 0) ? 0.0 : Msum.m[r][c]) + mPre[i].m[r][c];
   }
+  // the vertex differences the gradient needs (formed here, so only D matrices stay live instead
+  // of the D + 1 vertex monitors; the values are the same)
+  M<D> dmv[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+#pragma unroll
+    for (int r = 0; r < D; ++r)
+#pragma unroll
+      for (int c = 0; c < D; ++c) dmv[j].m[r][c] = mPre[j + 1].m[r][c] - mPre[0].m[r][c];
   M<D> Minv = inverse<D>(Msum);
 #pragma unroll
   for (int r = 0; r < D; ++r)
@@ -320,12 +329,7 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
     for (int c = 0; c < D; ++c) basisComb[c] = 0.0;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-      M<D> dm;
-#pragma unroll
-      for (int r = 0; r < D; ++r)
-#pragma unroll
-        for (int c = 0; c < D; ++c) dm.m[r][c] = mPre[j + 1].m[r][c] - mPre[0].m[r][c];
-      const double tr = trace<D>(mul<D>(dGdM, dm));
+      const double tr = trace<D>(mul<D>(dGdM, dmv[j]));
 #pragma unroll
       for (int c = 0; c < D; ++c) basisComb[c] += Einv.m[j][c] * tr;
     }

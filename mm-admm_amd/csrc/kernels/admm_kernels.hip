@@ -420,8 +420,8 @@ __device__ __forceinline__ void load_row(const BA& B, int i, double (&r)[K]) {
 #pragma unroll
   for (int j = 0; j < K; ++j) r[j] = B.get(i, j);
 }
-// row i of a pass: PIPE > 0 takes it from rn[0] (requested PIPE rows earlier), shifts the queue and
-// requests row i+PIPE
+// row i of a pass: with PIPE > 0 from rn[0] (requested PIPE rows earlier), after which the queue
+// shifts and row i+PIPE is requested.  i may be a run-time value (the rolled update pass).
 template <int K, int PIPE, class BA>
 __device__ __forceinline__ void next_row(const BA& B, int i, double (&row)[K], double (&rn)[PIPE > 0 ? PIPE : 1][K]) {
   if constexpr (PIPE > 0) {
@@ -446,12 +446,11 @@ __device__ __forceinline__ void start_rows(const BA& B, double (&rn)[PIPE > 0 ? 
 // Row i of the BFGS update (src/Mesh.cpp:848):
 // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2.  EXACT = false divides by
 // Markstein's correction (div_mk) and folds the range data into eBy / fin for the caller's check.
-template <int D, bool EXACT, class BA, int K, int PIPE>
-__device__ __forceinline__ void bfgs_update_row(BA& B, int i, double pki, double (&rn)[PIPE][K], const double (&yk)[K],
+template <int D, bool EXACT, class BA, int K>
+__device__ __forceinline__ void bfgs_update_row(BA& B, int i, double pki, const double (&row)[K], const double (&yk)[K],
                                                 const double (&pk)[K], const double (&yB)[K], double c1, double c2,
                                                 double rc2, unsigned& eBy, double& fin) {
-  double row[K], nrow[K], ykr[K];
-  next_row<K, BA::kPipe>(B, i, row, rn);
+  double nrow[K], ykr[K];
   // 3D: (y p^T)_qj is formed again for every row -- laundering y per row stops the compiler
   // from keeping all K*K = 144 products live across the rows (they spilled); 2D keeps its 36
 #pragma unroll
@@ -550,22 +549,27 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     double fin = 0.0;   // stays +0 while every new entry is finite
     B.fresh();
     // B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, row by row
-    start_rows<K, kPipe>(B, rn);
     if constexpr (BA::kRolled) {
       // one row per trip (3D: the unrolled pass is ~60 KB of code, more than the instruction
-      // cache; measured C4 prox 3.12 -> 2.93 ms)
+      // cache; measured C4 prox 3.12 -> 2.93 ms), rows requested kPipe ahead
+      start_rows<K, kPipe>(B, rn);
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         double pki = pk[0];
 #pragma unroll
         for (int k = 1; k < K; ++k) pki = (i == k) ? pk[k] : pki;
-        bfgs_update_row<D, EXACT>(B, i, pki, rn, yk, pk, yB, c1, c2, rc2, eBy, fin);
+        double row[K];
+        next_row<K, kPipe>(B, i, row, rn);
+        bfgs_update_row<D, EXACT>(B, i, pki, row, yk, pk, yB, c1, c2, rc2, eBy, fin);
       }
     } else {
+      start_rows<K, kPipe>(B, rn);
 #pragma unroll
       for (int i = 0; i < K; ++i) {
         MMX_ROW_FENCE(BA);
-        bfgs_update_row<D, EXACT>(B, i, pk[i], rn, yk, pk, yB, c1, c2, rc2, eBy, fin);
+        double row[K];
+        next_row<K, kPipe>(B, i, row, rn);
+        bfgs_update_row<D, EXACT>(B, i, pk[i], row, yk, pk, yB, c1, c2, rc2, eBy, fin);
       }
     }
     MMX_ROW_FENCE(BA);
@@ -838,7 +842,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 // by k_prox_fix from the untouched inputs, as in the 2D kernel.
 template <int D, bool COMP>
 #ifndef MMX_WAVE_OCC
-#define MMX_WAVE_OCC 1  // measured: one wave per SIMD (310 VGPRs) beats two with 65 spilled VGPRs
+#define MMX_WAVE_OCC 1  // measured: one wave per SIMD (310 VGPRs); two (12-53 spills, p/G/DXpU parked in LDS) gain < 2%
 #endif
 __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                      double* __restrict__ zg, double* __restrict__ ug,
