@@ -740,10 +740,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   constexpr int K = D * (D + 1), KK = K * K;
   __shared__ __attribute__((aligned(16))) double lds[KK * (BS + 1)];
   const int tid = threadIdx.x;
-#ifndef MMX_LDS_XCD
-#define MMX_LDS_XCD 0  // measured C3: no gain (2D blocks already share lines within one workgroup)
-#endif
-  const int lb = MMX_LDS_XCD ? logical_block_any() : (int)blockIdx.x;
+  const int lb = (int)blockIdx.x;  // (an XCD-contiguous mapping measured no gain: a 2D workgroup's simplices already share lines)
   const int s0 = lb * BS;
   const int nIn = min(BS, m.nF - s0);
   const bool act = tid < nIn;

@@ -328,11 +328,6 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           if (lane < 32) dma16(ca.dval + slot * 64 + lane * 2, sa + 256);  // 64 diagonals: words 256..383
         }
         dma4(ca.impNeed + slot, sa + 384);  // the same word in every lane
-#ifdef MMX_CHAIN_EXPT  // timing experiment only: publish before the DMA lands (wrong results)
-        if (lane == 0) lds_write(&s_tag[st], t);
-        nextPub = t + 2;
-        continue;
-#endif
         if ((t - nextPub) / 2 + 1 > LAG) {
           const unsigned long long l0 = ca.prof ? clk() : 0;
           wait_vm<NI * LAG>();

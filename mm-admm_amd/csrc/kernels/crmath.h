@@ -36,9 +36,10 @@ MMX_HD double cr_sqrt(double x) { return __builtin_sqrt(x); }
 // instructions instead of the ~11 of an IEEE division (one of them a quarter-rate v_rcp_f64).
 // Exact when c > 0 with c in [2^-100, 2^100] and x = +-0 or |x| in [2^-900, 2^900]: the residual
 // cannot underflow and q is normal.  Signed zeros: x = +0 gives +0, x = -0 gives -0 (e = +0,
-// -e * rc = -0).  The CALLER checks the ranges (mk_exp_ok) and takes the exact path otherwise;
+// -e * rc = -0).  The CALLER checks the ranges (mk_exp) and takes the exact path otherwise;
 // non-finite x gives NaN (the caller's finiteness check catches it).  Checked against IEEE
-// division on 4e8 random and near-midpoint operand pairs (dev note in DESIGN.md §3).
+// division on 4e8 random and near-midpoint operand pairs on the host and on the
+// device by tests/test_gpu_parity.py::test_device_division_by_reciprocal_is_correctly_rounded.
 MMX_HD double div_mk(double x, double c, double rc) {
   const double q = x * rc;
   const double e = cr_fma(q, c, -x);
@@ -312,16 +313,12 @@ MMX_HD double cr_round_t(double x, int num, int den, double hi, double lo, bool&
   const double half = std::fabs(nb - h) * 0.5;
   const double dist = half - std::fabs(l);  // distance of the dd value to the midpoint
   if (dist > std::fabs(h) * 0x1p-95) return h;
-#ifdef MMX_CR_NO_RESOLVE  // performance experiments only: skips the exact tie decision
-  return h;
-#else
   if constexpr (EXACT) {
     return cr_resolve(x, num, den, h, dir);
   } else {
     tie = true;
     return h;
   }
-#endif
 }
 
 MMX_HD double cr_round(double x, int num, int den, double hi, double lo) {
