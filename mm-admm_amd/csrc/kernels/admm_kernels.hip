@@ -353,10 +353,13 @@ __device__ void invertK(double* A) {
 template <int K>
 struct RegB {
   static constexpr bool kRowFence = false;
+  static constexpr int kHeld = 0;
   static constexpr bool kRolled = false;
   static constexpr int kPipe = 0;
   double* b;
   __device__ __forceinline__ double get(int i, int j) const { return b[i * K + j]; }
+  __device__ __forceinline__ double heldRow(int, int) const { return 0.0; }
+  __device__ __forceinline__ void holdRow(int, int, double) const {}
   __device__ __forceinline__ void set(int i, int j, double v) const { b[i * K + j] = v; }
   __device__ __forceinline__ void advance() {}
   __device__ __forceinline__ void fresh() {}
@@ -366,10 +369,13 @@ struct RegB {
 template <int K, int STRIDE = kLdsStride>
 struct LdsB {
   static constexpr bool kRowFence = true;
+  static constexpr int kHeld = 0;
   static constexpr bool kRolled = true;  // the update pass one row per trip (code size; 2D: same speed)
   static constexpr int kPipe = 0;
   double* base;  // &lds[tid], entries strided by STRIDE
   __device__ __forceinline__ double get(int i, int j) const { return base[(i * K + j) * STRIDE]; }
+  __device__ __forceinline__ double heldRow(int, int) const { return 0.0; }
+  __device__ __forceinline__ void holdRow(int, int, double) const {}
   __device__ __forceinline__ void set(int i, int j, double v) const { base[(i * K + j) * STRIDE] = v; }
   __device__ __forceinline__ void advance() {}
   // 2D: keeping the previous pass's K*K = 36 values in registers is cheaper than re-reading LDS
@@ -378,6 +384,9 @@ struct LdsB {
 // address-space-qualified pointers: they keep global (and LDS) accesses as global_/ds_ instructions
 // through the pointer laundering below (a plain pointer out of an asm operand becomes flat)
 typedef __attribute__((address_space(1))) double gdouble;
+#ifndef MMX_WAVE_HELD
+#define MMX_WAVE_HELD 6  // Bkinv rows kept in LDS (36 KB per wave at one wave per SIMD); C4: 4 rows -1.8%, 6 -3.1%
+#endif
 #ifndef MMX_ROW_PIPE
 #define MMX_ROW_PIPE 2  // global Bkinv rows: request row i+2 before working on row i (C4: 1 -> 2 rows -1.6%, 3 spills)
 #endif
@@ -392,9 +401,13 @@ struct WaveB {
   static constexpr bool kRowFence = true;
   static constexpr bool kRolled = true;
   static constexpr int kPipe = MMX_ROW_PIPE;
+  static constexpr int kHeld = MMX_WAVE_HELD;  // rows kept in LDS from pass 1 to passes 2 and 3
   const gdouble* rd;
   gdouble* wr;
+  ldouble* held;  // &lds[lane], kHeld rows, entries strided by 64
   __device__ __forceinline__ double get(int i, int j) const { return rd[(i * K + j) * 64]; }
+  __device__ __forceinline__ double heldRow(int i, int j) const { return held[(i * K + j) * 64]; }
+  __device__ __forceinline__ void holdRow(int i, int j, double v) const { held[(i * K + j) * 64] = v; }
   __device__ __forceinline__ void set(int i, int j, double v) const { wr[(i * K + j) * 64] = v; }
   __device__ __forceinline__ void advance() { rd = wr; }
   // a pass over the matrix re-reads it: an opaque pointer stops the compiler from forwarding the
@@ -420,11 +433,16 @@ __device__ __forceinline__ void load_row(const BA& B, int i, double (&r)[K]) {
 #pragma unroll
   for (int j = 0; j < K; ++j) r[j] = B.get(i, j);
 }
-// row i of a pass: with PIPE > 0 from rn[0] (requested PIPE rows earlier), after which the queue
-// shifts and row i+PIPE is requested.  i may be a run-time value (the rolled update pass).
+// row i of a pass: rows below BA::kHeld (when `held`) from the accessor's LDS copy; the others
+// with PIPE > 0 from rn[0] (requested PIPE rows earlier), after which the queue shifts and row
+// i+PIPE is requested.  i may be a run-time value (the rolled update pass).
 template <int K, int PIPE, class BA>
-__device__ __forceinline__ void next_row(const BA& B, int i, double (&row)[K], double (&rn)[PIPE > 0 ? PIPE : 1][K]) {
-  if constexpr (PIPE > 0) {
+__device__ __forceinline__ void next_row(const BA& B, int i, double (&row)[K], double (&rn)[PIPE > 0 ? PIPE : 1][K],
+                                         bool held = false) {
+  if (held && i < BA::kHeld) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) row[j] = B.heldRow(i, j);
+  } else if constexpr (PIPE > 0) {
 #pragma unroll
     for (int j = 0; j < K; ++j) row[j] = rn[0][j];
 #pragma unroll
@@ -436,11 +454,12 @@ __device__ __forceinline__ void next_row(const BA& B, int i, double (&row)[K], d
     load_row<K>(B, i, row);
   }
 }
-// the first PIPE rows of a pass
+// the first PIPE streamed rows of a pass (from row `first`)
 template <int K, int PIPE, class BA>
-__device__ __forceinline__ void start_rows(const BA& B, double (&rn)[PIPE > 0 ? PIPE : 1][K]) {
+__device__ __forceinline__ void start_rows(const BA& B, double (&rn)[PIPE > 0 ? PIPE : 1][K], int first = 0) {
 #pragma unroll
-  for (int d = 0; d < PIPE; ++d) load_row<K>(B, d, rn[d]);
+  for (int d = 0; d < PIPE; ++d)
+    if (first + d < K) load_row<K>(B, first + d, rn[d]);
 }
 
 // Row i of the BFGS update (src/Mesh.cpp:848):
@@ -497,6 +516,11 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
       MMX_ROW_FENCE(BA);
       double row[K];
       next_row<K, kPipe>(B, i, row, rn);
+      if constexpr (BA::kHeld > 0) {  // the first kHeld rows wait in LDS for passes 2 and 3
+        if (i < BA::kHeld)
+#pragma unroll
+          for (int j = 0; j < K; ++j) B.holdRow(i, j, row[j]);
+      }
       double sacc = (-row[0]) * G[0];
 #pragma unroll
       for (int j = 1; j < K; ++j) sacc += (-row[j]) * G[j];
@@ -526,12 +550,12 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.fresh();
     // one pass over B: By_i = sum_j B_ij y_j, yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij
     double yBy = 0.0, yB[K];
-    start_rows<K, kPipe>(B, rn);
+    start_rows<K, kPipe>(B, rn, BA::kHeld);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
       double row[K];
-      next_row<K, kPipe>(B, i, row, rn);
+      next_row<K, kPipe>(B, i, row, rn, true);
       double by = row[0] * yk[0];
 #pragma unroll
       for (int j = 1; j < K; ++j) by += row[j] * yk[j];
@@ -552,14 +576,14 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     if constexpr (BA::kRolled) {
       // one row per trip (3D: the unrolled pass is ~60 KB of code, more than the instruction
       // cache; measured C4 prox 3.12 -> 2.93 ms), rows requested kPipe ahead
-      start_rows<K, kPipe>(B, rn);
+      start_rows<K, kPipe>(B, rn, BA::kHeld);
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         double pki = pk[0];
 #pragma unroll
         for (int k = 1; k < K; ++k) pki = (i == k) ? pk[k] : pki;
         double row[K];
-        next_row<K, kPipe>(B, i, row, rn);
+        next_row<K, kPipe>(B, i, row, rn, true);
         bfgs_update_row<D, EXACT>(B, i, pki, row, yk, pk, yB, c1, c2, rc2, eBy, fin);
       }
     } else {
@@ -846,6 +870,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
                                                      const double* Bin, double* Bout, double* __restrict__ partials,
                                                      int useCache) {
   constexpr int K = D * (D + 1), KK = K * K;
+  __shared__ double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 1];
   const int tid = threadIdx.x;
 #ifndef MMX_WAVE_XCD
 #define MMX_WAVE_XCD 1  // measured C4: prox 3.42 -> 3.29 ms (neighbouring tets share x and monitor-grid lines in one L2)
@@ -892,7 +917,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     const size_t gb = (size_t)lb * KK * 64 + tid;
     int its;
     {
-      WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb)};
+      WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsHeld + tid)};
       its = tie ? 0
                 : bfgs_iterations<D, WaveB<K>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     }
