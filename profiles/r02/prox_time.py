@@ -19,5 +19,5 @@ st = E.stats()
 X = E.get("x")
 import hashlib, numpy as np
 h = hashlib.sha1(np.ascontiguousarray(X).tobytes()).hexdigest()[:12] if X is not None else '-'
-print(json.dumps({"wl": os.environ.get("WL", "c4"), "lib": os.environ.get("MMADMM_LIB", "default"), "prox_ms": round(st["t_prox_ms"] / max(st["n_prox"], 1), 4),
+print(json.dumps({"wl": os.environ.get("WL", "c4"), "lib": os.environ.get("MMADMM_LIB", "default"), "prox_ms": round(st["t_prox_ms"] / max(st["n_prox"], 1), 4), "xup_ms": round(st["t_xupdate_ms"] / max(st["n_xupdate"], 1), 4),
                   "it_s": round(30 / el, 2), "hash": h}))
