@@ -20,6 +20,9 @@ struct DeviceMesh {
   const int* inc_off;     // offset s*K + n*D of each local incident slot; -1-r for a slot of another
                           // rank: its D values are row r of `remote` (element partition)
   const double* remote;   // gathered interface-slot values of the other ranks (or nullptr)
+  // the x-update's term w (w (z - u)) of every local slot, written by the prox in the slot layout
+  // of z: the x-update then gathers D values per slot instead of 2 D (nullptr: it gathers z and u)
+  double* tslot;
   double* gcache;         // per simplex K+1: unregularised gradient and energy at the current z
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
@@ -57,7 +60,7 @@ void launch_predict(const DeviceMesh<D>& m, int mode, const double* gs, double* 
 template <int D>
 void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar,
                     const double* z, const double* u, double* x, double* partials, int* nblocks,
-                    bool resid, hipStream_t st);
+                    bool resid, hipStream_t st, bool useTslot = false);
 // useCache: z is unchanged since the previous prox, whose last blockGrad left the unregularised
 // gradient in m.gcache; the entry blockGrad then reduces to adding the regulariser.
 // 3D: pad[r 10 + n] = vals[r 9 + n], pad[r 10 + 9] = 0 (rebuilt whenever vals changes)

@@ -135,6 +135,17 @@ __device__ __forceinline__ void loadXi(const DeviceMesh<D>& m, const int (&f)[D 
   if (m.compMesh) gatherX<D>(m.Vc, f, xi);
 }
 
+// the x-update's term of the simplex's slots (DeviceMesh::tslot, the layout of z): the same
+// expression the x-update forms from z and u (bit-identical)
+template <int D>
+__device__ __forceinline__ void write_tslot(const DeviceMesh<D>& m, int s, const double* z, const double* u) {
+  if (!m.tslot) return;
+  constexpr int K = D * (D + 1);
+  double* ts = m.tslot + (size_t)s * K;
+#pragma unroll
+  for (int i = 0; i < K; ++i) ts[i] = m.w * (m.w * (z[i] - u[i]));
+}
+
 // z = D x (Dmat * x, src/MeshIntegrator.cpp:121,126): exact gather into simplex copies
 template <int D>
 __global__ void __launch_bounds__(kBlock) k_gather_z(DeviceMesh<D> m, const double* __restrict__ x,
@@ -214,7 +225,7 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
 // A node's incident slots are taken 8 at a time: their offsets, then all their z and u values
 // are requested before the first is added (branch-free: lanes past the end re-read the last
 // slot, a slot of another rank reads its gathered row), then summed in ascending order.
-template <int D, bool RESID>
+template <int D, bool RESID, bool TS>
 __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
                                                      const double* __restrict__ xBar,
                                                      const double* __restrict__ z,
@@ -243,20 +254,30 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         const bool loc = off[j] >= 0;
-        const double* pz = loc ? z + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
-        const double* pu = loc ? u + off[j] : pz;
+        if constexpr (TS) {  // the prox's terms; another rank's slot from `remote`
+          const double* pt = loc ? m.tslot + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
 #pragma unroll
-        for (int c = 0; c < D; ++c) {
-          zv[j][c] = pz[c];
-          uv[j][c] = pu[c];
+          for (int c = 0; c < D; ++c) zv[j][c] = pt[c];
+        } else {
+          const double* pz = loc ? z + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
+          const double* pu = loc ? u + off[j] : pz;
+#pragma unroll
+          for (int c = 0; c < D; ++c) {
+            zv[j][c] = pz[c];
+            uv[j][c] = pu[c];
+          }
         }
       }
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         if (t0 + j < e) {
 #pragma unroll
-          for (int c = 0; c < D; ++c)  // another rank's slot: the term formed there (launch_pack_export mode 0)
-            acc[c] += (off[j] >= 0) ? sc.w * (sc.w * (zv[j][c] - uv[j][c])) : zv[j][c];
+          for (int c = 0; c < D; ++c) {  // another rank's slot: the term formed there (launch_pack_export mode 0)
+            if constexpr (TS)
+              acc[c] += zv[j][c];
+            else
+              acc[c] += (off[j] >= 0) ? sc.w * (sc.w * (zv[j][c] - uv[j][c])) : zv[j][c];
+          }
         }
       }
     }
@@ -697,13 +718,16 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
   RegB<K> Bacc{B};
   const int its = bfgs_iterations<D>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc);
   double dual2 = 0.0;
+  double un[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     zs[i] = z[i];
-    us[i] = dx[i] - z[i];  // uBar = DXpU - z
+    un[i] = dx[i] - z[i];  // uBar = DXpU - z
+    us[i] = un[i];
     const double d = z[i] - zold[i];
     dual2 += d * d;
   }
+  write_tslot<D>(m, s, z, un);
 #pragma unroll
   for (int i = 0; i < K * K; ++i) Bout[bidx<D>(s, i)] = B[i];
   pv[0] = Ihsave;
@@ -837,11 +861,14 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     return;
   }
   if (act) {
+    double un[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       zs[i] = z[i];
-      us[i] = dx[i] - z[i];  // uBar = DXpU - z
+      un[i] = dx[i] - z[i];  // uBar = DXpU - z
+      us[i] = un[i];
     }
+    write_tslot<D>(m, s, z, un);
   }
 #pragma unroll 4
   for (int e = tid * 2; e < tot; e += BS * 2) {
@@ -939,11 +966,14 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     return;
   }
   if (act) {
+    double un[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       zs[i] = z[i];
-      us[i] = dx[i] - z[i];  // uBar = DXpU - z
+      un[i] = dx[i] - z[i];  // uBar = DXpU - z
+      us[i] = un[i];
     }
+    write_tslot<D>(m, s, z, un);
   }
   block_partials<6, 64>(pv, partials, lb);
 }
@@ -1275,15 +1305,23 @@ void launch_predict(const DeviceMesh<D>& m, int mode, const double* gs, double* 
 }
 template <int D>
 void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar, const double* z,
-                    const double* u, double* x, double* partials, int* nblocks, bool resid, hipStream_t st) {
+                    const double* u, double* x, double* partials, int* nblocks, bool resid, hipStream_t st,
+                    bool useTslot) {
   *nblocks = nblk_xcd(m.nP);
   if (m.nP == 0) return;
-  if (resid)
-    hipLaunchKernelGGL((k_xupdate<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
-                       partials, xcd_map());
+  const bool ts = useTslot && m.tslot;
+#define MMX_XU(R, T)                                                                                               \
+  hipLaunchKernelGGL((k_xupdate<D, R, T>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x, partials, \
+                     xcd_map())
+  if (resid && ts)
+    MMX_XU(true, true);
+  else if (resid)
+    MMX_XU(true, false);
+  else if (ts)
+    MMX_XU(false, true);
   else
-    hipLaunchKernelGGL((k_xupdate<D, false>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
-                       partials, xcd_map());
+    MMX_XU(false, false);
+#undef MMX_XU
 }
 __global__ void __launch_bounds__(kBlock) k_pad_rows(const double* __restrict__ vals, long long rows,
                                                       double* __restrict__ pad) {
@@ -1443,7 +1481,7 @@ void launch_add_inplace(int n, double* x, const double* dx, hipStream_t st) {
   template void launch_predict<D>(const DeviceMesh<D>&, int, const double*, double*, double*, double*,   \
                                   double, hipStream_t);                                                 \
   template void launch_xupdate<D>(const DeviceMesh<D>&, const StepScalars&, const double*, const double*, \
-                                  const double*, double*, double*, int*, bool, hipStream_t);            \
+                                  const double*, double*, double*, int*, bool, hipStream_t, bool);      \
   template void launch_prox<D>(const DeviceMesh<D>&, bool, bool, double, const double*, double*, double*,      \
                                const double*,                                                                \
                                double*, double*, int*, hipStream_t);                                    \

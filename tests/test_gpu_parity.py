@@ -207,3 +207,21 @@ def test_long_run_bitwise(dim, tol):
         G.step(5, tol)
     np.testing.assert_array_equal(G.get("x"), O.get("x"))
     np.testing.assert_array_equal(G.get("z"), O.get("z"))
+
+
+@pytest.mark.parametrize("dim,ts", [(2, "1"), (3, "0")])
+def test_xupdate_slot_terms_bitwise(dim, ts, monkeypatch):
+    """The x-update from the prox's slot terms w(w(z - u)) (DeviceMesh::tslot, on by default in
+    3D) and from z and u (the 2D default) give the same bits as the oracle: each engine is run
+    with the other choice forced (MMX_TSLOT)."""
+    monkeypatch.setenv("MMX_TSLOT", ts)
+    if dim == 2:
+        mesh, mon, rho = _hexdisc(30), 2, 100.0
+    else:
+        mesh, mon, rho = oracle_py.Mesh.rect(3, 8), 6, 2000.0
+    O, G = make_pair(mesh, mon, 0.025, 0.5, rho, False, 1, 1)
+    for tol in (-1.0, 1e-3, -1.0):
+        O.step(5, tol)
+        G.step(5, tol)
+    np.testing.assert_array_equal(G.get("x"), O.get("x"))
+    np.testing.assert_array_equal(G.get("z"), O.get("z"))
