@@ -566,8 +566,12 @@ class Engine final : public EngineBase {
     // z and u once each, xBar and invdiag, writes x.
     const double nF = nF_, nP = nP_;
     // + the gradient cache: K+1 doubles read at entry and written by the last BFGS iteration
-    s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2 + 8.0 * (K + 1) * 2) + nP * 8.0 * D;
-    s->xupdate_bytes = 4.0 * (nP + 1) + 4.0 * (D + 1) * nF + 16.0 * K * nF + 8.0 * D * nP * 2 + 8.0 * nP;
+    // with the slot terms (tslot, 3D) the prox also writes K doubles per simplex and the x-update
+    // reads those instead of z and u
+    const double ts = tslotOn_ ? 1.0 : 0.0;
+    s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2 + 8.0 * (K + 1) * 2 + ts * 8.0 * K) +
+                    nP * 8.0 * D;
+    s->xupdate_bytes = 4.0 * (nP + 1) + 4.0 * (D + 1) * nF + (16.0 - 8.0 * ts) * K * nF + 8.0 * D * nP * 2 + 8.0 * nP;
   }
 
   void resetStats() override {
