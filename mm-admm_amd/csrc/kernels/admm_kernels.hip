@@ -375,6 +375,7 @@ template <int K>
 struct RegB {
   static constexpr bool kRowFence = false;
   static constexpr int kHeld = 0;
+  static constexpr bool kCarry = false;
   static constexpr bool kRolled = false;
   static constexpr int kPipe = 0;
   double* b;
@@ -391,6 +392,7 @@ template <int K, int STRIDE = kLdsStride>
 struct LdsB {
   static constexpr bool kRowFence = true;
   static constexpr int kHeld = 0;
+  static constexpr bool kCarry = false;
   static constexpr bool kRolled = true;  // the update pass one row per trip (code size; 2D: same speed)
   static constexpr int kPipe = 0;
   double* base;  // &lds[tid], entries strided by STRIDE
@@ -405,6 +407,9 @@ struct LdsB {
 // address-space-qualified pointers: they keep global (and LDS) accesses as global_/ds_ instructions
 // through the pointer laundering below (a plain pointer out of an asm operand becomes flat)
 typedef __attribute__((address_space(1))) double gdouble;
+#ifndef MMX_WAVE_CARRY
+#define MMX_WAVE_CARRY 1  // C4: -1.5..2% (the first streamed rows of passes 2 and 3 ready when they start)
+#endif
 #ifndef MMX_WAVE_HELD
 #define MMX_WAVE_HELD 6  // Bkinv rows kept in LDS (36 KB per wave at one wave per SIMD); C4: 4 rows -1.8%, 6 -3.1%
 #endif
@@ -423,6 +428,7 @@ struct WaveB {
   static constexpr bool kRolled = true;
   static constexpr int kPipe = MMX_ROW_PIPE;
   static constexpr int kHeld = MMX_WAVE_HELD;  // rows kept in LDS from pass 1 to passes 2 and 3
+  static constexpr bool kCarry = MMX_WAVE_CARRY;
   const gdouble* rd;
   gdouble* wr;
   ldouble* held;  // &lds[lane], kHeld rows, entries strided by 64
@@ -531,6 +537,10 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.fresh();
     double pk[K];
     double rn[kPipe > 0 ? kPipe : 1][K];  // kPipe rows requested ahead of the row being worked on
+    // kCarry: the first kPipe streamed rows of a pass are kept in registers from the previous pass
+    // (the next pass starts without waiting for their loads)
+    constexpr bool kCarry = BA::kCarry && kPipe > 0;
+    double rc[kPipe > 0 ? kPipe : 1][K];
     start_rows<K, kPipe>(B, rn);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -541,6 +551,11 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
         if (i < BA::kHeld)
 #pragma unroll
           for (int j = 0; j < K; ++j) B.holdRow(i, j, row[j]);
+      }
+      if constexpr (kCarry) {
+        if (i >= BA::kHeld && i < BA::kHeld + kPipe)
+#pragma unroll
+          for (int j = 0; j < K; ++j) rc[i - BA::kHeld][j] = row[j];
       }
       double sacc = (-row[0]) * G[0];
 #pragma unroll
@@ -571,12 +586,24 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.fresh();
     // one pass over B: By_i = sum_j B_ij y_j, yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij
     double yBy = 0.0, yB[K];
-    start_rows<K, kPipe>(B, rn, BA::kHeld);
+    if constexpr (kCarry) {
+#pragma unroll
+      for (int d = 0; d < kPipe; ++d)
+#pragma unroll
+        for (int j = 0; j < K; ++j) rn[d][j] = rc[d][j];
+    } else {
+      start_rows<K, kPipe>(B, rn, BA::kHeld);
+    }
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
       double row[K];
       next_row<K, kPipe>(B, i, row, rn, true);
+      if constexpr (kCarry) {
+        if (i >= BA::kHeld && i < BA::kHeld + kPipe)
+#pragma unroll
+          for (int j = 0; j < K; ++j) rc[i - BA::kHeld][j] = row[j];
+      }
       double by = row[0] * yk[0];
 #pragma unroll
       for (int j = 1; j < K; ++j) by += row[j] * yk[j];
@@ -597,7 +624,14 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     if constexpr (BA::kRolled) {
       // one row per trip (3D: the unrolled pass is ~60 KB of code, more than the instruction
       // cache; measured C4 prox 3.12 -> 2.93 ms), rows requested kPipe ahead
-      start_rows<K, kPipe>(B, rn, BA::kHeld);
+      if constexpr (kCarry) {
+#pragma unroll
+        for (int d = 0; d < kPipe; ++d)
+#pragma unroll
+          for (int j = 0; j < K; ++j) rn[d][j] = rc[d][j];
+      } else {
+        start_rows<K, kPipe>(B, rn, BA::kHeld);
+      }
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         double pki = pk[0];
