@@ -156,6 +156,14 @@ int mmadmm_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, doub
 /* compact_mask = 0 keeps the reference's pre-compaction mask indexing (MeshUtils.h:487) */
 int mmadmm_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int btype,
                            int compact_mask, mmadmm_mesh* out);
+/* utils::meshFromLevelSetFun 3D with spherePhi (src/MeshUtils.h:540-667, main.cpp:87-97): the cube
+ * cut to the tetrahedra with a vertex inside the sphere r = 0.4 centred (0.5, 0.5, 0.5), outside
+ * vertices moved by interpolateBoundaryLocation 3D (388-402), nodes numbered as the reference's
+ * pntMap (descending original id).  The reference never hands its result back (663-666 reassign
+ * pointer copies); here it is returned.  compact_mask = 0: the reference's pre-compaction mask
+ * indexing (595-597); 1: the mask remapped to the new numbering. */
+int mmadmm_mesh_levelset3d(int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za,
+                           double zb, int btype, int compact_mask, mmadmm_mesh* out);
 /* hexagonal disc of radius r centred (cx, cy): 3N(N+1)+1 nodes, 6N^2 triangles, rim FIXED */
 /* setUpShoulderExperiment (main.cpp:403-630): rect mesh minus the upper (x, y[, z]) quadrant's
  * simplices, re-marked boundary, interior vertices moved by up to h/10 in a random direction drawn with

@@ -114,7 +114,9 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   std::vector<long long> doneAt(n, 0);  // iteration (band-relative + offset) a row is published
   std::vector<long long> offset(S.nbands, 0);
   std::vector<std::vector<int>> srcBands(S.nbands);  // bands each band imports from
-  int RI = 256;
+  // the importer runs at most RI imports ahead of the compute wave: it takes the whole ring (a
+  // band importing hundreds of values per iteration needs many iterations of run-ahead)
+  const int RI = kChainImpMax;
   for (int b = 0; b < S.nbands; ++b) {
     const int c0 = b * L, nl = std::min(L, C - c0);
     first.clear();
@@ -181,10 +183,6 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
         if (first[ord[q]] <= last[ord[q - ri]]) return false;
       return true;
     };
-    while (!fits(RI) && RI < kChainImpMax) RI *= 2;
-    // the importer runs at most RI imports ahead of the compute wave: take the whole ring (a
-    // band importing hundreds of values per iteration needs many iterations of run-ahead)
-    RI = kChainImpMax;
     if (!fits(RI)) {
       S.why = "import ring too small for band " + std::to_string(b);
       return S;

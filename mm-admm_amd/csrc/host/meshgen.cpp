@@ -5,6 +5,8 @@
 //   mmadmm_mesh_levelset2d  utils::meshFromLevelSetFun 2D with circlePhi (src/MeshUtils.h:404-538,
 //                           main.cpp:33-40); the O(nP*nF) remap loop (510-518) is replaced by an
 //                           O(N) ascending-rank compaction with the same result
+//   mmadmm_mesh_levelset3d  utils::meshFromLevelSetFun 3D with spherePhi (src/MeshUtils.h:540-667,
+//                           main.cpp:87-97), O(N), with the reference's hand-back defect repaired
 //   mmadmm_mesh_hexdisc     a well-shaped disc mesh (not in the reference)
 //   mmadmm_mesh_shoulder    setUpShoulderExperiment's mesh (main.cpp:403-630): the rect mesh without
 //                           the simplices whose centroid lies in the upper (x, y[, z]) quadrant, its
@@ -195,6 +197,78 @@ void levelset2d(int nx, int ny, double xa, double xb, double ya, double yb, int 
     if (std::abs(circlePhi(m.Vp[(size_t)p * 2], m.Vp[(size_t)p * 2 + 1])) < EPS) m.mask[p] = kFixed;
 }
 
+double spherePhi(double x, double y, double z) {  // main.cpp:87-97 (squared form)
+  const double r = 0.4, cx = 0.5, cy = 0.5, cz = 0.5;
+  const double xval = (x - cx), yval = (y - cy), zval = (z - cz);
+  return xval * xval + yval * yval + zval * zval - r * r;
+}
+
+// utils::meshFromLevelSetFun 3D (src/MeshUtils.h:540-667) with spherePhi (main.cpp:363), O(N):
+// the cube cut to the tetrahedra with a vertex inside (phi <= -EPS), the used vertices with
+// phi > -EPS moved by interpolateBoundaryLocation 3D (388-402: central-difference normal,
+// h = 2 sqrt(eps), p - phi(p) n) and marked bType, then the used vertices numbered in DESCENDING
+// original id (the reference's pntMap, 645-651) with F remapped alike.  Repaired:
+// the reference hands nothing back -- `delete Vp; Vp = Vpnew;` (663-666) reassigns its own
+// pointer copies, so the caller's arrays are left deleted -- and it does not compact the mask;
+// compact = true remaps the mask to the new numbering (false: the reference's old-id indexing).
+void levelset3d(int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za, double zb, int bType,
+                bool compact, MeshBuf& m) {
+  const double EPS = 1e-12;
+  MeshBuf g;
+  rect3d(nx, ny, nz, (int)xa, (int)xb, (int)ya, (int)yb, (int)za, (int)zb, bType, g);
+  for (auto& v : g.mask) v = kInterior;
+  const int nF0 = g.nF(), nP0 = g.nP();
+  std::vector<double> phi(nP0);
+  for (int p = 0; p < nP0; ++p) phi[p] = spherePhi(g.Vp[(size_t)p * 3], g.Vp[(size_t)p * 3 + 1], g.Vp[(size_t)p * 3 + 2]);
+  std::vector<int> keep;
+  keep.reserve(nF0);
+  for (int s = 0; s < nF0; ++s) {  // drop the tetrahedra with every vertex outside
+    bool out = true;
+    for (int j = 0; j < 4; ++j) out = out && phi[g.F[(size_t)s * 4 + j]] > -EPS;
+    if (!out) keep.push_back(s);
+  }
+  std::vector<char> used(nP0, 0);
+  for (int s : keep)
+    for (int j = 0; j < 4; ++j) used[g.F[(size_t)s * 4 + j]] = 1;
+  const double h = 2.0 * sqrt(2.220446049250313080847e-16);
+  for (int p = 0; p < nP0; ++p) {
+    if (!used[p] || !(phi[p] > -EPS)) continue;
+    double* x = &g.Vp[(size_t)p * 3];
+    double n[3];
+    n[0] = (spherePhi(x[0] + h, x[1], x[2]) - spherePhi(x[0] - h, x[1], x[2])) / (2.0 * h);
+    n[1] = (spherePhi(x[0], x[1] + h, x[2]) - spherePhi(x[0], x[1] - h, x[2])) / (2.0 * h);
+    n[2] = (spherePhi(x[0], x[1], x[2] + h) - spherePhi(x[0], x[1], x[2] - h)) / (2.0 * h);
+    const double sq = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];  // Eigen normalize()
+    if (sq > 0) {
+      const double nrm = sqrt(sq);
+      for (int c = 0; c < 3; ++c) n[c] = n[c] / nrm;
+    }
+    const double ph = phi[p];
+    for (int c = 0; c < 3; ++c) x[c] = x[c] - ph * n[c];
+    g.mask[p] = bType;
+  }
+  int cnt = 0;
+  for (int p = 0; p < nP0; ++p) cnt += used[p];
+  std::vector<int> rank(nP0, -1);
+  for (int p = nP0 - 1, r = 0; p >= 0; --p)
+    if (used[p]) rank[p] = r++;
+  m.dim = 3;
+  m.Vp.resize((size_t)cnt * 3);
+  for (int p = 0; p < nP0; ++p)
+    if (used[p])
+      for (int c = 0; c < 3; ++c) m.Vp[(size_t)rank[p] * 3 + c] = g.Vp[(size_t)p * 3 + c];
+  m.F.resize(keep.size() * 4);
+  for (size_t i = 0; i < keep.size(); ++i)
+    for (int j = 0; j < 4; ++j) m.F[i * 4 + j] = rank[g.F[(size_t)keep[i] * 4 + j]];
+  if (compact) {
+    m.mask.assign(cnt, kInterior);
+    for (int p = 0; p < nP0; ++p)
+      if (used[p]) m.mask[rank[p]] = g.mask[p];
+  } else {
+    m.mask = g.mask;
+  }
+}
+
 void hexdisc(int N, double r, double cx, double cy, int bType, MeshBuf& m) {
   const long nP = 3L * N * (N + 1) + 1;
   m.dim = 2;
@@ -355,6 +429,16 @@ int mmadmm_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, doub
     if (!out || nx < 1 || ny < 1) throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_levelset2d: bad arguments");
     auto* m = new MeshBuf();
     mmx::levelset2d(nx, ny, xa, xb, ya, yb, btype, compact_mask != 0, *m);
+    *out = reinterpret_cast<mmadmm_mesh>(m);
+  });
+}
+
+int mmadmm_mesh_levelset3d(int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za, double zb,
+                           int btype, int compact_mask, mmadmm_mesh* out) {
+  return guarded([&] {
+    if (!out || nx < 1 || ny < 1 || nz < 1) throw Error(MMADMM_ERR_INVALID, "mmadmm_mesh_levelset3d: bad arguments");
+    auto* m = new MeshBuf();
+    mmx::levelset3d(nx, ny, nz, xa, xb, ya, yb, za, zb, btype, compact_mask != 0, *m);
     *out = reinterpret_cast<mmadmm_mesh>(m);
   });
 }

@@ -122,7 +122,9 @@ std::vector<int> partition_owners(int D, int nP, const double* Xp, int nF, const
     const long long want = cut - P.b, tolr = std::max<long long>(1, (P.e - P.b) / 50);
     int pick = -1;
     for (size_t j = 0; j < cand.size(); ++j) {
-      if (left[j] <= 0 || left[j] >= P.e - P.b || std::llabs(left[j] - want) > tolr) continue;
+      // each side keeps at least one simplex per rank it goes to (the proportional cut does too,
+      // since every part holds at least as many simplices as ranks), so no rank ends up empty
+      if (left[j] < nlo || (P.e - P.b) - left[j] < P.nr - nlo || std::llabs(left[j] - want) > tolr) continue;
       if (pick < 0 || strad[j] < strad[pick] ||
           (strad[j] == strad[pick] && std::llabs(left[j] - want) < std::llabs(left[pick] - want)))
         pick = (int)j;

@@ -46,7 +46,9 @@ MMX_HD double div_mk(double x, double c, double rc) {
   return cr_fma(-e, rc, q);
 }
 // frexp exponent of x biased so that (unsigned) <= 2*lim - 1 <=> x = 0 or |x| in [2^-lim, 2^lim]
-// (frexp: |x| in [2^(e-1), 2^e); 0 for zero, inf and NaN)
+// (frexp: |x| in [2^(e-1), 2^e); 0 for zero, inf and NaN).  Non-finite x therefore counts as IN
+// range: callers must check finiteness themselves (bfgs_update_row folds every new entry into its
+// `fin` check, which a NaN or infinite operand reaches).
 MMX_HD unsigned mk_exp(double x, int lim) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return (unsigned)(__builtin_amdgcn_frexp_exp(x) + (lim - 1));

@@ -100,6 +100,8 @@ def lib():
                                                                                  ctypes.POINTER(ctypes.c_void_p)]
     L.mmadmm_mesh_levelset2d.argtypes = [ctypes.c_int] * 2 + [ctypes.c_double] * 4 + [
         ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.mmadmm_mesh_levelset3d.argtypes = [ctypes.c_int] * 3 + [ctypes.c_double] * 6 + [
+        ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.mmadmm_mesh_hexdisc.argtypes = [ctypes.c_int] + [ctypes.c_double] * 3 + [ctypes.c_int,
                                                                                ctypes.POINTER(ctypes.c_void_p)]
     L.mmadmm_mesh_shoulder.argtypes = [ctypes.c_int] * 4 + [ctypes.c_double] * 6 + [ctypes.c_int,
@@ -212,6 +214,14 @@ class MeshData:
     def levelset2d(n, xa=0.0, xb=1.0, ya=0.0, yb=1.0, btype=BOUNDARY_FIXED, compact_mask=True):
         h = ctypes.c_void_p()
         _check(lib().mmadmm_mesh_levelset2d(n, n, xa, xb, ya, yb, btype, int(compact_mask), ctypes.byref(h)))
+        return MeshData._take(h)
+
+    @staticmethod
+    def levelset3d(n, xa=0.0, xb=1.0, ya=0.0, yb=1.0, za=0.0, zb=1.0, btype=BOUNDARY_FIXED, compact_mask=True):
+        """utils::meshFromLevelSetFun 3D with spherePhi (src/MeshUtils.h:540-667, main.cpp:87-97)."""
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_mesh_levelset3d(n, n, n, xa, xb, ya, yb, za, zb, btype, int(compact_mask),
+                                            ctypes.byref(h)))
         return MeshData._take(h)
 
     @staticmethod

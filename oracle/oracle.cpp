@@ -30,6 +30,8 @@
 #include <cstring>
 #include <fstream>
 #include <limits>
+#include <map>
+#include <set>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -501,6 +503,91 @@ static void genLevelSet2D(int nx, int ny, double xa, double xb, double ya, doubl
   for (int p = 0; p < cnt; ++p) {
     const double phi = circlePhi(m.Vp[p * 2], m.Vp[p * 2 + 1]);
     if (std::abs(phi) < EPS) m.mask[p] = BOUNDARY_FIXED;
+  }
+}
+
+static double spherePhi(double x, double y, double z) {  // main.cpp:87-97 (squared form, not a distance)
+  const double r = 0.4, cx = 0.5, cy = 0.5, cz = 0.5;
+  const double xv = (x - cx), yv = (y - cy), zv = (z - cz);
+  return xv * xv + yv * yv + zv * zv - r * r;
+}
+
+// MeshUtils.h:540-667 (3D meshFromLevelSetFun with spherePhi, main.cpp:363) restated, with the two
+// defects that make the reference's 3D generator unusable repaired:
+//  * its result never reaches the caller: `delete Vc; Vc = Vcnew; delete Vp; Vp = Vpnew;`
+//    (663-666) reassigns the function's own pointer copies, leaving the caller's Vp/Vc deleted
+//    (dangling) while F has been remapped -- here Vp and F are the remapped mesh;
+//  * the mask is not compacted (written at the pre-compaction ids, 595-597); compactMask != 0
+//    remaps it (the evident intent, as for 2D), 0 keeps the reference's indexing.
+// The node numbering is the reference's: pntMap maps the i-th LARGEST used id to i (645-651, the
+// reversed rank) and F is remapped with it, consistently with Vp.  No final |phi| < EPS pass (the
+// 2D generator has one, 531-537; the 3D one does not).  The interior-side projection is
+// interpolateBoundaryLocation 3D (388-402): a central-difference gradient of spherePhi with
+// h = 2 sqrt(eps), normalised (Eigen normalize: divided by sqrt of the squared norm), and
+// p - phi(p) n -- with the squared-distance phi this moves outside points towards, not onto,
+// the sphere.
+static void genLevelSet3D(int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za,
+                          double zb, int bType, int compactMask, MeshData& m) {
+  const double EPS = 1e-12;
+  MeshData g;
+  genRect(3, nx, ny, nz, xa, xb, ya, yb, za, zb, bType, g);
+  for (auto& v : g.mask) v = INTERIOR;
+  const int nF0 = g.nF();
+  auto phiAt = [&](int v) { return spherePhi(g.Vp[v * 3], g.Vp[v * 3 + 1], g.Vp[v * 3 + 2]); };
+  std::vector<int> idsToBeRemoved;
+  for (int s = 0; s < nF0; ++s) {
+    const int* f = &g.F[s * 4];
+    const double p0 = phiAt(f[0]), p1 = phiAt(f[1]), p2 = phiAt(f[2]), p3 = phiAt(f[3]);
+    if (p0 > -EPS && p1 > -EPS && p2 > -EPS && p3 > -EPS) idsToBeRemoved.push_back(s);
+  }
+  std::vector<int> Fk;  // removeRow in descending id order == the others kept in order
+  {
+    size_t r = 0;
+    for (int s = 0; s < nF0; ++s) {
+      if (r < idsToBeRemoved.size() && idsToBeRemoved[r] == s) {
+        ++r;
+        continue;
+      }
+      Fk.insert(Fk.end(), g.F.begin() + (size_t)s * 4, g.F.begin() + (size_t)(s + 1) * 4);
+    }
+  }
+  std::set<int> usedPnts(Fk.begin(), Fk.end());
+  const double h = 2.0 * sqrt(std::numeric_limits<double>::epsilon());
+  for (int p : usedPnts) {
+    double x[3] = {g.Vp[p * 3], g.Vp[p * 3 + 1], g.Vp[p * 3 + 2]};
+    if (spherePhi(x[0], x[1], x[2]) > -EPS) {
+      double gr[3];
+      gr[0] = (spherePhi(x[0] + h, x[1], x[2]) - spherePhi(x[0] - h, x[1], x[2])) / (2.0 * h);
+      gr[1] = (spherePhi(x[0], x[1] + h, x[2]) - spherePhi(x[0], x[1] - h, x[2])) / (2.0 * h);
+      gr[2] = (spherePhi(x[0], x[1], x[2] + h) - spherePhi(x[0], x[1], x[2] - h)) / (2.0 * h);
+      const double sq = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2];
+      if (sq > 0) {
+        const double nrm = sqrt(sq);
+        for (int c = 0; c < 3; ++c) gr[c] = gr[c] / nrm;
+      }
+      const double ph = spherePhi(x[0], x[1], x[2]);
+      for (int c = 0; c < 3; ++c) x[c] = x[c] - ph * gr[c];
+      g.mask[p] = bType;
+    }
+    for (int c = 0; c < 3; ++c) g.Vp[p * 3 + c] = x[c];
+  }
+  std::vector<int> pntsSorted(usedPnts.begin(), usedPnts.end());
+  std::map<int, int> pntMap;
+  const int cnt = (int)pntsSorted.size();
+  m.dim = 3;
+  m.Vp.resize((size_t)cnt * 3);
+  for (int i = 0; i < cnt; i++) {
+    const int off = pntsSorted[cnt - i - 1];
+    pntMap[off] = i;
+    for (int c = 0; c < 3; ++c) m.Vp[(size_t)i * 3 + c] = g.Vp[(size_t)off * 3 + c];
+  }
+  m.F.resize(Fk.size());
+  for (size_t e = 0; e < Fk.size(); ++e) m.F[e] = pntMap[Fk[e]];
+  if (compactMask) {
+    m.mask.assign(cnt, INTERIOR);
+    for (const auto& kv : pntMap) m.mask[kv.second] = g.mask[kv.first];
+  } else {
+    m.mask = g.mask;
   }
 }
 
@@ -1467,6 +1554,12 @@ void* orc_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, doubl
                           int compactMask) {
   auto* m = new MeshData();
   genLevelSet2D(nx, ny, xa, xb, ya, yb, btype, compactMask, *m);
+  return m;
+}
+void* orc_mesh_levelset3d(int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za,
+                          double zb, int btype, int compactMask) {
+  auto* m = new MeshData();
+  genLevelSet3D(nx, ny, nz, xa, xb, ya, yb, za, zb, btype, compactMask, *m);
   return m;
 }
 void* orc_mesh_read(int dim, const char* tri, const char* pnts, const char* mask) {

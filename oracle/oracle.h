@@ -30,6 +30,9 @@ void* orc_mesh_rect(int dim, int nx, int ny, int nz, double xa, double xb, doubl
                     double yb, double za, double zb, int btype);
 void* orc_mesh_levelset2d(int nx, int ny, double xa, double xb, double ya, double yb,
                           int btype, int compactMask);
+// MeshUtils.h:540-667 + main.cpp:87-97 (3D, spherePhi) with the pointer hand-back repaired
+void* orc_mesh_levelset3d(int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za,
+                          double zb, int btype, int compactMask);
 void* orc_mesh_read(int dim, const char* tri, const char* pnts, const char* mask);
 void orc_mesh_sizes(void* m, int* nP, int* nF, int* maskLen);
 void orc_mesh_copy(void* m, double* Vp, int* F, int* mask);

@@ -33,6 +33,8 @@ def lib():
         L.orc_mesh_rect.argtypes = [ctypes.c_int] * 4 + [ctypes.c_double] * 6 + [ctypes.c_int]
         L.orc_mesh_levelset2d.restype = ctypes.c_void_p
         L.orc_mesh_levelset2d.argtypes = [ctypes.c_int] * 2 + [ctypes.c_double] * 4 + [ctypes.c_int] * 2
+        L.orc_mesh_levelset3d.restype = ctypes.c_void_p
+        L.orc_mesh_levelset3d.argtypes = [ctypes.c_int] * 3 + [ctypes.c_double] * 6 + [ctypes.c_int] * 2
         L.orc_mesh_read.restype = ctypes.c_void_p
         L.orc_mesh_read.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.orc_mesh_sizes.argtypes = [ctypes.c_void_p, c_int_p, c_int_p, c_int_p]
@@ -113,6 +115,11 @@ class Mesh:
     def levelset2d(n, xa=0.0, xb=1.0, ya=0.0, yb=1.0, btype=1, compact_mask=True):
         h = lib().orc_mesh_levelset2d(n, n, xa, xb, ya, yb, btype, int(compact_mask))
         return Mesh._from_handle(2, h)
+
+    @staticmethod
+    def levelset3d(n, xa=0.0, xb=1.0, ya=0.0, yb=1.0, za=0.0, zb=1.0, btype=1, compact_mask=True):
+        h = lib().orc_mesh_levelset3d(n, n, n, xa, xb, ya, yb, za, zb, btype, int(compact_mask))
+        return Mesh._from_handle(3, h)
 
     @staticmethod
     def read(dim, tri, pnts, mask):

@@ -114,3 +114,23 @@ def test_argument_and_partition_errors():
         P.backwards_euler_step(0.025)
     P.close()
     comm.close()
+
+
+def test_backward_euler_at_bench_size_bitwise():
+    """The bench's method-2 workload (SquareGrid n = 707: 1,001,113 nodes, 2,002,226 unknowns,
+    MEx3, dt 0.025 tau 0.5 rho 100): two backward-Euler steps bit-identical to the oracle run with
+    the GPU's CG-STAB summation order -- the FD Jacobian, the Newton counts and x after each step --
+    so the size-dependent parts of the method-2 path (Jacobian assembly, the n = 2 M factor and
+    chain sweeps) meet the restatement at the size the bench times."""
+    m = mx.MeshData.rect(2, 707)
+    assert m.nP == 1001113
+    om = oracle_py.Mesh(2, m.Xp, m.F, m.mask)
+    O, G = make_pair(om, 3, 0.025, 0.5, 100.0, False, 1, 1)
+    for s in range(2):
+        ih_o, n_o = O.backwards_euler_step(0.025, 1e-3, tree=True)
+        ih_g, n_g = G.backwards_euler_step(0.025, 1e-3)
+        assert n_o == n_g, f"Newton iterations differ at step {s}"
+        assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
+        np.testing.assert_array_equal(G.get("x"), O.get("x"), err_msg=f"x step {s}")
+    np.testing.assert_array_equal(G.jacobian()[2], O.jacobian()[2])
+    G.close()

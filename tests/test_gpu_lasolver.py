@@ -253,3 +253,46 @@ def test_chain_sweeps_equal_level_sweeps(la, mesh, monkeypatch):
     assert _bit(yc, yl) and il == ic and _bit(xc, xl)
     if N < 20000:  # and both equal the restatement
         assert _bit(yc, L.ilu_solve(ia, ja, L.ilu0(ia, ja, a), b))
+
+
+@pytest.mark.parametrize("shift", [0.5, 0.3])
+def test_full_size_factor_sweeps_and_solve_bitwise(la, shift):
+    """The bench's ILU(0)-CG-STAB solve at its size (SquareGrid n=707 Jacobian pattern, 2,002,226
+    rows, 28,008,516 nonzeros; shift 0.5 = the bench's diagonal, 0.3 = a harder system with more
+    iterations): the numeric factor (k_ilu_factor_lds on the level schedule), the chain/band
+    sweeps (2,048-slot import ring, ticket order, the one-iteration bands) and the whole CG-STAB
+    solve are bit-identical to the restatement (dotMode 1: the GPU's reduction order), with the
+    same iteration count; the sequential-dot restatement agrees within resid_reduc."""
+    import mmadmm_amd as mx
+    mesh = mx.MeshData.rect(2, 707)
+    s = la.MatrixStruc(2 * mesh.nP)
+    s.mesh_pattern(2, mesh.F)
+    s.pack()
+    ia, ja = s.getia(), s.getja()
+    n = len(ia) - 1
+    assert n == 2002226 and len(ja) == 28008516
+    rng = np.random.default_rng(20221015)
+    a = rng.uniform(-1.0, 1.0, len(ja))
+    rng.uniform(-1.0, 1.0, n)  # (the bench's SpMV vector: keeps b the bench's right-hand side)
+    rows = np.repeat(np.arange(n), np.diff(ia))
+    d = np.nonzero(ja == rows)[0]
+    a[d] = np.add.reduceat(np.abs(a), ia[:-1]) * shift + 1.0
+    b = rng.uniform(-1.0, 1.0, n)
+    A = la.MatrixIter(s)
+    A.a[:] = a
+    A.b[:] = b
+    p = la.ParamIter.mesh()
+    A.sfac(p)
+    A.factor()
+    st = A.stats()
+    assert st["sweep_mode"] == 1  # the chain/band sweeps
+    af = L.ilu0(ia, ja, a)
+    assert _bit(A.get_factor()[2], af)
+    assert _bit(A.ilu_solve(b), L.ilu_solve(ia, ja, af, b))
+    x = np.zeros(n)
+    it = A.solve(p, x)
+    xt, itt, _ = L.solve(ia, ja, a, b, tree=True)
+    assert it == itt and it > 0 and _bit(x, xt), (it, itt)
+    xo, io, _ = L.solve(ia, ja, a, b)
+    assert abs(it - io) <= 1 and _rel(x, xo) <= p.resid_reduc, (it, io, _rel(x, xo))
+    A.close()

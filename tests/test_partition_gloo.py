@@ -157,3 +157,18 @@ def test_rcb_is_deterministic_and_rank_consistent():
         assert cnt[(q, r)] == (v, s)
     again = mx.partition_plan(3, mesh.Xp, mesh.F, world, 2)
     assert np.array_equal(again["localSimplices"], plans[2]["localSimplices"])
+
+
+@pytest.mark.parametrize("dim,n,world", [(2, 1, 4), (2, 2, 13), (2, 3, 32), (2, 4, 50), (2, 4, 64), (2, 5, 7),
+                                         (3, 1, 6)])
+def test_rcb_gives_every_rank_a_simplex(dim, n, world):
+    """Small parts (nF = 4n^2 triangles in 2D): a snapped cut plane never leaves one side with
+    fewer simplices than ranks, so no rank is left without simplices (each of the first five cases
+    left ranks empty before the cut was restricted)."""
+    import mmadmm_amd as mx
+    mesh = mx.MeshData.rect(dim, n)
+    assert len(mesh.F) >= world
+    plans = [mx.partition_plan(dim, mesh.Xp, mesh.F, world, r) for r in range(world)]
+    sizes = [len(p["localSimplices"]) for p in plans]
+    assert min(sizes) >= 1 and sum(sizes) == len(mesh.F), sizes
+    assert all(len(p["localNodes"]) >= dim + 1 for p in plans)
