@@ -89,6 +89,8 @@ typedef struct mmadmm_stats {
   double t_solve_ms;      /* backward Euler: wall time in the linear solves (ILU(0) + CG-STAB) */
   double t_be_ms;         /* backward Euler: wall time of whole steps */
   long long regrids;      /* monitor-grid rebuilds on the device (mmadmm_regrid / set_regrid) */
+  long long regrid_rows;  /* grid rows the last rebuild filled (an element partition: this rank's box) */
+  double regrid_gather_bytes; /* vertex positions this rank received for the last rebuild */
 } mmadmm_stats;
 
 /* Time-varying monitors (the reference's Mesh<D>::setUp hook, commented out at

@@ -148,6 +148,16 @@ class Engine final : public EngineBase {
       ownLocal_.upload(mine.data(), std::max<size_t>(mine.size(), 1), st_);
       MMX_HIP(hipStreamSynchronize(st_));
     }
+    for (int s = 0; s < nF_; ++s)  // the partitioned regrid's margin: the widest local simplex per axis
+      for (int d = 0; d < D; ++d) {
+        double a = INFINITY, b = -INFINITY;
+        for (int n = 0; n < D + 1; ++n) {
+          const double c = Vp[(size_t)plan_.localNodes[plan_.Flocal[(size_t)s * (D + 1) + n]] * D + d];
+          a = std::min(a, c);
+          b = std::max(b, c);
+        }
+        extMax_[d] = std::max(extMax_[d], b - a);
+      }
     const int nl = nP_;
     // t = M + dt^2 WD_T W D is block diagonal: t_vv = tau + dt^2 * (w*w summed valence times)
     std::vector<double> invdiag(nl);
@@ -225,8 +235,8 @@ class Engine final : public EngineBase {
     z_.alloc((size_t)nF_ * K);
     gcache_.alloc((size_t)nF_ * (K + 1));
     tieList_.alloc((size_t)nF_ / 64 + 1);  // prox blocks queued for the exact recomputation
-    tieCount_.alloc(1);
-    MMX_HIP(hipMemsetAsync(tieCount_.p, 0, sizeof(unsigned), st_));
+    tieCount_.alloc(2);  // [0] queued blocks, [1] workgroups of the exact pass done with the queue
+    MMX_HIP(hipMemsetAsync(tieCount_.p, 0, 2 * sizeof(unsigned), st_));
     u_.alloc((size_t)nF_ * K);
     gs_.alloc((size_t)nF_ * K);
     MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
@@ -710,33 +720,46 @@ class Engine final : public EngineBase {
     const int nG = (nranks_ > 1) ? plan_.nP : nP_;  // vertices the grid is built from
     const int nb = std::max(1, std::min(256, (nG + 255) / 256));
     if (!rgPart_.p) {
-      rgPart_.alloc((size_t)256 * 2 * D);
+      rgPart_.alloc((size_t)512 * 2 * D);  // global bbox partials, then this rank's
       rgMon_.alloc((size_t)nG * DD);
       rgCellOf_.alloc(nG);
       rgNodes_.alloc(nG);
       rgTmp_.alloc(gvals_.n);
+      if (nranks_ > 1) rgTmp2_.alloc(gvals_.n);
       if (nranks_ > 1) {
         rgXg_.alloc((size_t)nG * D);
         rgSend_.alloc((size_t)maxOwned_ * D);
         rgRecv_.alloc((size_t)nranks_ * maxOwned_ * D);
       }
-      MMX_HIP(hipHostMalloc((void**)&rgHost_, sizeof(double) * 256 * 2 * D, hipHostMallocDefault));
+      MMX_HIP(hipHostMalloc((void**)&rgHost_, sizeof(double) * 512 * 2 * D, hipHostMallocDefault));
     }
     const double* X = Vp_.p;
-    if (nranks_ > 1) {
+    const bool part = nranks_ > 1;
+    const int nbl = part ? std::max(1, std::min(256, (nP_ + 255) / 256)) : 0;  // blocks of the local bbox
+    if (part) {
       launch_rows_gather(D, ownLocal_.p, nOwned_, Vp_.p, rgSend_.p, st_);
       comm_->allgather(rank_, rgSend_.p, rgRecv_.p, (size_t)maxOwned_ * D, st_);
       launch_rows_scatter(D, ownAllGid_.p, nranks_ * maxOwned_, rgRecv_.p, rgXg_.p, st_);
       X = rgXg_.p;
+      launch_bbox<D>(Vp_.p, nP_, rgPart_.p + (size_t)256 * 2 * D, nbl, st_);  // this rank's vertices
     }
     launch_bbox<D>(X, nG, rgPart_.p, nb, st_);
     MMX_HIP(hipMemcpyAsync(rgHost_, rgPart_.p, sizeof(double) * nb * 2 * D, hipMemcpyDeviceToHost, st_));
+    if (part)
+      MMX_HIP(hipMemcpyAsync(rgHost_ + (size_t)256 * 2 * D, rgPart_.p + (size_t)256 * 2 * D, sizeof(double) * nbl * 2 * D,
+                             hipMemcpyDeviceToHost, st_));
     MMX_HIP(hipStreamSynchronize(st_));
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int b = 0; b < nb; ++b)
       for (int d = 0; d < D; ++d) {
         lo[d] = std::min(lo[d], rgHost_[(size_t)b * 2 * D + d]);
         hi[d] = std::max(hi[d], rgHost_[(size_t)b * 2 * D + D + d]);
+      }
+    for (int b = 0; b < nbl; ++b)
+      for (int d = 0; d < D; ++d) {
+        llo[d] = std::min(llo[d], rgHost_[(size_t)(256 + b) * 2 * D + d]);
+        lhi[d] = std::max(lhi[d], rgHost_[(size_t)(256 + b) * 2 * D + D + d]);
       }
     grid_geometry(D, nG, lo, hi, grid_);
     gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
@@ -782,18 +805,49 @@ class Engine final : public EngineBase {
       MMX_HIP(hipMemcpyAsync(rgMon_.p, mv.data(), mv.size() * sizeof(double), hipMemcpyHostToDevice, st_));
       MMX_HIP(hipStreamSynchronize(st_));
     }
-    launch_nn_fill<D>(X, cg, rgStarts_.p, rgNodes_.p, gx_.p, gy_.p, D == 3 ? gz_.p : gy_.p, grid_.nx, grid_.ny,
-                      grid_.nz, rgMon_.p, rgTmp_.p, st_);
+    // the grid rows to rebuild: all of them on one rank; on an element partition the box of rows
+    // this rank's monitor evaluations can reach (its vertices' bounding box, widened by two
+    // simplex extents and two cells for the motion within a step), plus the smoothing passes'
+    // halo for the nearest-vertex fill.  Every vertex is binned, so each fill is exact; the rows
+    // outside the box are set to NaN, so an evaluation that left the box could not pass silently.
     const int passes = (D == 2) ? 5 : 2;  // smoothMonitorGrid
+    const int gn3[3] = {grid_.nx, grid_.ny, D == 3 ? grid_.nz : 0};
+    GridBox R{{0, 0, 0}, {gn3[0], gn3[1], gn3[2]}};
+    if (part) {
+      for (int d = 0; d < D; ++d) {  // evalMonitor reads rows zInd P + yInd (nx+1) + xInd: storage axis d = axis d
+        const std::vector<double>& g = d == 0 ? grid_.gx : d == 1 ? grid_.gy : grid_.gz;
+        const double h = g[1] - g[0];
+        const int M = (int)std::ceil(2.0 * extMax_[d] / h) + 2;
+        R.lo[d] = std::max(0, std::min(gn3[d], (int)std::floor((llo[d] - g[0]) / h) - M));
+        R.hi[d] = std::max(0, std::min(gn3[d], (int)std::floor((lhi[d] - g[0]) / h) + 1 + M));
+      }
+    }
+    auto widen = [&](const GridBox& b, int w) {
+      GridBox o = b;
+      for (int d = 0; d < D; ++d) {
+        o.lo[d] = std::max(0, b.lo[d] - w);
+        o.hi[d] = std::min(gn3[d], b.hi[d] + w);
+      }
+      return o;
+    };
+    const GridBox H = widen(R, part ? passes : 0);
+    launch_nn_fill<D>(X, cg, rgStarts_.p, rgNodes_.p, gx_.p, gy_.p, D == 3 ? gz_.p : gy_.p, grid_.nx, grid_.ny,
+                      grid_.nz, rgMon_.p, rgTmp_.p, H, st_);
     double* cur = rgTmp_.p;
-    double* oth = gvals_.p;
+    double* oth = part ? rgTmp2_.p : gvals_.p;
     for (int it = 0; it < passes; ++it) {
-      launch_smooth<D>(cur, oth, grid_.nx, grid_.ny, grid_.nz, st_);
+      launch_smooth<D>(cur, oth, grid_.nx, grid_.ny, grid_.nz, widen(R, part ? passes - 1 - it : 0), st_);
       std::swap(cur, oth);
     }
-    if (cur != gvals_.p)
-      MMX_HIP(hipMemcpyAsync(gvals_.p, cur, gvals_.n * sizeof(double), hipMemcpyDeviceToDevice, st_));
-    if (D == 3) launch_pad_rows(gvals_.p, (long long)(gvals_.n / 9), gpad_.p, st_);
+    if (part) {
+      launch_box_commit<D>(cur, gvals_.p, D == 3 ? gpad_.p : nullptr, grid_.nx, grid_.ny, grid_.nz, R, st_);
+    } else {
+      if (cur != gvals_.p)
+        MMX_HIP(hipMemcpyAsync(gvals_.p, cur, gvals_.n * sizeof(double), hipMemcpyDeviceToDevice, st_));
+      if (D == 3) launch_pad_rows(gvals_.p, (long long)(gvals_.n / 9), gpad_.p, st_);
+    }
+    st_stats_.regrid_rows = (long long)(H.hi[0] - H.lo[0] + 1) * (H.hi[1] - H.lo[1] + 1) * (H.hi[2] - H.lo[2] + 1);
+    st_stats_.regrid_gather_bytes = part ? (double)nranks_ * maxOwned_ * D * sizeof(double) : 0.0;
     MMX_HIP(hipGetLastError());
     gridOnDevice_ = true;
     m_ = makeView();
@@ -814,6 +868,7 @@ class Engine final : public EngineBase {
     m.gcache = gcache_.p;
     m.tieList = tieList_.p;
     m.tieCount = tieCount_.p;
+    m.tieDone = tieCount_.p + 1;
     m.nodeOrder = nodeOrder_.p;
     {
       const char* ft = getenv("MMX_FORCE_TIE");
@@ -882,7 +937,8 @@ class Engine final : public EngineBase {
   mmadmm_monitor_fn monFn_ = nullptr;
   void* monUser_ = nullptr;
   bool regridEachStep_ = false, gridOnDevice_ = false;
-  DevBuf<double> rgPart_, rgMon_, rgTmp_, rgXg_, rgSend_, rgRecv_;
+  DevBuf<double> rgPart_, rgMon_, rgTmp_, rgTmp2_, rgXg_, rgSend_, rgRecv_;
+  double extMax_[3] = {0.0, 0.0, 0.0};  // largest extent of a local simplex per axis (partitioned regrid box)
   DevBuf<int> ownLocal_, ownAllGid_;  // partitioned regrid: my owned vertices (local ids), all ranks' (global ids)
   int nOwned_ = 0, maxOwned_ = 1;
   DevBuf<int> rgCellOf_, rgNodes_, rgCounts_, rgStarts_, rgFill_;

@@ -13,7 +13,9 @@
 // Build: -ffp-contract=off (no fused multiply-add unless written), see DESIGN.md.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "admm_device.h"
 #include "admm_kernels.h"
@@ -789,14 +791,29 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
 // wrote nothing back (z, u, Bkinv unchanged), so each of its simplices restarts from its inputs
 // with cr_resolve, Bkinv in registers and a full entry blockGrad (bit-identical to the cached
 // form, which the fast pass may have overwritten), and the block's partials are formed with the
-// same workgroup shape -- the same values in the same tree.  One workgroup walks the list (ties
-// are rare; with none it only reads the counter) and re-arms the counter for the next prox.
+// same workgroup shape -- the same values in the same tree.  The workgroups of a fixed grid (one
+// per CU at most) stride over the list, so a prox with many ties is not serialised on one CU; the
+// last workgroup to finish re-arms the counter for the next prox (with no ties each workgroup only
+// reads the counter).
+__device__ __forceinline__ void rearm_tie_queue(unsigned* tieCount, unsigned* tieDone) {
+  __shared__ unsigned last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = (atomicAdd(tieDone, 1u) == gridDim.x - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    *tieCount = 0u;
+    *tieDone = 0u;
+  }
+}
 template <int D, int BS>
 __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                  double* __restrict__ zg, double* __restrict__ ug,
                                                  const double* Bin, double* Bout, double* __restrict__ partials) {
   const unsigned n = *m.tieCount;
-  for (unsigned i = 0; i < n; ++i) {
+  for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
     const int b = m.tieList[i];
     const int s = b * BS + (int)threadIdx.x;
     double pv[6] = {0, 0, 0, 0, 0, 0};
@@ -804,7 +821,7 @@ __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, co
     block_partials<6, BS>(pv, partials, b);
     __syncthreads();
   }
-  if (threadIdx.x == 0 && n != 0) *m.tieCount = 0u;
+  rearm_tie_queue(m.tieCount, m.tieDone);
 }
 
 // Steady-state prox (every prox after the first), Bkinv staged through LDS.  The workgroup's
@@ -1020,6 +1037,498 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     write_tslot<D>(m, s, z, un);
   }
   block_partials<6, 64>(pv, partials, lb);
+}
+
+// ---- 3D steady-state prox, four lanes per tetrahedron (k_prox_quad) ------------------------------
+// Lane 4t + k of a workgroup works on tetrahedron t with quad lane k: it holds rows 3k..3k+2 of the
+// tet's Bkinv in registers for the whole prox (Bkinv is read once and written once) and the
+// components of vertex k (z, DXpU, gradient, p, y).  Full 12-vectors are assembled on demand from
+// the four lanes with DPP quad broadcasts; every value any lane computes is formed with exactly the
+// operations, in exactly the order, of the one-lane kernel (bit-identical): values that depend on
+// the whole simplex (the 3x3 algebra of blockGrad, the powers, the scalar sums c2, yBy, |G|_1,
+// ||z - zPrev||^2, the regulariser's ||DXpU - z||^2) are computed by all four lanes alike; the
+// four vertex monitors of blockGrad are evaluated one per lane; the row-wise work (p = -B G,
+// B y, the rank-two update) is split by rows; the column sums y^T B, sequential over the rows
+// (src/Mesh.cpp:848), pass from quad lane to quad lane in row order.
+template <int Q>
+__device__ __forceinline__ double qb(double v) {  // quad lane Q's value, in every lane of the quad
+  const int2 i = __builtin_bit_cast(int2, v);
+  int2 r;
+  r.x = __builtin_amdgcn_update_dpp(0, i.x, Q * 0x55, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_update_dpp(0, i.y, Q * 0x55, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ int qb_or(int v) {  // OR over the quad
+  int r = v;
+  r |= __builtin_amdgcn_update_dpp(0, v, 1 * 0x55, 0xF, 0xF, false);
+  r |= __builtin_amdgcn_update_dpp(0, v, 0 * 0x55, 0xF, 0xF, false);
+  r |= __builtin_amdgcn_update_dpp(0, v, 2 * 0x55, 0xF, 0xF, false);
+  r |= __builtin_amdgcn_update_dpp(0, v, 3 * 0x55, 0xF, 0xF, false);
+  return r;
+}
+// full[3q + c] = own[c] of quad lane q
+__device__ __forceinline__ void qfull(const double (&own)[3], double (&full)[12]) {
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    full[c] = qb<0>(own[c]);
+    full[3 + c] = qb<1>(own[c]);
+    full[6 + c] = qb<2>(own[c]);
+    full[9 + c] = qb<3>(own[c]);
+  }
+}
+template <int Q>
+__device__ __forceinline__ M<3> qbM(const M<3>& a) {
+  M<3> r;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) r.m[i][j] = qb<Q>(a.m[i][j]);
+  return r;
+}
+
+// AdaptationFunctional<3>::blockGrad (src/AdaptationFunctional.cpp:102-287) with GRAD and REG,
+// cooperatively: z = the tet's 12 coordinates (all lanes), zo / dxo = this lane's vertex (k) of z
+// and DXpU; returns the regularised energy (all lanes) and this lane's 3 gradient components in
+// go.  ghuang (the gradient cache of the simplex, or nullptr): this lane's unregularised
+// components, and Igt from quad lane 0.  Same operations in the same order as blockGrad<3, true,
+// true, EXACT> (admm_device.h), so every value is bit-identical to it.
+template <bool EXACT>
+__device__ __forceinline__ double blockGradQuad(const GridView<3>& g, const FunctionalConsts<3>& fc, int k,
+                                                const double (&z)[12], const double* xi, const double (&zo)[3],
+                                                const double (&dxo)[3], double (&go)[3], double& Igt,
+                                                double* ghuang, bool* tiep) {
+  bool tie = false;
+  const double dFact = 6.0;
+  // the vertex monitors: this lane's, then M = ((0 + m0) + m1) + m2) + m3 and the lane's own
+  // difference m_k - m0 (the gradient's monitor-variation term needs m_{j+1} - m0 from lane j+1)
+  M<3> mk;
+  evalMonitor<3>(g, zo, mk);
+  M<3> Msum, dmk;
+  {
+    const M<3> m0 = qbM<0>(mk);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        Msum.m[r][c] = 0.0 + m0.m[r][c];
+        dmk.m[r][c] = mk.m[r][c] - m0.m[r][c];
+      }
+  }
+  {
+    const M<3> t = qbM<1>(mk);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) Msum.m[r][c] = Msum.m[r][c] + t.m[r][c];
+  }
+  {
+    const M<3> t = qbM<2>(mk);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) Msum.m[r][c] = Msum.m[r][c] + t.m[r][c];
+  }
+  {
+    const M<3> t = qbM<3>(mk);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) Msum.m[r][c] = Msum.m[r][c] + t.m[r][c];
+  }
+  M<3> Minv = inverse<3>(Msum);
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Minv.m[r][c] = Minv.m[r][c] / ((double)3 + 1);
+  M<3> E, Ehat;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      E.m[r][j] = z[3 * (j + 1) + r] - z[r];
+      Ehat.m[r][j] = fc.compMesh ? (xi[3 * (j + 1) + r] - xi[r]) : fc.Ehat[r * 3 + j];
+    }
+  }
+  // the regulariser's ||DXpU - z||^2, summed in index order over the four lanes' components
+  double sq;
+  {
+    double t[3], tf[12];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) t[c] = dxo[c] - zo[c];
+    qfull(t, tf);
+    sq = tf[0] * tf[0];
+#pragma unroll
+    for (int i = 1; i < 12; ++i) sq = sq + tf[i] * tf[i];
+  }
+  const double Edet = det<3>(E);
+  if (!(Edet > 0)) {
+    const double nan = __builtin_nan("");
+#pragma unroll
+    for (int c = 0; c < 3; ++c) go[c] = nan;
+    if (ghuang) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) ghuang[3 * k + c] = nan;
+      if (k == 0) ghuang[12] = nan;
+    }
+    Igt = nan;
+    return nan;
+  }
+  const M<3> Einv = inverse<3>(E);
+  const M<3> FJ = mul<3>(Ehat, Einv);
+  const double detFJ = det<3>(FJ);
+  const double d = 3.0;
+  const double p = 1.5;
+  const double theta = 1.0 / 3.0;
+  const M<3> FJt = transpose<3>(FJ);
+  const M<3> MinvJt = mul<3>(Minv, FJt);
+  const M<3> JMJt = mul<3>(FJ, MinvJt);
+  const double trJMJt = trace<3>(JMJt);
+  const double detM = cr_sqrt(1.0 / det<3>(Minv));
+  const double tr_dp2 = pow_dp2<3, EXACT>(trJMJt, tie);
+  const double G = theta * detM * tr_dp2 + (1.0 - 2.0 * theta) * fc.powd * detM * cr_pow_p15<EXACT>(detFJ / detM, tie);
+  const double absK = __builtin_fabs(Edet / dFact);
+  const double tr_dp2m1 = pow_dp2m1<3, EXACT>(trJMJt, tie);
+  const double detM_1mp = cr_pow_m05<EXACT>(detM, tie);
+  M<3> dGdJ;
+  {
+    const double s = d * p * theta * detM * tr_dp2m1;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) dGdJ.m[r][c] = s * MinvJt.m[r][c];
+  }
+  const double dGddet = p * (1.0 - 2.0 * theta) * fc.powd * detM_1mp * cr_pow_p05(detFJ);
+  M<3> dGdM;
+  {
+    const double s1 = -0.5 * theta * d * p * detM * tr_dp2m1;
+    const M<3> MinvT = transpose<3>(Minv);
+    M<3> T;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) T.m[r][c] = s1 * MinvT.m[r][c];
+    T = mul<3>(mul<3>(mul<3>(T, FJt), FJ), Minv);
+    const double s2 = 0.5 * theta * detM * tr_dp2 +
+                      ((0.5 - theta) * (1.0 - p) * fc.powd) * detM_1mp * cr_pow_p15<EXACT>(detFJ, tie);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) dGdM.m[r][c] = T.m[r][c] + s2 * Minv.m[r][c];
+  }
+  // trace(dGdM (m_{j+1} - m0)) from lane j + 1 (lane 0's value is not used)
+  const double trk = trace<3>(mul<3>(dGdM, dmk));
+  const double trj[3] = {qb<1>(trk), qb<2>(trk), qb<3>(trk)};
+  double basisComb[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) basisComb[c] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) basisComb[c] += Einv.m[j][c] * trj[j];
+  const double c1 = (-G + dGddet * detFJ);
+  M<3> vLoc;
+  {
+    const M<3> P = mul<3>(mul<3>(Einv, dGdJ), FJ);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) vLoc.m[r][c] = c1 * Einv.m[r][c] + P.m[r][c];
+  }
+#pragma unroll
+  for (int n = 0; n < 3; n++)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) vLoc.m[n][c] -= (basisComb[c]) / ((double)3 + 1.0);
+  // this lane's gradient components: vertex 0 sums the columns of vLoc, vertex n >= 1 is -vLoc[n-1]
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double s = 0.0;
+#pragma unroll
+    for (int n = 0; n < 3; n++) s += vLoc.m[n][c];
+    const double g0 = s + (basisComb[c] + 0.0);
+    const double gn = (k == 1) ? -vLoc.m[0][c] : (k == 2) ? -vLoc.m[1][c] : -vLoc.m[2][c];
+    go[c] = ((k == 0) ? g0 : gn) * absK;
+  }
+  double Ih = absK * G;
+  Igt = Ih;
+  if constexpr (!EXACT) *tiep = *tiep || tie;
+  if (ghuang) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ghuang[3 * k + c] = go[c];
+    if (k == 0) ghuang[12] = Igt;
+  }
+  Ih += 0.5 * fc.w * fc.w * sq;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) go[c] += fc.w * fc.w * (-dxo[c] + zo[c]);
+  return Ih;
+}
+
+// The steady-state 3D prox with four lanes per tetrahedron (see above).  One workgroup of 256
+// lanes = the 64 tets of one group of the wave-interleaved Bkinv layout (bidx<3>); Bkinv is
+// double-buffered as for k_prox_wave (Bin only read, Bout written).  EXACT = false is the fast
+// path (no tie resolution, Markstein divisions): a block that meets a near-midpoint power or a
+// quotient outside div_mk's range writes nothing back and is queued; EXACT = true recomputes the
+// queued blocks (the workgroups stride over the queue) with the exact decisions, a full entry
+// blockGrad and the same partial-sum tree, and the last workgroup to finish re-arms the queue.
+constexpr int kQuadImg = 36 * 64 + 16;  // doubles per quad-lane block of k_prox_quad's LDS image
+template <bool COMP, bool EXACT>
+__global__ void __launch_bounds__(256, 2) k_prox_quad(DeviceMesh<3> m, double tol, const double* __restrict__ x,
+                                                       double* __restrict__ zg, double* __restrict__ ug,
+                                                       const double* Bin, double* Bout,
+                                                       double* __restrict__ partials, int useCache) {
+  constexpr int K = 12, KK = 144;
+  // LDS image of the block's Bkinv: quad lane k's rows of the 64 tets in block k (3 x 12 entries of
+  // 64 tets), the blocks 32 dwords apart in the banks, so a wavefront's access to one entry of its
+  // 16 tets x 4 quad lanes takes the minimum two passes
+  __shared__ __attribute__((aligned(16))) double img[4 * kQuadImg];
+  const int tid = threadIdx.x, k = tid & 3, tl = tid >> 2;
+  const unsigned nWork = EXACT ? *m.tieCount : 1u;
+  for (unsigned w = EXACT ? blockIdx.x : 0u; w < nWork; w += EXACT ? gridDim.x : 1u) {
+    const int lb = EXACT ? m.tieList[w] : logical_block_any();
+    const int s0 = lb * 64;
+    const bool act = s0 + tl < m.nF;
+    const int s = act ? s0 + tl : s0;
+    const int fk = m.F[(size_t)s * 4 + k];
+    const unsigned fixedBits = m.sbits[s] & 0xF;
+    const bool ownFixed = (fixedBits >> k) & 1u;
+    double* zs = zg + (size_t)s * K + 3 * k;
+    double* us = ug + (size_t)s * K + 3 * k;
+    double* gc = m.gcache + (size_t)s * (K + 1);
+    double zo[3], z0[3], dxo[3], go[3], Igt = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      zo[c] = zs[c];
+      z0[c] = zo[c];
+      dxo[c] = x[(size_t)fk * 3 + c] + us[c];  // DXpU = D x + uBar
+    }
+    const bool cached = !EXACT && useCache;
+    if (cached) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) go[c] = gc[3 * k + c];
+      Igt = gc[K];
+    }
+    double xi[K];
+    if constexpr (COMP) {
+      double xo[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xo[c] = m.Vc[(size_t)fk * 3 + c];
+      qfull(xo, xi);
+    }
+    // the block's Bkinv chunk (64 tets x 144, contiguous in the wave-interleaved layout) staged
+    // through LDS with 16-byte coalesced loads, then this lane's three rows into registers
+    const size_t gb = (size_t)lb * KK * 64;
+#pragma unroll 6
+    for (int e = tid * 2; e < KK * 64; e += 512) {
+      const v2nt v = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(Bin + gb + e));
+      const int ij = e >> 6, t = e & 63, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
+      *reinterpret_cast<v2nt*>(&img[kk * kQuadImg + (r * K + j) * 64 + t]) = v;
+    }
+    // entry (r, j) of this lane's rows at mine[(r K + j) 64]: read into registers by each pass (not
+    // held across the blockGrad), the new values written back by the update pass
+    double* const mine = img + k * kQuadImg + tl;
+    __syncthreads();
+    double pv[6] = {0, 0, 0, 0, 0, 0};
+    bool tie = false;
+    if (act) {
+      const GridView<3> g = gridOf<3>(m);
+      FunctionalConsts<3> fc = constsOf<3>(m);
+      fc.compMesh = COMP ? 1 : 0;
+      bool bad = false;
+      if (cached) {  // entry_grad with the cache: the unregularised part plus the regulariser
+#pragma unroll
+        for (int c = 0; c < 3; ++c) go[c] += fc.w * fc.w * (-dxo[c] + zo[c]);
+        bad |= (Igt != Igt);
+      } else {
+        double zf[K];
+        qfull(zo, zf);
+        const double e = blockGradQuad<EXACT>(g, fc, k, zf, xi, zo, dxo, go, Igt, nullptr, &tie);
+        bad |= (e != e);
+      }
+      if (ownFixed)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) go[c] = 0.0;
+      const double Ihsave = Igt;
+      int iter;
+      for (iter = 0; iter < 50 && !tie; iter++) {
+        // p = -B G (rows 3k..3k+2)
+        double po[3];
+        {
+          double Gf[K];
+          qfull(go, Gf);
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {
+            double row[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) row[j] = mine[(r * K + j) * 64];
+            double sacc = (-row[0]) * Gf[0];
+#pragma unroll
+            for (int j = 1; j < K; ++j) sacc += (-row[j]) * Gf[j];
+            po[r] = sacc;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) zo[c] += po[c];
+        double G1o[3], Ig1;
+        {
+          double zf[K];
+          qfull(zo, zf);
+          const double e = blockGradQuad<EXACT>(g, fc, k, zf, xi, zo, dxo, G1o, Ig1, gc, &tie);
+          bad |= (e != e);
+        }
+        if constexpr (!EXACT) {
+          if (qb_or(tie ? 1 : 0)) {
+            tie = true;
+            break;
+          }
+        }
+        if (ownFixed)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) G1o[c] = 0.0;
+        double Ix = 0;
+        double yo[3], yf[K];
+        {
+          double G1f[K];
+          qfull(G1o, G1f);
+#pragma unroll
+          for (int i = 0; i < K; i++) Ix += __builtin_fabs(G1f[i]);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) yo[c] = G1o[c] - go[c];
+        qfull(yo, yf);
+        double c2;
+        {
+          double pf[K];
+          qfull(po, pf);
+          c2 = pf[0] * yf[0];
+#pragma unroll
+          for (int i = 1; i < K; ++i) c2 += pf[i] * yf[i];
+        }
+        // pass 2: By (rows), yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij (i ascending: lane to lane);
+        // yB ends in quad lane 3 and is handed out as slices like p: yBo[c] = yB_{3k+c}
+        double yBy, yBo[3];
+        double rows[3][K];  // live through passes 2 and 3 (the update reads the old rows throughout)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int j = 0; j < K; ++j) rows[r][j] = mine[(r * K + j) * 64];
+        {
+          double byo[3], byf[K];
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {
+            double by = rows[r][0] * yf[0];
+#pragma unroll
+            for (int j = 1; j < K; ++j) by += rows[r][j] * yf[j];
+            byo[r] = by;
+          }
+          qfull(byo, byf);
+          yBy = yf[0] * byf[0];
+#pragma unroll
+          for (int i = 1; i < K; ++i) yBy = yBy + yf[i] * byf[i];
+          double P[K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) P[j] = (yo[0] * rows[0][j] + yo[1] * rows[1][j]) + yo[2] * rows[2][j];
+#pragma unroll
+          for (int j = 0; j < K; ++j) P[j] = ((qb<0>(P[j]) + yo[0] * rows[0][j]) + yo[1] * rows[1][j]) + yo[2] * rows[2][j];
+#pragma unroll
+          for (int j = 0; j < K; ++j) P[j] = ((qb<1>(P[j]) + yo[0] * rows[0][j]) + yo[1] * rows[1][j]) + yo[2] * rows[2][j];
+#pragma unroll
+          for (int j = 0; j < K; ++j) P[j] = ((qb<2>(P[j]) + yo[0] * rows[0][j]) + yo[1] * rows[1][j]) + yo[2] * rows[2][j];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const double a0 = qb<3>(P[c]), a1 = qb<3>(P[3 + c]), a2 = qb<3>(P[6 + c]), a3 = qb<3>(P[9 + c]);
+            yBo[c] = (k == 0) ? a0 : (k == 1) ? a1 : (k == 2) ? a2 : a3;
+          }
+        }
+        const double c1 = (c2 + yBy) / cr_pow_2(c2);
+        const double rc2 = 1.0 / c2;
+        unsigned eBy = 0u;
+        double fin = 0.0;
+        // pass 3: B_ij += c1 p_i p_j - (B (y p^T))_ij / c2 - p_i (y^T B)_j / c2, column by column
+        // (column j's products y_q p_j shared by the three rows), into the LDS image
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const double pj = (j < 3) ? qb<0>(po[j % 3]) : (j < 6) ? qb<1>(po[j % 3]) : (j < 9) ? qb<2>(po[j % 3]) : qb<3>(po[j % 3]);
+          const double yBj =
+              (j < 3) ? qb<0>(yBo[j % 3]) : (j < 6) ? qb<1>(yBo[j % 3]) : (j < 9) ? qb<2>(yBo[j % 3]) : qb<3>(yBo[j % 3]);
+          double v[K];
+#pragma unroll
+          for (int q = 0; q < K; ++q) v[q] = yf[q] * pj;
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {
+            double by = rows[r][0] * v[0];
+#pragma unroll
+            for (int q = 1; q < K; ++q) by += rows[r][q] * v[q];
+            double nb;
+            if constexpr (EXACT) {
+              nb = rows[r][j] + (((c1 * (po[r] * pj)) - by / c2) - (po[r] * yBj) / c2);
+            } else {
+              eBy = max(eBy, mk_exp(by, 900));
+              nb = rows[r][j] + (((c1 * (po[r] * pj)) - div_mk(by, c2, rc2)) - div_mk(po[r] * yBj, c2, rc2));
+              fin = cr_fma(nb, 0.0, fin);
+            }
+            mine[(r * K + j) * 64] = nb;
+          }
+        }
+        if constexpr (!EXACT) {
+          // the ranges of p and yB: each lane checks its slices (a max: order-free), the quad ORs
+          unsigned ePY = 0u;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) ePY = max(ePY, max(mk_exp(po[c], 450), mk_exp(yBo[c], 450)));
+          const bool out = !(c2 >= 0x1p-100 && c2 <= 0x1p100) || eBy > 1799u || ePY > 899u || fin != 0.0;
+          if (qb_or(out ? 1 : 0)) {
+            tie = true;
+            break;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) go[c] = G1o[c];
+        if (Ix < tol) break;
+      }
+      const int its = (iter == 50) ? 50 : iter + 1;
+      double dual2 = 0.0;
+      {
+        double dz[3], dzf[K];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dz[c] = zo[c] - z0[c];
+        qfull(dz, dzf);
+#pragma unroll
+        for (int i = 0; i < K; ++i) dual2 += dzf[i] * dzf[i];
+      }
+      if (k == 0) {
+        pv[0] = Ihsave;
+        pv[1] = dual2;
+        pv[3] = (double)its;
+        pv[4] = bad ? 1.0 : 0.0;
+        pv[5] = (double)its;
+      }
+    }
+    if constexpr (!EXACT) {
+      if (m.forceTie > 0 && tid == 0 && (int)((unsigned)lb % (unsigned)m.forceTie) == 0) tie = true;
+      if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to the exact instance
+        if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = lb;
+        return;
+      }
+    }
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const double un = dxo[c] - zo[c];  // uBar = DXpU - z
+        zs[c] = zo[c];
+        us[c] = un;
+        if (m.tslot) m.tslot[(size_t)s * K + 3 * k + c] = m.w * (m.w * (zo[c] - un));
+      }
+    }
+    if constexpr (EXACT) __syncthreads();  // (the fast path's __syncthreads_or orders the image)
+    // the new Bkinv chunk back with 16-byte coalesced stores (inactive tets: the unchanged image)
+#pragma unroll 6
+    for (int e = tid * 2; e < KK * 64; e += 512) {
+      const int ij = e >> 6, t = e & 63, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
+      const v2nt v = *reinterpret_cast<const v2nt*>(&img[kk * kQuadImg + (r * K + j) * 64 + t]);
+      __builtin_nontemporal_store(v, reinterpret_cast<v2nt*>(Bout + gb + e));
+    }
+    block_partials<6, 256>(pv, partials, lb);
+    if constexpr (EXACT) __syncthreads();  // the partials scratch is reused by the next block
+  }
+  if constexpr (EXACT) rearm_tie_queue(m.tieCount, m.tieDone);
 }
 
 // Mesh::computeEnergy (src/Mesh.cpp:496-530) on positions x
@@ -1413,6 +1922,15 @@ static int prox_block() {
   return b;
 }
 
+// 3D steady-state prox kernel: k_prox_wave (one lane per tet, default: C4 2.77 ms) or k_prox_quad
+// (four lanes per tet, MMX_PROX3D=quad: bit-identical, C4 3.92 ms -- DESIGN.md §3).  Read at every
+// launch, so a test can switch kernels between steps.
+static int prox3d_quad() {
+  const char* e = getenv("MMX_PROX3D");
+  return (e && std::string(e) == "quad") ? 1 : 0;
+}
+constexpr int kFixGrid = 256;  // workgroups of the exact (tie) recomputation: at most one per CU
+
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z, double* u,
                  const double* Bin, double* Bout, double* partials, int* nblocks, hipStream_t st) {
@@ -1425,23 +1943,37 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
     double* B = Bout;  // in place (LDS image)
     const int bs = prox_block();
     *nblocks = (m.nF + bs - 1) / bs;
+    const dim3 fg(std::min(*nblocks, kFixGrid));
     if (bs == 64) {
       hipLaunchKernelGGL((k_prox_lds<D, 64>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, B, partials, uc);
-      hipLaunchKernelGGL((k_prox_fix<D, 64>), dim3(1), dim3(64), 0, st, m, tol, x, z, u, B, B, partials);
+      hipLaunchKernelGGL((k_prox_fix<D, 64>), fg, dim3(64), 0, st, m, tol, x, z, u, B, B, partials);
     } else if (bs == 128) {
       hipLaunchKernelGGL((k_prox_lds<D, 128>), dim3(*nblocks), dim3(128), 0, st, m, tol, x, z, u, B, partials, uc);
-      hipLaunchKernelGGL((k_prox_fix<D, 128>), dim3(1), dim3(128), 0, st, m, tol, x, z, u, B, B, partials);
+      hipLaunchKernelGGL((k_prox_fix<D, 128>), fg, dim3(128), 0, st, m, tol, x, z, u, B, B, partials);
     } else {
       hipLaunchKernelGGL((k_prox_lds<D, 256>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, B, partials, uc);
-      hipLaunchKernelGGL((k_prox_fix<D, 256>), dim3(1), dim3(256), 0, st, m, tol, x, z, u, B, B, partials);
+      hipLaunchKernelGGL((k_prox_fix<D, 256>), fg, dim3(256), 0, st, m, tol, x, z, u, B, B, partials);
     }
   } else {
     *nblocks = (m.nF + 63) / 64;
+    const dim3 fg(std::min(*nblocks, kFixGrid));
+    if (prox3d_quad()) {  // four lanes per tetrahedron; the exact instance recomputes queued blocks
+      if (m.compMesh) {
+        hipLaunchKernelGGL((k_prox_quad<true, false>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, Bin, Bout,
+                           partials, uc);
+        hipLaunchKernelGGL((k_prox_quad<true, true>), fg, dim3(256), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+      } else {
+        hipLaunchKernelGGL((k_prox_quad<false, false>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, Bin, Bout,
+                           partials, uc);
+        hipLaunchKernelGGL((k_prox_quad<false, true>), fg, dim3(256), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+      }
+      return;
+    }
     if (m.compMesh)
       hipLaunchKernelGGL((k_prox_wave<D, true>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
     else
       hipLaunchKernelGGL((k_prox_wave<D, false>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
-    hipLaunchKernelGGL((k_prox_fix<D, 64>), dim3(1), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+    hipLaunchKernelGGL((k_prox_fix<D, 64>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
   }
 }
 template <int D>

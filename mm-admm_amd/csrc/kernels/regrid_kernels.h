@@ -14,6 +14,13 @@ struct CellGrid {
   double hmin;    // smallest cell edge
 };
 
+// a box of grid rows in STORAGE coordinates (row = k (nx+1)(ny+1) + sy (nx+1) + sx), inclusive
+// bounds; the full grid is {0,0,0} .. {nx, ny, nz} (nz = 0 in 2D)
+struct GridBox {
+  int lo[3];
+  int hi[3];
+};
+
 // per-block partial bounding boxes: partials[b * 2D + d] = min_d, [b * 2D + D + d] = max_d
 template <int D>
 void launch_bbox(const double* X, int n, double* partials, int nblocks, hipStream_t st);
@@ -26,14 +33,20 @@ size_t bin_scan_bytes(int ncell);
 // MonType 7 at the vertices, centre c[3] of the moving bump at the current time
 template <int D>
 void launch_monitor_tv(const double* X, int n, const double* c, double* monVals, hipStream_t st);
-// nearest vertex of every grid point -> grid rows (host layout, 3D x/y swap included)
+// nearest vertex of the grid point of every row in `box` -> its monitor value (host layout: 3D
+// rows swap x and y, src/MeshInterpolator.cpp:234); rows enumerated in storage order
 template <int D>
 void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, const int* cellNodes, const double* gx,
                     const double* gy, const double* gz, int nx, int ny, int nz, const double* monVals, double* vals,
-                    hipStream_t st);
-// one Jacobi smoothing pass in -> out
+                    const GridBox& box, hipStream_t st);
+// one Jacobi smoothing pass in -> out over the rows of `box` (the others are not written)
 template <int D>
-void launch_smooth(const double* in, double* out, int nx, int ny, int nz, hipStream_t st);
+void launch_smooth(const double* in, double* out, int nx, int ny, int nz, const GridBox& box, hipStream_t st);
+// partitioned regrid: vals (and, 3D, the 10-double padded copy) = src inside `box`, NaN outside it
+// (a monitor evaluation outside the rank's box turns into a NaN energy: reported, never silent)
+template <int D>
+void launch_box_commit(const double* src, double* vals, double* pad, int nx, int ny, int nz, const GridBox& box,
+                       hipStream_t st);
 
 // rows of D doubles: out[i] = in[idx[i]] (gather) / out[idx[i]] = in[i] for idx[i] >= 0 (scatter)
 void launch_rows_gather(int D, const int* idx, int n, const double* in, double* out, hipStream_t st);

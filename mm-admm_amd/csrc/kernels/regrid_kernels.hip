@@ -108,27 +108,37 @@ __global__ void __launch_bounds__(kRB) k_monitor_tv(const double* __restrict__ X
   for (int i = 0; i < D * D; ++i) monVals[(size_t)v * D * D + i] = (i / D == i % D) ? s : 0.0;
 }
 
-// nearest vertex of every grid point; the grid row takes that vertex's monitor value
+// storage coordinates (sx, sy, k) of the p-th row of a box, and the row
+__device__ __forceinline__ size_t box_row(const GridBox& b, long long p, int nx, int ny, int& sx, int& sy, int& sk) {
+  const long long bx = b.hi[0] - b.lo[0] + 1, by = b.hi[1] - b.lo[1] + 1;
+  sx = b.lo[0] + (int)(p % bx);
+  sy = b.lo[1] + (int)((p / bx) % by);
+  sk = b.lo[2] + (int)(p / (bx * by));
+  return ((size_t)sk * (ny + 1) + sy) * (nx + 1) + sx;
+}
+__device__ __forceinline__ long long box_rows(const GridBox& b) {
+  return (long long)(b.hi[0] - b.lo[0] + 1) * (b.hi[1] - b.lo[1] + 1) * (b.hi[2] - b.lo[2] + 1);
+}
+
+// nearest vertex of the grid point of every row of the box; the row takes that vertex's monitor
+// value.  Rows are enumerated in storage order (coalesced writes); the row's grid point follows
+// the host set-up's layout: 2D row j(nx+1) + i holds point (i, j); 3D row (nx+1)(ny+1)k + i(nx+1) + j
+// holds point (i, j, k) (src/MeshInterpolator.cpp:234: x and y swapped), i.e. storage (sx, sy) is
+// point (sy, sx).
 template <int D>
 __global__ void __launch_bounds__(kRB) k_nn_fill(const double* __restrict__ X, CellGrid cg,
                                                  const int* __restrict__ starts, const int* __restrict__ cellNodes,
                                                  const double* __restrict__ gx, const double* __restrict__ gy,
                                                  const double* __restrict__ gz, int nx, int ny, int nz,
-                                                 const double* __restrict__ monVals, double* __restrict__ vals) {
+                                                 const double* __restrict__ monVals, double* __restrict__ vals,
+                                                 GridBox box) {
   constexpr int DD = D * D;
   const long long p = (long long)blockIdx.x * kRB + threadIdx.x;
-  const long long npts = (long long)(nx + 1) * (ny + 1) * (D == 3 ? nz + 1 : 1);
-  if (p >= npts) return;
-  // p enumerates (i fastest, then j, then k); rows follow the host set-up's layout
-  const int i = (int)(p % (nx + 1));
-  const int j = (int)((p / (nx + 1)) % (ny + 1));
-  const int k = (D == 3) ? (int)(p / ((long long)(nx + 1) * (ny + 1))) : 0;
+  if (p >= box_rows(box)) return;
+  int sx, sy, k;
+  const size_t row = box_row(box, p, nx, ny, sx, sy, k);
+  const int i = (D == 2) ? sx : sy, j = (D == 2) ? sy : sx;
   double q[3] = {gx[i], gy[j], D == 3 ? gz[k] : 0.0};
-  size_t row;
-  if constexpr (D == 2)
-    row = (size_t)j * (nx + 1) + i;
-  else  // src/MeshInterpolator.cpp:234: (nx+1)(ny+1)k + i(nx+1) + j (x and y swapped)
-    row = (size_t)(nx + 1) * (ny + 1) * k + (size_t)i * (nx + 1) + j;
   int c[3] = {0, 0, 0};
   cellOf<D>(q, cg, c);
   double best = INFINITY;
@@ -172,15 +182,13 @@ __global__ void __launch_bounds__(kRB) k_nn_fill(const double* __restrict__ X, C
 // smoothMonitorGrid (src/MeshInterpolator.cpp:366-404): one Jacobi pass, interior points
 template <int D>
 __global__ void __launch_bounds__(kRB) k_smooth(const double* __restrict__ in, double* __restrict__ out, int nx,
-                                                int ny, int nz) {
+                                                int ny, int nz, GridBox box) {
   constexpr int DD = D * D;
-  const long long c = (long long)blockIdx.x * kRB + threadIdx.x;
+  const long long p = (long long)blockIdx.x * kRB + threadIdx.x;
   const long long P = (long long)(nx + 1) * (ny + 1);
-  const long long rows = P * (D == 3 ? nz + 1 : 1);
-  if (c >= rows) return;
-  const int i = (int)(c % (nx + 1));
-  const int j = (int)((c / (nx + 1)) % (ny + 1));
-  const int k = (D == 3) ? (int)(c / P) : 0;
+  if (p >= box_rows(box)) return;
+  int i, j, k;
+  const long long c = (long long)box_row(box, p, nx, ny, i, j, k);
   const bool interior = i >= 1 && i < nx && j >= 1 && j < ny && (D == 2 || (k >= 1 && k < nz));
   for (int q = 0; q < DD; ++q) {
     double v;
@@ -198,6 +206,24 @@ __global__ void __launch_bounds__(kRB) k_smooth(const double* __restrict__ in, d
           h * in[(c - nx - 1) * DD + q] + h * in[(c + P) * DD + q] + h * in[(c - P) * DD + q];
     }
     out[c * DD + q] = v;
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(kRB) k_box_commit(const double* __restrict__ src, double* __restrict__ vals,
+                                                    double* __restrict__ pad, int nx, int ny, int nz, GridBox box) {
+  constexpr int DD = D * D;
+  const long long c = (long long)blockIdx.x * kRB + threadIdx.x;
+  const long long P = (long long)(nx + 1) * (ny + 1);
+  if (c >= P * (D == 3 ? nz + 1 : 1)) return;
+  const int i = (int)(c % (nx + 1)), j = (int)((c / (nx + 1)) % (ny + 1)), k = (D == 3) ? (int)(c / P) : 0;
+  const bool in = i >= box.lo[0] && i <= box.hi[0] && j >= box.lo[1] && j <= box.hi[1] && k >= box.lo[2] &&
+                  k <= box.hi[2];
+  const double nan = __builtin_nan("");
+  for (int q = 0; q < DD; ++q) vals[c * DD + q] = in ? src[c * DD + q] : nan;
+  if (D == 3 && pad) {
+    for (int q = 0; q < DD; ++q) pad[c * 10 + q] = in ? src[c * DD + q] : nan;
+    pad[c * 10 + 9] = 0.0;
   }
 }
 
@@ -248,19 +274,31 @@ void launch_monitor_tv(const double* X, int n, const double* c, double* monVals,
   hipLaunchKernelGGL(k_monitor_tv<D>, dim3(blocks(n)), dim3(kRB), 0, st, X, n, c[0], c[1], c[2], monVals);
 }
 
-template <int D>
-void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, const int* cellNodes, const double* gx,
-                    const double* gy, const double* gz, int nx, int ny, int nz, const double* monVals, double* vals,
-                    hipStream_t st) {
-  const long long npts = (long long)(nx + 1) * (ny + 1) * (D == 3 ? nz + 1 : 1);
-  hipLaunchKernelGGL(k_nn_fill<D>, dim3(blocks(npts)), dim3(kRB), 0, st, X, cg, starts, cellNodes, gx, gy, gz, nx, ny,
-                     nz, monVals, vals);
+static long long host_box_rows(const GridBox& b) {
+  return (long long)(b.hi[0] - b.lo[0] + 1) * (b.hi[1] - b.lo[1] + 1) * (b.hi[2] - b.lo[2] + 1);
 }
 
 template <int D>
-void launch_smooth(const double* in, double* out, int nx, int ny, int nz, hipStream_t st) {
+void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, const int* cellNodes, const double* gx,
+                    const double* gy, const double* gz, int nx, int ny, int nz, const double* monVals, double* vals,
+                    const GridBox& box, hipStream_t st) {
+  const long long n = host_box_rows(box);
+  if (n > 0)
+    hipLaunchKernelGGL(k_nn_fill<D>, dim3(blocks(n)), dim3(kRB), 0, st, X, cg, starts, cellNodes, gx, gy, gz, nx, ny,
+                       nz, monVals, vals, box);
+}
+
+template <int D>
+void launch_smooth(const double* in, double* out, int nx, int ny, int nz, const GridBox& box, hipStream_t st) {
+  const long long n = host_box_rows(box);
+  if (n > 0) hipLaunchKernelGGL(k_smooth<D>, dim3(blocks(n)), dim3(kRB), 0, st, in, out, nx, ny, nz, box);
+}
+
+template <int D>
+void launch_box_commit(const double* src, double* vals, double* pad, int nx, int ny, int nz, const GridBox& box,
+                       hipStream_t st) {
   const long long rows = (long long)(nx + 1) * (ny + 1) * (D == 3 ? nz + 1 : 1);
-  hipLaunchKernelGGL(k_smooth<D>, dim3(blocks(rows)), dim3(kRB), 0, st, in, out, nx, ny, nz);
+  hipLaunchKernelGGL(k_box_commit<D>, dim3(blocks(rows)), dim3(kRB), 0, st, src, vals, pad, nx, ny, nz, box);
 }
 
 void launch_rows_gather(int D, const int* idx, int n, const double* in, double* out, hipStream_t st) {
@@ -277,8 +315,9 @@ void launch_rows_scatter(int D, const int* idx, int n, const double* in, double*
   template void launch_monitor_tv<D>(const double*, int, const double*, double*, hipStream_t);                  \
   template void launch_nn_fill<D>(const double*, const CellGrid&, const int*, const int*, const double*,        \
                                   const double*, const double*, int, int, int, const double*, double*,          \
-                                  hipStream_t);                                                                \
-  template void launch_smooth<D>(const double*, double*, int, int, int, hipStream_t);
+                                  const GridBox&, hipStream_t);                                                \
+  template void launch_smooth<D>(const double*, double*, int, int, int, const GridBox&, hipStream_t);           \
+  template void launch_box_commit<D>(const double*, double*, double*, int, int, int, const GridBox&, hipStream_t);
 MMX_REGRID_INST(2)
 MMX_REGRID_INST(3)
 #undef MMX_REGRID_INST

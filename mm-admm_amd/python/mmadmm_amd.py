@@ -45,7 +45,8 @@ class mmadmm_stats(ctypes.Structure):
                 ("prox_bytes", ctypes.c_double), ("xupdate_bytes", ctypes.c_double),
                 ("newton_iters", ctypes.c_longlong), ("jacobians", ctypes.c_longlong),
                 ("cg_iters", ctypes.c_longlong), ("t_jac_ms", ctypes.c_double), ("t_solve_ms", ctypes.c_double),
-                ("t_be_ms", ctypes.c_double), ("regrids", ctypes.c_longlong)]
+                ("t_be_ms", ctypes.c_double), ("regrids", ctypes.c_longlong), ("regrid_rows", ctypes.c_longlong),
+                ("regrid_gather_bytes", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

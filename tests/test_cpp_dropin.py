@@ -140,3 +140,23 @@ def test_python_monitor_subclass_equals_builtin():
     for _ in range(3):
         assert a.step(10, -1.0) == b.step(10, -1.0)
     np.testing.assert_array_equal(a.get("x"), b.get("x"))
+
+
+def test_meshutils_header():
+    """include/mmadmm/MeshUtils.h -- the reference's utils:: surface used by main.cpp's set-up
+    functions (linspace, findLimInfMeshPoint, generateUniformRectMesh, removeRow,
+    meshFromLevelSetFun 2D/3D with the caller's phi, readTriangles) -- compiles against the
+    reference's signatures and equals the library's generators bit for bit (host only)."""
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, "meshutils_check")
+    cmd = ["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wall", "-Wno-unused-variable",
+           "-I", os.path.join(INC, "mmadmm", "eigen_shim"), "-I", os.path.join(INC, "mmadmm"),
+           os.path.join(ROOT, "tests", "cpp", "meshutils_check.cpp"), "-o", exe,
+           "-L", os.path.join(ROOT, "mm-admm_amd", "lib"), "-lmmadmm", "-Wl,-rpath,$ORIGIN/../../mm-admm_amd/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "BaseCircle")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 7 and all(" ok" in ln for ln in lines), r.stdout

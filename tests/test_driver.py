@@ -70,8 +70,8 @@ def test_dry_run_shoulder(tmp_path):
 
 
 def test_unsupported_is_reported(tmp_path):
-    cfg = dict(MONITOR210, TestType="LevelSet", Dim=3, nz=10, za=0, zb=1)
-    r = _run(_root(tmp_path, "Ls3", cfg), "Ls3", "0", "1", "--dry-run")
+    cfg = dict(MONITOR210, TestType="Annulus")  # not a TestType of main.cpp
+    r = _run(_root(tmp_path, "An", cfg), "An", "0", "1", "--dry-run")
     assert r.returncode == 2 and "not available" in r.stderr
     r = _run(_root(tmp_path / "m3", "Monitor210", MONITOR210), "Monitor210", "3", "1", "--dry-run")
     assert r.returncode == 2 and "unknown Method" in r.stderr

@@ -122,7 +122,7 @@ TRACES = sorted((n, m) for n in os.listdir(GOLDEN) if os.path.isdir(os.path.join
 # its JSON describes after this many rows; only that prefix is a pin.  Run past it, the JSON's
 # trajectory inverts an element (the reference would abort on assert(Edet > 0)), so the driver is
 # given the config with nSteps = prefix - 1.
-STALE_PREFIX = {("Monitor1160", 0): 23, ("Monitor1320", 0): 23, ("Monitor140", 0): 7}
+STALE_PREFIX = {("Monitor1160", 0): 23, ("Monitor1320", 0): 23, ("Monitor140", 0): 7, ("Monitor180", 0): 7}
 
 
 @pytest.mark.gpu

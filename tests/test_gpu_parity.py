@@ -225,3 +225,45 @@ def test_xupdate_slot_terms_bitwise(dim, ts, monkeypatch):
         G.step(5, tol)
     np.testing.assert_array_equal(G.get("x"), O.get("x"))
     np.testing.assert_array_equal(G.get("z"), O.get("z"))
+
+
+@pytest.mark.parametrize("name", ["rect3d_3_mex1", "circle3d6_compmesh"])
+@pytest.mark.parametrize("force_tie", [0, 2])
+def test_quad_lane_prox_bitwise(name, force_tie, monkeypatch):
+    """The cooperative 3D prox (k_prox_quad, four lanes per tetrahedron, MMX_PROX3D=quad) against
+    the oracle bit for bit, alone and with every second block sent down its exact instance
+    (MMX_FORCE_TIE=2), which strides over the tie queue with a grid of workgroups."""
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    monkeypatch.setenv("MMX_PROX3D", "quad")
+    if force_tie:
+        monkeypatch.setenv("MMX_FORCE_TIE", str(force_tie))
+    O, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    for s in range(3):
+        ih_o = O.step(5, -1.0)[0]
+        ih_g = G.step(5, -1.0)[0]
+        assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
+        for f in ("x", "z", "u"):
+            np.testing.assert_array_equal(G.get(f), O.get(f), err_msg=f"{f} step {s}")
+    np.testing.assert_array_equal(G.get("hess"), O.get("hess"))
+    assert G.stats()["bfgs_iters"] == O.bfgs_iters()
+
+
+def test_quad_lane_prox_equals_wave_at_c4(monkeypatch):
+    """C4 (3,000,564 tets): one step of 10 iterations with k_prox_quad equals k_prox_wave bit for
+    bit (state and Bkinv), with and without forced exact recomputation of every 7th block."""
+    m = mx.MeshData.rect(3, 63)
+    M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 6), rho=2000.0, tau=0.5)
+    W = mx.Engine(M, 0.025)
+    W.step(10, -1.0)
+    W.step(10, -1.0)
+    monkeypatch.setenv("MMX_PROX3D", "quad")
+    monkeypatch.setenv("MMX_FORCE_TIE", "7")
+    Q = mx.Engine(M, 0.025)
+    Q.step(10, -1.0)
+    Q.step(10, -1.0)
+    for f in ("x", "z", "u", "hess"):
+        np.testing.assert_array_equal(Q.get(f), W.get(f), err_msg=f)
+    assert Q.stats()["bfgs_iters"] == W.stats()["bfgs_iters"]
+    W.close()
+    Q.close()

@@ -98,11 +98,22 @@ def test_partitioned_equals_single(mx, name, gen, dim, mon, rho, tau, dt, nranks
     comm.close()
 
 
-@pytest.mark.parametrize("mon,dim,nranks", [(7, 2, 2), (1, 2, 3), (7, 3, 2)])
-def test_partitioned_regrid_equals_single(mx, mon, dim, nranks):
+def _check_rank_grid(e, gr, r):
+    """A rank's rebuilt grid: the rows of its box equal the single-GPU grid, the others are NaN."""
+    g = e.get("grid")
+    ok = ~np.isnan(g)
+    assert ok.any(), f"rank {r}: empty box"
+    assert np.array_equal(g[ok], gr[ok]), f"rank {r}: grid rows differ"
+    st = e.stats()
+    assert 0 < st["regrid_rows"] <= len(g) // (e.dim * e.dim)
+
+
+@pytest.mark.parametrize("mon,dim,nranks,n", [(7, 2, 2, 12), (1, 2, 3, 12), (7, 3, 2, 4), (7, 2, 4, 40), (7, 3, 4, 10)])
+def test_partitioned_regrid_equals_single(mx, mon, dim, nranks, n):
     """Time-varying monitor on a partition: every rank all-gathers the vertex positions and
-    rebuilds the same grid; node positions stay bit-identical to the single-GPU run."""
-    mesh = mx.MeshData.rect(dim, 12 if dim == 2 else 4)
+    rebuilds the grid rows its simplices can reach (NaN elsewhere); node positions stay
+    bit-identical to the single-GPU run."""
+    mesh = mx.MeshData.rect(dim, n)
     M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, mon), rho=200.0, tau=0.5, device=0)
     ref = mx.Engine(M, 0.05)
     ref.set_regrid(True)
@@ -124,10 +135,38 @@ def test_partitioned_regrid_equals_single(mx, mon, dim, nranks):
     xr = ref.get("x").reshape(-1, dim)
     gr = ref.get("grid")
     for r, e in enumerate(parts):
-        assert np.array_equal(e.get("grid"), gr), f"rank {r}: grid differs"
+        _check_rank_grid(e, gr, r)
         assert np.array_equal(e.get("x").reshape(-1, dim), xr[e.local_nodes()]), f"rank {r}: positions differ"
         assert e.stats()["regrids"] == steps
     for e in parts:
+        e.close()
+    comm.close()
+
+
+def test_c4_eight_ranks_regrid_equals_single(mx):
+    """C4 (3D SquareGrid n = 63, 512,191 nodes, 3,000,564 tets) on an 8-rank loopback partition
+    with the time-varying monitor rebuilt every step: one step of 3 ADMM iterations, node
+    positions bit-identical to one GPU, each rank's grid rows equal to the single-GPU grid inside
+    its box, and each rank fills well under the whole grid."""
+    mesh = mx.MeshData.rect(3, 63)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(3, 7), rho=2000.0, tau=0.5, device=0)
+    ref = mx.Engine(M, 0.025)
+    ref.set_regrid(True)
+    ref.step(3, -1.0)
+    xr = ref.get("x").reshape(-1, 3)
+    gr = ref.get("grid")
+    total = len(gr) // 9
+    ref.close()
+    nranks = 8
+    comm = mx.Comm.loopback(nranks)
+    parts = [mx.Engine(M, 0.025, rank=r, nranks=nranks, comm=comm) for r in range(nranks)]
+    for e in parts:
+        e.set_regrid(True)
+    _run_parallel([(lambda e: (lambda: e.step(3, -1.0)))(e) for e in parts])
+    for r, e in enumerate(parts):
+        assert np.array_equal(e.get("x").reshape(-1, 3), xr[e.local_nodes()]), f"rank {r}: positions differ"
+        _check_rank_grid(e, gr, r)
+        assert e.stats()["regrid_rows"] < 0.5 * total, (r, e.stats()["regrid_rows"], total)
         e.close()
     comm.close()
 
