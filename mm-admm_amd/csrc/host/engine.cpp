@@ -234,8 +234,8 @@ class Engine final : public EngineBase {
     }
     z_.alloc((size_t)nF_ * K);
     gcache_.alloc((size_t)nF_ * (K + 1));
-    tieList_.alloc((size_t)nF_ / 64 + 1);  // prox blocks queued for the exact recomputation
-    tieCount_.alloc(2);  // [0] queued blocks, [1] workgroups of the exact pass done with the queue
+    tieList_.alloc((size_t)nF_ / 16 + 1);  // prox blocks queued for the exact recomputation
+    tieCount_.alloc(2);  // queued blocks, double-buffered over the steady proxes (k_prox_fix)
     MMX_HIP(hipMemsetAsync(tieCount_.p, 0, 2 * sizeof(unsigned), st_));
     u_.alloc((size_t)nF_ * K);
     gs_.alloc((size_t)nF_ * K);
@@ -249,8 +249,9 @@ class Engine final : public EngineBase {
       launch_bkinv_identity<D>(nF_, B_.p, st_);
       if (D == 3) B2_.alloc(nB);
     }
-    // prox workgroups can be 64 lanes; node kernels pad their grid to a multiple of 8 (XCD map)
-    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 63) / 64, (nP_ + 255) / 256 + 8));
+    // prox workgroups take 16 (3D quad) to 256 simplices; node kernels pad their grid to a multiple of 8 (XCD map)
+    // (k_prox_quad: 16 tets per workgroup)
+    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 15) / 16, (nP_ + 255) / 256 + 8));
     maxBlocks_ = maxBlocks;
     partA_.alloc(maxBlocks * kNumPartials);
     partB_.alloc(maxBlocks * kNumPartials);
@@ -317,6 +318,10 @@ class Engine final : public EngineBase {
       }
       const bool firstProx = !hessComputed_;          // another kernel, another partial count
       const bool swapB = (D == 3) && hessComputed_;  // 3D steady state: B_ -> B2_, then swap
+      if (hessComputed_) {  // fast + exact pair: flip the tie queue
+        tiePar_ ^= 1;
+        std::swap(m_.tieCount, m_.tieStale);
+      }
       launch_prox<D>(m_, !hessComputed_, gcacheValid_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p,
                      swapB ? B2_.p : B_.p, partA_.p + (deferRed ? slice * i : 0), &nbp, st_);
       if (swapB) std::swap(B_.p, B2_.p);
@@ -867,8 +872,8 @@ class Engine final : public EngineBase {
     m.tslot = tslotOn_ ? tslot_.p : nullptr;
     m.gcache = gcache_.p;
     m.tieList = tieList_.p;
-    m.tieCount = tieCount_.p;
-    m.tieDone = tieCount_.p + 1;
+    m.tieCount = tieCount_.p + tiePar_;  // keep the queue's parity across a rebuilt view (regrid)
+    m.tieStale = tieCount_.p + (tiePar_ ^ 1);
     m.nodeOrder = nodeOrder_.p;
     {
       const char* ft = getenv("MMX_FORCE_TIE");
@@ -954,6 +959,7 @@ class Engine final : public EngineBase {
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
   DevBuf<int32_t> expOff_, tieList_, nodeOrder_;
   DevBuf<unsigned> tieCount_;
+  int tiePar_ = 0;
   PartitionPlan plan_;
   Comm* comm_ = nullptr;
   int rank_ = 0, nranks_ = 1;

@@ -792,21 +792,14 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
 // with cr_resolve, Bkinv in registers and a full entry blockGrad (bit-identical to the cached
 // form, which the fast pass may have overwritten), and the block's partials are formed with the
 // same workgroup shape -- the same values in the same tree.  The workgroups of a fixed grid (one
-// per CU at most) stride over the list, so a prox with many ties is not serialised on one CU; the
-// last workgroup to finish re-arms the counter for the next prox (with no ties each workgroup only
-// reads the counter).
-__device__ __forceinline__ void rearm_tie_queue(unsigned* tieCount, unsigned* tieDone) {
-  __shared__ unsigned last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = (atomicAdd(tieDone, 1u) == gridDim.x - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    *tieCount = 0u;
-    *tieDone = 0u;
-  }
+// per CU at most) stride over the list, so a prox with many ties is not serialised on one CU (with
+// no ties each workgroup only reads the counter).  The queue counters are double-buffered over the
+// steady proxes: this prox's recomputation clears the previous prox's counter (whose recomputation
+// has finished, stream order), which the next prox appends to -- a plain store, no atomics.  The queue counters are double-buffered over the steady proxes: this prox's
+// recomputation clears the previous prox's counter (whose recomputation has finished, stream
+// order), which the next prox appends to -- a plain store, no completion atomics.
+__device__ __forceinline__ void rearm_tie_queue(unsigned* tieStale) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *tieStale = 0u;
 }
 template <int D, int BS>
 __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, const double* __restrict__ x,
@@ -821,7 +814,7 @@ __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, co
     block_partials<6, BS>(pv, partials, b);
     __syncthreads();
   }
-  rearm_tie_queue(m.tieCount, m.tieDone);
+  rearm_tie_queue(m.tieStale);
 }
 
 // Steady-state prox (every prox after the first), Bkinv staged through LDS.  The workgroup's
@@ -1262,29 +1255,31 @@ __device__ __forceinline__ double blockGradQuad(const GridView<3>& g, const Func
   return Ih;
 }
 
-// The steady-state 3D prox with four lanes per tetrahedron (see above).  One workgroup of 256
-// lanes = the 64 tets of one group of the wave-interleaved Bkinv layout (bidx<3>); Bkinv is
-// double-buffered as for k_prox_wave (Bin only read, Bout written).  EXACT = false is the fast
-// path (no tie resolution, Markstein divisions): a block that meets a near-midpoint power or a
-// quotient outside div_mk's range writes nothing back and is queued; EXACT = true recomputes the
-// queued blocks (the workgroups stride over the queue) with the exact decisions, a full entry
-// blockGrad and the same partial-sum tree, and the last workgroup to finish re-arms the queue.
-constexpr int kQuadImg = 36 * 64 + 16;  // doubles per quad-lane block of k_prox_quad's LDS image
-template <bool COMP, bool EXACT>
-__global__ void __launch_bounds__(256, 2) k_prox_quad(DeviceMesh<3> m, double tol, const double* __restrict__ x,
-                                                       double* __restrict__ zg, double* __restrict__ ug,
-                                                       const double* Bin, double* Bout,
-                                                       double* __restrict__ partials, int useCache) {
-  constexpr int K = 12, KK = 144;
-  // LDS image of the block's Bkinv: quad lane k's rows of the 64 tets in block k (3 x 12 entries of
-  // 64 tets), the blocks 32 dwords apart in the banks, so a wavefront's access to one entry of its
-  // 16 tets x 4 quad lanes takes the minimum two passes
-  __shared__ __attribute__((aligned(16))) double img[4 * kQuadImg];
+// The steady-state 3D prox with four lanes per tetrahedron (see above).  A workgroup of QW lanes
+// takes QW / 4 consecutive tets (a quarter or all of one group of the wave-interleaved Bkinv layout,
+// bidx<3>); Bkinv is double-buffered as for k_prox_wave (Bin only read, Bout written).  EXACT =
+// false is the fast path (no tie resolution, Markstein divisions): a block that meets a
+// near-midpoint power or a quotient outside div_mk's range writes nothing back and is queued;
+// EXACT = true recomputes the queued blocks (the workgroups stride over the queue) with the exact
+// decisions, a full entry blockGrad and the same partial-sum tree, and the last workgroup to finish
+// re-arms the queue.
+template <int TB>
+constexpr int kQuadImg = 36 * TB + 8;  // doubles per quad-lane block of the LDS image (bank offset 16 dwords)
+template <bool COMP, bool EXACT, int QW>
+__global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol, const double* __restrict__ x,
+                                                             double* __restrict__ zg, double* __restrict__ ug,
+                                                             const double* Bin, double* Bout,
+                                                             double* __restrict__ partials, int useCache) {
+  constexpr int K = 12, KK = 144, TB = QW / 4, KB = kQuadImg<TB>;
+  // LDS image of the block's Bkinv: quad lane k's rows of the TB tets in block k (3 x 12 entries of
+  // TB tets); the four blocks 16 dwords apart in the banks, so the 32 lanes of a half-wavefront (8
+  // tets x 4 quad lanes) reading one entry hit 64 distinct banks
+  __shared__ __attribute__((aligned(16))) double img[4 * KB];
   const int tid = threadIdx.x, k = tid & 3, tl = tid >> 2;
   const unsigned nWork = EXACT ? *m.tieCount : 1u;
   for (unsigned w = EXACT ? blockIdx.x : 0u; w < nWork; w += EXACT ? gridDim.x : 1u) {
     const int lb = EXACT ? m.tieList[w] : logical_block_any();
-    const int s0 = lb * 64;
+    const int s0 = lb * TB;
     const bool act = s0 + tl < m.nF;
     const int s = act ? s0 + tl : s0;
     const int fk = m.F[(size_t)s * 4 + k];
@@ -1315,16 +1310,17 @@ __global__ void __launch_bounds__(256, 2) k_prox_quad(DeviceMesh<3> m, double to
     }
     // the block's Bkinv chunk (64 tets x 144, contiguous in the wave-interleaved layout) staged
     // through LDS with 16-byte coalesced loads, then this lane's three rows into registers
-    const size_t gb = (size_t)lb * KK * 64;
+    // the block's TB tets in their group of 64: entry ij of tet s0 + t at gb + ij 64 + t
+    const size_t gb = (size_t)(s0 >> 6) * KK * 64 + (s0 & 63);
 #pragma unroll 6
-    for (int e = tid * 2; e < KK * 64; e += 512) {
-      const v2nt v = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(Bin + gb + e));
-      const int ij = e >> 6, t = e & 63, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
-      *reinterpret_cast<v2nt*>(&img[kk * kQuadImg + (r * K + j) * 64 + t]) = v;
+    for (int e = tid * 2; e < KK * TB; e += 2 * QW) {
+      const int ij = e / TB, t = e % TB, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
+      const v2nt v = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(Bin + gb + (size_t)ij * 64 + t));
+      *reinterpret_cast<v2nt*>(&img[kk * KB + (r * K + j) * TB + t]) = v;
     }
     // entry (r, j) of this lane's rows at mine[(r K + j) 64]: read into registers by each pass (not
     // held across the blockGrad), the new values written back by the update pass
-    double* const mine = img + k * kQuadImg + tl;
+    double* const mine = img + k * KB + tl;
     __syncthreads();
     double pv[6] = {0, 0, 0, 0, 0, 0};
     bool tie = false;
@@ -1358,7 +1354,7 @@ __global__ void __launch_bounds__(256, 2) k_prox_quad(DeviceMesh<3> m, double to
           for (int r = 0; r < 3; ++r) {
             double row[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) row[j] = mine[(r * K + j) * 64];
+            for (int j = 0; j < K; ++j) row[j] = mine[(r * K + j) * TB];
             double sacc = (-row[0]) * Gf[0];
 #pragma unroll
             for (int j = 1; j < K; ++j) sacc += (-row[j]) * Gf[j];
@@ -1409,7 +1405,7 @@ __global__ void __launch_bounds__(256, 2) k_prox_quad(DeviceMesh<3> m, double to
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
-          for (int j = 0; j < K; ++j) rows[r][j] = mine[(r * K + j) * 64];
+          for (int j = 0; j < K; ++j) rows[r][j] = mine[(r * K + j) * TB];
         {
           double byo[3], byf[K];
 #pragma unroll
@@ -1465,7 +1461,7 @@ __global__ void __launch_bounds__(256, 2) k_prox_quad(DeviceMesh<3> m, double to
               nb = rows[r][j] + (((c1 * (po[r] * pj)) - div_mk(by, c2, rc2)) - div_mk(po[r] * yBj, c2, rc2));
               fin = cr_fma(nb, 0.0, fin);
             }
-            mine[(r * K + j) * 64] = nb;
+            mine[(r * K + j) * TB] = nb;
           }
         }
         if constexpr (!EXACT) {
@@ -1520,15 +1516,15 @@ __global__ void __launch_bounds__(256, 2) k_prox_quad(DeviceMesh<3> m, double to
     if constexpr (EXACT) __syncthreads();  // (the fast path's __syncthreads_or orders the image)
     // the new Bkinv chunk back with 16-byte coalesced stores (inactive tets: the unchanged image)
 #pragma unroll 6
-    for (int e = tid * 2; e < KK * 64; e += 512) {
-      const int ij = e >> 6, t = e & 63, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
-      const v2nt v = *reinterpret_cast<const v2nt*>(&img[kk * kQuadImg + (r * K + j) * 64 + t]);
-      __builtin_nontemporal_store(v, reinterpret_cast<v2nt*>(Bout + gb + e));
+    for (int e = tid * 2; e < KK * TB; e += 2 * QW) {
+      const int ij = e / TB, t = e % TB, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
+      const v2nt v = *reinterpret_cast<const v2nt*>(&img[kk * KB + (r * K + j) * TB + t]);
+      __builtin_nontemporal_store(v, reinterpret_cast<v2nt*>(Bout + gb + (size_t)ij * 64 + t));
     }
-    block_partials<6, 256>(pv, partials, lb);
+    block_partials<6, QW>(pv, partials, lb);
     if constexpr (EXACT) __syncthreads();  // the partials scratch is reused by the next block
   }
-  if constexpr (EXACT) rearm_tie_queue(m.tieCount, m.tieDone);
+  if constexpr (EXACT) rearm_tie_queue(m.tieStale);
 }
 
 // Mesh::computeEnergy (src/Mesh.cpp:496-530) on positions x
@@ -1930,6 +1926,10 @@ static int prox3d_quad() {
   return (e && std::string(e) == "quad") ? 1 : 0;
 }
 constexpr int kFixGrid = 256;  // workgroups of the exact (tie) recomputation: at most one per CU
+#ifndef MMX_QUAD_TETS
+#define MMX_QUAD_TETS 64
+#endif
+constexpr int kQuadTets = MMX_QUAD_TETS;  // tets per k_prox_quad workgroup (64: 4.03 ms at C4, 16: 4.37 ms)
 
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z, double* u,
@@ -1957,15 +1957,19 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
   } else {
     *nblocks = (m.nF + 63) / 64;
     const dim3 fg(std::min(*nblocks, kFixGrid));
-    if (prox3d_quad()) {  // four lanes per tetrahedron; the exact instance recomputes queued blocks
+    if (prox3d_quad()) {  // four lanes per tetrahedron, 16 per workgroup; the exact instance recomputes queued blocks
+      *nblocks = (m.nF + kQuadTets - 1) / kQuadTets;
+      const dim3 qg(std::min(*nblocks, kFixGrid));
       if (m.compMesh) {
-        hipLaunchKernelGGL((k_prox_quad<true, false>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, Bin, Bout,
-                           partials, uc);
-        hipLaunchKernelGGL((k_prox_quad<true, true>), fg, dim3(256), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+        hipLaunchKernelGGL((k_prox_quad<true, false, 4 * kQuadTets>), dim3(*nblocks), dim3(4 * kQuadTets), 0, st, m,
+                           tol, x, z, u, Bin, Bout, partials, uc);
+        hipLaunchKernelGGL((k_prox_quad<true, true, 4 * kQuadTets>), qg, dim3(4 * kQuadTets), 0, st, m, tol, x, z, u,
+                           Bin, Bout, partials, 0);
       } else {
-        hipLaunchKernelGGL((k_prox_quad<false, false>), dim3(*nblocks), dim3(256), 0, st, m, tol, x, z, u, Bin, Bout,
-                           partials, uc);
-        hipLaunchKernelGGL((k_prox_quad<false, true>), fg, dim3(256), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+        hipLaunchKernelGGL((k_prox_quad<false, false, 4 * kQuadTets>), dim3(*nblocks), dim3(4 * kQuadTets), 0, st, m,
+                           tol, x, z, u, Bin, Bout, partials, uc);
+        hipLaunchKernelGGL((k_prox_quad<false, true, 4 * kQuadTets>), qg, dim3(4 * kQuadTets), 0, st, m, tol, x, z, u,
+                           Bin, Bout, partials, 0);
       }
       return;
     }
