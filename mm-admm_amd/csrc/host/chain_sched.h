@@ -8,8 +8,11 @@
 //   * bands: 64 consecutive chains, one per lane of a wavefront; lane l processes position
 //     p = t - skew[l] of its chain at iteration t, with static skews that satisfy every
 //     dependency inside the band, whose values pass through a per-lane LDS ring;
+//   * segments: a row wider than 32 entries (3D) takes ns consecutive positions of its lane, 32
+//     entries each, its partial sum carried in a register; every row of a chain has the same ns;
 //   * imports: values from other bands (or too old for the ring) are copied from the global
-//     granules into an LDS import ring by a helper wavefront, in order of first use; it publishes
+//     granules into LDS import slots by a helper wavefront, in order of first use (slots assigned
+//     by interval colouring: the slot whose previous import's last use has passed); it publishes
 //     how many it has delivered, and iteration t waits for impNeed[t] (the highest it reads).
 // Entries address one LDS array: [0] = +0.0 (pads: value 0 times +0.0 changes nothing, not even
 // the sign of a zero), [1, 1 + 64 (R+1)) the lane rings, then RI import slots.
@@ -24,24 +27,31 @@ constexpr int kChainLanes = 64;
 constexpr int kChainRingMax = 32;    // LDS ring slots per lane (doubles) -- chain_sweep.hip kRingMax
 constexpr int kChainImpMax = 2048;   // LDS import slots (16-byte granules) -- chain_sweep.hip kImpMax
 constexpr int kChainPad = -2147483647 - 1;  // empty entry slot (schedule building only)
+constexpr int kChainSegMax = 4;      // segments of E = 32 entries a row may take (rows up to 128 entries)
 
 struct ChainSchedule {
   bool ok = false;
   std::string why;      // reason when !ok
   bool fwd = true;
-  int E = 0;            // entry slots per row (8, 16 or 32)
+  int E = 0;            // entry slots per row segment (8, 16 or 32)
+  bool seg = false;     // rows wider than 32 entries: split into segments at consecutive positions
   int R = 0;            // ring slots per lane (power of two); ring stride R + 1
   int RI = 0;           // import slots (power of two)
   int nbands = 0, nchains = 0, maxLen = 0, maxSkew = 0, maxT = 0;
   long long slots = 0;      // sum over bands of their iteration counts
   long long nImports = 0;
   long long estIters = 0;   // simulated critical path (iterations)
+  bool aligned = false;     // lane skews also wait for the lane's imports (chain_sched.cpp pass 1)
   std::vector<int> bandSlot, bandT, bandImp, bandNImp;  // per band
-  std::vector<int> laneStart, laneLen, laneSkew;        // per band * 64 + lane
+  std::vector<int> laneStart, laneLen, laneSkew;        // per band * 64 + lane (laneLen in positions)
+  std::vector<int> laneNs;                              // per band * 64 + lane: segments per row
   std::vector<int> code;   // per (slot * E + e) * 64 + lane: LDS index of the value (0 for pads)
   std::vector<int> src;    // same shape: index of the value in the factor (af), -1 for pads
   std::vector<int> dsrc;   // backward: per slot * 64 + lane, index of the diagonal in af (-1 idle)
   std::vector<int> impRow, impFree;  // per import: producer row; last iteration it is read
+  std::vector<int> impSlot, impWait; // per import: LDS slot; iterations to complete before it is
+                                     // delivered (the slot's previous import's last use, -1 none)
+  int maxImpSlots = 0;               // the most import slots a band uses
   std::vector<int> impNeed;          // per slot: highest import index read at that iteration (-1)
   std::vector<int> bandE;            // per band: entry slots in use (multiple of 4, <= E)
   std::vector<int> bandOrder;        // per ticket: the band taken (every band after the bands it

@@ -185,12 +185,12 @@ struct SparseMatrix {
   DevBuf<uint64_t> d_gy, d_gx;
   unsigned epoch = 0, fepoch = 0;
   // chain/band-scheduled sweeps (host/chain_sched.h); level-scheduled when a schedule is not
-  // possible (a triangle row wider than 32 entries) or MMX_SWEEP=level
+  // possible or MMX_SWEEP=level (rows wider than 32 entries: segmented schedule, chain_sched.h)
   struct ChainDir {
     int E = 0;
     long long nent = 0, nslot = 0;
-    DevBuf<int> bandSlot, bandT, bandImp, bandNImp, bandE, bandOrder, laneStart, laneLen, laneSkew, code, src, dsrc, impRow,
-        impFree, impNeed;
+    DevBuf<int> bandSlot, bandT, bandImp, bandNImp, bandE, bandOrder, laneStart, laneLen, laneSkew, laneNs, code, src, dsrc,
+        impRow, impSlot, impWait, impNeed;
     DevBuf<double> val, dval;
     ChainArgs args{};
   };
@@ -387,11 +387,13 @@ struct SparseMatrix {
     up(c.laneStart, S.laneStart);
     up(c.laneLen, S.laneLen);
     up(c.laneSkew, S.laneSkew);
+    up(c.laneNs, S.laneNs);
     up(c.code, S.code);
     up(c.src, S.src);
     up(c.dsrc, S.dsrc);
     up(c.impRow, S.impRow);
-    up(c.impFree, S.impFree);
+    up(c.impSlot, S.impSlot);
+    up(c.impWait, S.impWait);
     up(c.impNeed, S.impNeed);
     up(c.bandE, S.bandE);
     up(c.bandOrder, S.bandOrder);
@@ -406,8 +408,8 @@ struct SparseMatrix {
       MMX_HIP(hipMemsetAsync(d_cprof.p, 0, 1024 * sizeof(unsigned long long), st));
     }
     c.args = ChainArgs{c.bandSlot.p, c.bandT.p, c.bandImp.p, c.bandNImp.p, c.laneStart.p, c.laneLen.p, c.laneSkew.p,
-                       c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impFree.p, c.impNeed.p, c.bandOrder.p,
-                       S.nbands, S.R, S.RI,
+                       c.laneNs.p, c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impSlot.p, c.impWait.p, c.impNeed.p,
+                       c.bandOrder.p, S.nbands, S.R, S.RI, S.seg ? 1 : 0,
                        d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr, (pe && atoi(pe) >= 2) ? 1 : 0};
   }
 

@@ -941,22 +941,24 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 // wave-interleaved layout -- every access of a wavefront to one entry is 512 contiguous bytes --
 // and double-buffered (WaveB): the previous prox's buffer is only read, so a block whose fast
 // pass meets a near-midpoint power (EXACT = false) is abandoned unwritten and recomputed exactly
-// by k_prox_fix from the untouched inputs, as in the 2D kernel.
-template <int D, bool COMP>
+// by k_prox_wave_fix from the untouched inputs, as in the 2D kernel.
 #ifndef MMX_WAVE_OCC
 #define MMX_WAVE_OCC 1  // measured: one wave per SIMD (310 VGPRs); two (12-53 spills, p/G/DXpU parked in LDS) gain < 2%
 #endif
-__global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
-                                                     double* __restrict__ zg, double* __restrict__ ug,
-                                                     const double* Bin, double* Bout, double* __restrict__ partials,
-                                                     int useCache) {
-  constexpr int K = D * (D + 1), KK = K * K;
-  __shared__ double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 1];
-  const int tid = threadIdx.x;
 #ifndef MMX_WAVE_XCD
 #define MMX_WAVE_XCD 1  // measured C4: prox 3.42 -> 3.29 ms (neighbouring tets share x and monitor-grid lines in one L2)
 #endif
-  const int lb = MMX_WAVE_XCD ? logical_block_any() : (int)blockIdx.x;  // XCD-contiguous tet ranges
+// One block (64 tets) of the 3D steady-state prox.  EXACT = false (k_prox_wave): the fast path;
+// returns false, having written nothing, when a power met a near-midpoint (the block is queued).
+// EXACT = true (k_prox_wave_fix): the exact recomputation of a queued block, entry gradient
+// included (the fast pass may have left the cache at a point it then abandoned).
+template <int D, bool COMP, bool EXACT>
+__device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double tol, const double* __restrict__ x,
+                                                double* __restrict__ zg, double* __restrict__ ug, const double* Bin,
+                                                double* Bout, double* __restrict__ partials, int useCache, int lb,
+                                                double* ldsHeld) {
+  constexpr int K = D * (D + 1), KK = K * K;
+  const int tid = threadIdx.x;
   const int s0 = lb * 64;
   const bool act = s0 + tid < m.nF;
   const int s = act ? s0 + tid : s0;
@@ -972,7 +974,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     z[i] = zs[i];
     dx[i] = us[i];
   }
-  if (useCache) {
+  if (!EXACT && useCache) {
 #pragma unroll
     for (int i = 0; i <= K; ++i) gcv[i] = gc[i];
   }
@@ -992,7 +994,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     fc.compMesh = COMP ? 1 : 0;
     double G[K], Igt;
     bool bad = false;
-    entry_grad<D, false>(g, fc, z, xi, dx, gcv, useCache != 0, G, Igt, bad, &tie);
+    entry_grad<D, EXACT>(g, fc, z, xi, dx, gcv, !EXACT && useCache != 0, G, Igt, bad, &tie);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
     const size_t gb = (size_t)lb * KK * 64 + tid;
@@ -1000,7 +1002,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     {
       WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsHeld + tid)};
       its = tie ? 0
-                : bfgs_iterations<D, WaveB<K>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+                : bfgs_iterations<D, WaveB<K>, EXACT>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     }
     double dual2 = 0.0;
 #pragma unroll
@@ -1014,10 +1016,12 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     pv[4] = bad ? 1.0 : 0.0;
     pv[5] = (double)its;
   }
-  if (m.forceTie > 0 && tid == 0 && (int)((unsigned)lb % (unsigned)m.forceTie) == 0) tie = true;
-  if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to k_prox_fix
-    if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = lb;
-    return;
+  if constexpr (!EXACT) {
+    if (m.forceTie > 0 && tid == 0 && (int)((unsigned)lb % (unsigned)m.forceTie) == 0) tie = true;
+    if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to k_prox_wave_fix
+      if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = lb;
+      return;
+    }
   }
   if (act) {
     double un[K];
@@ -1030,6 +1034,35 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
     write_tslot<D>(m, s, z, un);
   }
   block_partials<6, 64>(pv, partials, lb);
+}
+
+template <int D, bool COMP>
+__global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+                                                     double* __restrict__ zg, double* __restrict__ ug,
+                                                     const double* Bin, double* Bout, double* __restrict__ partials,
+                                                     int useCache) {
+  constexpr int K = D * (D + 1);
+  __shared__ double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 1];
+  const int lb = MMX_WAVE_XCD ? logical_block_any() : (int)blockIdx.x;  // XCD-contiguous tet ranges
+  prox_wave_block<D, COMP, false>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
+}
+
+// The exact recomputation of the blocks k_prox_wave queued, with the same Bkinv streaming (the
+// generic one-lane k_prox_fix holds a tet's 144 Bkinv entries in registers and spills: ~0.3 ms
+// for one block).  A fixed grid strides over the queue, as k_prox_fix.
+template <int D, bool COMP>
+__global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave_fix(DeviceMesh<D> m, double tol,
+                                                         const double* __restrict__ x, double* __restrict__ zg,
+                                                         double* __restrict__ ug, const double* Bin, double* Bout,
+                                                         double* __restrict__ partials) {
+  constexpr int K = D * (D + 1);
+  __shared__ double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 1];
+  const unsigned n = *m.tieCount;
+  for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
+    prox_wave_block<D, COMP, true>(m, tol, x, zg, ug, Bin, Bout, partials, 0, m.tieList[i], ldsHeld);
+    __syncthreads();
+  }
+  rearm_tie_queue(m.tieStale);
 }
 
 // ---- 3D steady-state prox, four lanes per tetrahedron (k_prox_quad) ------------------------------
@@ -1973,11 +2006,13 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
       }
       return;
     }
-    if (m.compMesh)
+    if (m.compMesh) {
       hipLaunchKernelGGL((k_prox_wave<D, true>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
-    else
+      hipLaunchKernelGGL((k_prox_wave_fix<D, true>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+    } else {
       hipLaunchKernelGGL((k_prox_wave<D, false>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
-    hipLaunchKernelGGL((k_prox_fix<D, 64>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+      hipLaunchKernelGGL((k_prox_wave_fix<D, false>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+    }
   }
 }
 template <int D>

@@ -13,7 +13,9 @@
 //           order of first use, stores each into its slot once the slot is free and publishes the
 //           length of the delivered prefix.
 // Every row is x_i = (b_i - sum_k a_k x_jk) [/ d_i] with the terms subtracted in ascending column
-// order, exactly as the level-scheduled k_sweep and the reference.
+// order, exactly as the level-scheduled k_sweep and the reference.  SEG: a lane's rows take ns
+// positions each (32 entries per position, the partial sum carried in a register), for triangles
+// with rows wider than 32 entries (3D).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -100,7 +102,7 @@ __device__ __forceinline__ void prof_add(unsigned long long* prof, int i, unsign
   if (prof) atomicAdd(prof + i, v);
 }
 
-template <bool FWD, int PRO, int E>
+template <bool FWD, int PRO, int E, bool SEG>
 __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double* __restrict__ src,
                                                      double* __restrict__ pvec, const double* __restrict__ res,
                                                      const double* __restrict__ avbar, const CgsScalars* __restrict__ sc,
@@ -120,7 +122,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
   __shared__ int s_prog, s_band, s_impDone;
 
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int R = ca.R, RI = ca.RI;
+  const int R = ca.R;
   const int impBase = 1 + 64 * (R + 1);
   double beta = 0.0, omega = 0.0, alpha = 0.0;
   if (FWD && PRO == 1) {
@@ -144,10 +146,10 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
     const bool skip = aborted(err);
     const int sb = ca.bandSlot[b], T = ca.bandT[b];
     const int g = b * 64 + lane;
-    int cst = ca.laneStart[g], len = ca.laneLen[g], skew = ca.laneSkew[g];
+    int cst = ca.laneStart[g], len = ca.laneLen[g], skew = ca.laneSkew[g], ns = SEG ? ca.laneNs[g] : 1;
     // launder the loaded lane values: inside the loops they must not count as pending loads, or the
     // waitcnt pass waits for every younger store/DMA (vmcnt(0)) at each iteration
-    asm volatile("" : "+v"(cst), "+v"(len), "+v"(skew));
+    asm volatile("" : "+v"(cst), "+v"(len), "+v"(skew), "+v"(ns));
 
     if (skip) {
       // nothing: an earlier wait gave up; the host reports it
@@ -210,6 +212,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       // stage's tag, the import count, and the next stage's contents (valid when that tag, read
       // first and served first, says the stage has landed) -- then the chain
       int seen = 0;  // import count read by the previous batch
+      double carry = 0.0;  // SEG: the partial sum of a row whose next segment comes at the next position
       auto step = [&](int t, const Fetched& f, Fetched& nx) {
         const int need = __builtin_amdgcn_readfirstlane(f.need);
         if (need >= 0 && seen <= need) {  // imports this iteration reads: wait for their delivery
@@ -235,23 +238,33 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
         if (hasNext) load_stage(stn, nx);
         const int p = t - skew;
         if (p >= 0 && p < len) {
-          const int row = FWD ? cst + p : cst - p;
+          int ri = p, sg = 0;  // row of the chain, segment of the row
+          if constexpr (SEG) {
+            ri = p / ns;
+            sg = p - ri * ns;
+          }
+          const int row = FWD ? cst + ri : cst - ri;
           // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
-          double acc = f.init;
+          double acc = (SEG && sg != 0) ? carry : f.init;
 #pragma unroll
           for (int e0 = 0; e0 < E; e0 += 4)
             if (e0 < Eb) {
 #pragma unroll
               for (int q = 0; q < 4; ++q) acc -= f.a[e0 + q] * v[e0 + q];
             }
-          if (!FWD) acc = acc / f.diag;
-          s_dep[1 + lane * (R + 1) + (p & (R - 1))] = acc;
-          const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
-          __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (!FWD) out[row] = acc;
-          if (FWD && PRO != 0) pvec[row] = f.init;
+          if (SEG && sg != ns - 1) {
+            carry = acc;  // the row goes on at the next position
+          } else {
+            if (!FWD) acc = acc / f.diag;
+            s_dep[1 + lane * (R + 1) + (p & (R - 1))] = acc;
+            const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
+            __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            if (!FWD) out[row] = acc;
+            if (FWD && PRO != 0) pvec[row] = f.init;
+          }
         }
         if (lane == 0) lds_write(&s_prog, t + 1);
         seen = doneN;
@@ -308,7 +321,8 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 #pragma unroll
         for (int i = 0; i < E / 4; ++i) dma16(gc + i * 256 + lane * 4, s_code + st * E * 64 + i * 256);
         const int p = t - skew;
-        const int row = (p >= 0 && p < len) ? (FWD ? cst + p : cst - p) : 0;
+        const int ri = SEG ? p / ns : p;  // the row's operands at each of its segments
+        const int row = (p >= 0 && p < len) ? (FWD ? cst + ri : cst - ri) : 0;
         uint32_t* sa = s_aux + st * kAuxWords;
         if (FWD) {
           const double* v0 = (PRO == 0) ? src : res;
@@ -357,7 +371,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       int k = lane;
       int published = 0;
       unsigned spins = 0;
-      int jq[Q], nq[Q];
+      int jq[Q], nq[Q], sq[Q];
       bool fresh = true;
       while (ni > 0) {
         if (fresh) {  // the rows and slot-free iterations of the lane's next Q imports
@@ -365,14 +379,15 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           for (int q = 0; q < Q; ++q) {
             const int kq = k + 64 * q;
             jq[q] = kq < ni ? ca.impRow[ib + kq] : 0;
-            nq[q] = (kq < ni && kq >= RI) ? ca.impFree[ib + kq - RI] : -1;
+            nq[q] = kq < ni ? ca.impWait[ib + kq] : -1;
+            sq[q] = kq < ni ? ca.impSlot[ib + kq] : 0;
           }
           fresh = false;
         }
         const int progNow = (k < ni) ? lds_read(&s_prog) : 0;
         uint64_t lo[Q], hi[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {  // a slot is free once its previous import is no longer read
+        for (int q = 0; q < Q; ++q) {  // a slot is free once its previous import's last reader has run
           lo[q] = hi[q] = 0;
           if (k + 64 * q < ni && progNow > nq[q]) {
             lo[q] = __hip_atomic_load(gout + 2 * (size_t)jq[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -383,7 +398,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 #pragma unroll
         for (int q = 0; q < Q; ++q) {  // the ready prefix, in order
           if (d == q && k + 64 * q < ni && (unsigned)(lo[q] >> 32) == epoch && (unsigned)(hi[q] >> 32) == epoch) {
-            s_dep[impBase + ((k + 64 * q) & (RI - 1))] = join_words((uint32_t)lo[q], (uint32_t)hi[q]);
+            s_dep[impBase + sq[q]] = join_words((uint32_t)lo[q], (uint32_t)hi[q]);
             d = q + 1;
           }
         }
@@ -422,17 +437,19 @@ void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const dou
                         unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st) {
   if (ca.nbands <= 0) return;
   const dim3 grid(ca.nbands < 256 ? ca.nbands : 256), block(256);
-#define MMX_CHAIN(F, P, EE)                                                                                    \
-  hipLaunchKernelGGL((k_chain_sweep<F, P, EE>), grid, block, 0, st, ca, src, p, res, avbar, sc, gin, gout, out, \
-                     epoch, ticket, err)
-#define MMX_CHAIN_E(F, P)    \
-  do {                       \
-    if (E == 8)              \
-      MMX_CHAIN(F, P, 8);    \
-    else if (E == 16)        \
-      MMX_CHAIN(F, P, 16);   \
-    else                     \
-      MMX_CHAIN(F, P, 32);   \
+#define MMX_CHAIN(F, P, EE, SG)                                                                                    \
+  hipLaunchKernelGGL((k_chain_sweep<F, P, EE, SG>), grid, block, 0, st, ca, src, p, res, avbar, sc, gin, gout, \
+                     out, epoch, ticket, err)
+#define MMX_CHAIN_E(F, P)      \
+  do {                         \
+    if (ca.seg)                \
+      MMX_CHAIN(F, P, 32, true); \
+    else if (E == 8)           \
+      MMX_CHAIN(F, P, 8, false); \
+    else if (E == 16)          \
+      MMX_CHAIN(F, P, 16, false); \
+    else                       \
+      MMX_CHAIN(F, P, 32, false); \
   } while (0)
   if (!fwd)
     MMX_CHAIN_E(false, 0);

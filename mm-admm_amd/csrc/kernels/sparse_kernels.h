@@ -73,15 +73,18 @@ struct ChainArgs {
   const int* laneStart;
   const int* laneLen;
   const int* laneSkew;
+  const int* laneNs;   // per band * 64 + lane: segments per row (seg schedules; rows wider than 32 entries)
   const int* bandE;    // per band: entry slots in use (multiple of 4)
   const double* val;   // [slot][E][64] entry values (filled from the factor by launch_chain_fill)
   const int* code;     // [slot][E][64] LDS index of the entry's value (0: the zero cell)
   const double* dval;  // [slot][64] diagonals (backward)
   const int* impRow;
-  const int* impFree;
+  const int* impSlot;  // per import: LDS import slot
+  const int* impWait;  // per import: iterations the compute wave completes before it is delivered (-1 none)
   const int* impNeed;  // per slot: highest import index read at that iteration (-1: none)
   const int* bandOrder;  // per ticket: the band taken
   int nbands, R, RI;
+  int seg;             // the schedule splits rows into segments of 32 entries (k_chain_sweep<..., 32, true>)
   unsigned long long* prof;  // optional cycle counters (MMX_CHAIN_PROF), see chain_sweep.hip
   int profIter;              // MMX_CHAIN_PROF=2: also time the waits inside iterations (perturbs them)
 };

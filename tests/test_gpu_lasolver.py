@@ -224,10 +224,12 @@ def _sweep_run(la, ia, ja, a, b, mode, monkeypatch):
     return y, x, it, st["sweep_mode"]
 
 
-@pytest.mark.parametrize("mesh", [("rect", 2, 45), ("hexdisc", 40), ("circle", "CircleEx24"), ("rect", 2, 300)])
+@pytest.mark.parametrize("mesh", [("rect", 2, 45), ("hexdisc", 40), ("circle", "CircleEx24"), ("rect", 2, 300),
+                                  ("rect", 3, 12), ("rect", 3, 30)])
 def test_chain_sweeps_equal_level_sweeps(la, mesh, monkeypatch):
     """The chain/band-scheduled sweeps (chain_sweep.hip) and the level-scheduled ones compute every
-    row with the same operations in the same order: ILU solves and CG-STAB iterates are identical."""
+    row with the same operations in the same order: ILU solves and CG-STAB iterates are identical.
+    3D: the upper rows (up to 44 entries) run as two 32-entry segments (k_chain_sweep<..., SEG>)."""
     import mmadmm_amd as mx
     from conftest import circle_mesh
     if mesh[0] == "rect":

@@ -86,7 +86,8 @@ def _schedule_info(ia, ja, level, fwd):
 
 
 @pytest.mark.parametrize("mesh,level", [(("rect", 2, 20), 0), (("rect", 2, 57), 0), (("rect", 2, 20), 1),
-                                        (("hexdisc", 30), 0), (("circle", "CircleEx24"), 0), (("rect", 3, 6), 0)])
+                                        (("hexdisc", 30), 0), (("circle", "CircleEx24"), 0), (("rect", 3, 6), 0),
+                                        (("rect", 3, 14), 0)])
 def test_chain_schedule_is_valid(mesh, level):
     """The chain/band sweep schedule (host/chain_sched.cpp) replays correctly on the host: every row
     once with the reference's entry order, ring values live when read, imports right and ordered
@@ -105,8 +106,11 @@ def test_chain_schedule_is_valid(mesh, level):
     ia, ja = L.mesh_pattern(dim, nP, F)
     for fwd in (True, False):
         info = _schedule_info(ia, ja, level, fwd)
-        if dim == 3 and not fwd:
-            continue  # upper rows wider than 32 entries: the level-scheduled sweep is used
         assert info["ok"] == 1, info
-        # the critical path stays close to the dependency DAG's depth
-        assert info["estIters"] <= 1.3 * info["levels"] + 64, info
+        if dim == 3:
+            # 3D: the upper rows (up to 44 entries) take two 32-entry segments, and each band's lanes
+            # wait for imports from several planes; the modelled path stays within a few DAG depths
+            assert info["E"] == 32 and info["estIters"] <= 4 * info["levels"] + 64, info
+        else:
+            # the critical path stays close to the dependency DAG's depth
+            assert info["estIters"] <= 1.3 * info["levels"] + 64, info
