@@ -134,36 +134,43 @@ def spmv_bench(torch, la, mx, with_cpu):
     return out
 
 
-def be_bench(mx, with_cpu):
-    """Method 2 (Mesh::backwardsEulerStep, src/Mesh.cpp:1263-1341) on the device: SquareGrid
+def be_bench(mx, with_cpu, dim=2):
+    """Method 2 (Mesh::backwardsEulerStep, src/Mesh.cpp:1263-1341) on the device.  dim 2: SquareGrid
     n = 707 (1,001,113 nodes, the SpMV matrix's mesh), MEx3, dt 0.025, tau 0.5, rho 100 (the
-    Monitor220 family).  First step (pattern, symbolic ILU, sweep schedules, FD Jacobian) and the
-    steady steps after it are timed separately."""
-    mesh = mx.MeshData.rect(2, 707)
-    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 3), rho=100.0, tau=0.5)
+    Monitor220 family).  dim 3: the C4 cube (3D SquareGrid n = 63, 512,191 nodes, a 1,536,573-row
+    Jacobian whose upper rows take the segmented chain sweeps), the C4 monitor (MonType 6), dt 0.025,
+    tau 0.5.  First step (pattern, symbolic ILU, sweep schedules, FD Jacobian) and the steady steps
+    after it are timed separately; the CPU leg runs the oracle on the same mesh."""
+    if dim == 2:
+        mesh = mx.MeshData.rect(2, 707)
+        mon, rho, steps, csteps = 3, 100.0, 3, 2
+        desc = "SquareGrid n=707 (%d nodes, %d triangles), MEx3, dt 0.025 tau 0.5 rho 100" % (mesh.nP, mesh.nF)
+    else:
+        mesh = mx.MeshData.rect(3, 63)
+        mon, rho, steps, csteps = 6, 2000.0, 2, 1
+        desc = ("C4: 3D SquareGrid n=63 (%d nodes, %d tetrahedra), MonType 6 (anisotropic shell), dt 0.025 "
+                "tau 0.5" % (mesh.nP, mesh.nF))
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, mon), rho=rho, tau=0.5)
     E = mx.Engine(M, 0.025)
     t0 = time.perf_counter()
     E.backwards_euler_step(0.025)
     first = time.perf_counter() - t0
     E.reset_stats()
-    steps = 3
     t0 = time.perf_counter()
     for _ in range(steps):
         E.backwards_euler_step(0.025)
     dt = (time.perf_counter() - t0) / steps
     st = E.stats()
-    out = {"workload": "SquareGrid n=707 (%d nodes, %d triangles), MEx3, dt 0.025 tau 0.5 rho 100" % (mesh.nP, mesh.nF),
-           "first_step_s": round(first, 3), "step_ms": round(dt * 1e3, 2),
+    out = {"workload": desc, "first_step_s": round(first, 3), "step_ms": round(dt * 1e3, 2), "steps": steps,
            "newton_per_step": st["newton_iters"] / steps, "cg_iters_per_step": st["cg_iters"] / steps,
            "solve_ms_per_step": round(st["t_solve_ms"] / steps, 2)}
     E.close()
     def _cpu():  # the oracle's restatement, one core, on the same mesh and parameters
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_py
-        om = oracle_py.Mesh(2, mesh.Xp, mesh.F, mesh.mask)
-        O = oracle_py.Integrator(om, 3, 0.025, 0.5, 100.0, nthreads=1)
+        om = oracle_py.Mesh(dim, mesh.Xp, mesh.F, mesh.mask)
+        O = oracle_py.Integrator(om, mon, 0.025, 0.5, rho, nthreads=1)
         O.backwards_euler_step(0.025)
-        csteps = 2
         t0 = time.perf_counter()
         for _ in range(csteps):
             O.backwards_euler_step(0.025)
@@ -171,8 +178,7 @@ def be_bench(mx, with_cpu):
         out["cpu_baseline"] = {"step_ms": round(cdt * 1e3, 1), "nodes": int(om.nP), "cores": 1, "kind": "port",
                                "gpu_speedup": round(cdt * 1e3 / out["step_ms"], 1),
                                "sample": "oracle/oracle.cpp backwards_euler_step (FD Jacobian + LASolver "
-                                         "restatement) on the same SquareGrid n=707 mesh, %d steady steps after "
-                                         "the first" % csteps}
+                                         "restatement) on the same mesh, %d steady step(s) after the first" % csteps}
     if with_cpu:  # CPU baselines run after every GPU measurement (main)
         DEFERRED.append(_cpu)
     return out
@@ -615,6 +621,12 @@ def main():
         result["c4_3d"] = c4_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
         log("3D time-varying monitor")
         result["c4_time_varying"] = tv_bench(mx, 63, args.admm_iter)
+        if not args.no_be:
+            log("3D backward Euler (C4)")
+            try:
+                result["backward_euler_c4"] = be_bench(mx, not args.no_cpu_baseline, dim=3)
+            except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
+                result["backward_euler_c4"] = {"error": str(e)}
     if args.c5 and world == 1 and rank == 0:
         log("3D C5 time-varying (5.09 M nodes)")
         result["c5_time_varying"] = tv_bench(mx, 136, args.admm_iter, steps=2)

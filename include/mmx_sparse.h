@@ -71,6 +71,7 @@ typedef struct mmx_sparse_stats {
   double last_rms, rmsi;
   int sweep_mode;     /* triangular sweeps: 0 level-scheduled, 1 chain/band-scheduled */
   int sweep_e;        /* chain sweeps: entry slots per row (8, 16, 32) */
+  int factor_mode;    /* numeric factor: 0 level-scheduled, 1 chain/band-scheduled */
 } mmx_sparse_stats;
 
 void mmx_param_iter_default(mmx_param_iter* p);

@@ -21,7 +21,7 @@ int pow2_at_least(int v) {
 }  // namespace
 
 ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std::vector<int>& jaf,
-                                   const std::vector<int>& dg, bool fwd) {
+                                   const std::vector<int>& dg, bool fwd, int forceG) {
   ChainSchedule S;
   S.fwd = fwd;
   auto rb = [&](int i) { return fwd ? iaf[i] : dg[i] + 1; };
@@ -30,32 +30,48 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   for (int i = 0; i < n; ++i) emax = std::max(emax, re(i) - rb(i));
   // rows wider than 32 entries (3D) are split into segments of E = 32 entries computed at
   // consecutive positions of their lane (the partial sum carried in a register, so the order of
-  // the subtractions is unchanged); every row of a chain takes the chain's segment count ns
+  // the subtractions is unchanged); every row of a chain takes the chain's segment count ns.
+  // Narrower rows (2D) are computed two per position (G = 2): the chain's next row takes the
+  // first one's value straight from the register (MMX_CHAIN_PAIR=0: one row per position).
   S.E = emax <= 8 ? 8 : emax <= 16 ? 16 : 32;
   S.seg = emax > 32;
   if (emax > kChainSegMax * 32) {
     S.why = "a row has more than " + std::to_string(kChainSegMax * 32) + " entries in the triangle";
     return S;
   }
-  auto nsRow = [&](int i) { return std::max(1, (re(i) - rb(i) + S.E - 1) / S.E); };
+  {
+    const char* pe = getenv("MMX_CHAIN_PAIR");
+    S.G = (!S.seg && S.E <= 16 && !(pe && atoi(pe) == 0)) ? 2 : 1;
+    if (forceG == 1 || (forceG == 2 && !S.seg && S.E <= 16)) S.G = forceG;
+  }
+  const int G = S.G, E = S.E, EE = E * G;
+  auto nsRow = [&](int i) { return S.seg ? std::max(1, (re(i) - rb(i) + E - 1) / E) : 1; };
   // chains in processing order (forward: ascending rows; backward: descending); a chain also ends
   // where the segment count changes, so no row pays for a wider neighbour's segments
-  std::vector<int> chainOf(n), posOf(n), cStart, cLen, cNs;
+  std::vector<int> chainOf(n), rowIdx(n), cStart, cRows, cNs;
   for (int t = 0; t < n; ++t) {
     const int i = fwd ? t : n - 1 - t;
     const int b = rb(i), e = re(i), ns = nsRow(i);
-    const bool cont = t > 0 && cLen.back() < kChainLenCap && cNs.back() == ns &&
+    const bool cont = t > 0 && cRows.back() < kChainLenCap && cNs.back() == ns &&
                       (fwd ? (e > b && jaf[e - 1] == i - 1) : (e > b && jaf[b] == i + 1));
     if (!cont) {
       cStart.push_back(i);
-      cLen.push_back(0);
+      cRows.push_back(0);
       cNs.push_back(ns);
     }
     chainOf[i] = (int)cStart.size() - 1;
-    posOf[i] = cLen.back() + ns - 1;  // the row's value is ready after its last segment
-    cLen.back() += ns;
+    rowIdx[i] = cRows.back()++;
   }
   const int C = (int)cStart.size();
+  // positions: a row's value is final at posOf (its last segment / its pair's position); ringOf
+  // is the row's sequence number in its lane's LDS ring
+  std::vector<int> cLen(C), posOf(n), ringOf(n);
+  for (int c = 0; c < C; ++c) cLen[c] = (G == 2) ? (cRows[c] + 1) / 2 : cRows[c] * cNs[c];
+  for (int i = 0; i < n; ++i) {
+    const int c = chainOf[i];
+    posOf[i] = (G == 2) ? rowIdx[i] / 2 : rowIdx[i] * cNs[c] + cNs[c] - 1;
+    ringOf[i] = (G == 2) ? rowIdx[i] : posOf[i];
+  }
   S.nchains = C;
   S.nbands = (C + kChainLanes - 1) / kChainLanes;
   const int L = kChainLanes;
@@ -67,8 +83,23 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   S.bandT.assign(S.nbands, 0);
   S.bandImp.assign(S.nbands, 0);
   S.bandNImp.assign(S.nbands, 0);
-  // row and segment at position p of chain c
-  auto rowAt = [&](int c, int p) { return fwd ? cStart[c] + p / cNs[c] : cStart[c] - p / cNs[c]; };
+  // part g of position p of chain c: its row (-1: none) and segment q, entries [kb, ke)
+  auto part = [&](int c, int p, int g, int& q, int& kb, int& ke) {
+    int ri;
+    if (G == 2) {
+      ri = 2 * p + g;
+      q = 0;
+      if (ri >= cRows[c]) return -1;
+    } else {
+      if (g > 0) return -1;
+      ri = p / cNs[c];
+      q = p % cNs[c];
+    }
+    const int i = fwd ? cStart[c] + ri : cStart[c] - ri;
+    kb = rb(i) + q * E;
+    ke = std::min(re(i), kb + E);
+    return i;
+  };
 
   // pass 1: skews and band lengths, with a model of the critical path: band b starts at iteration
   // offset[b] (not before band b - 1), a row is published at offset + position + skew + 1 and an
@@ -88,18 +119,19 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
       for (int l = 0; l < nl; ++l) {
         const int c = c0 + l;
         long long sk = 0;
-        for (int p = 0; p < cLen[c]; ++p) {
-          const int i = rowAt(c, p), q = p % cNs[c];
-          const int kb = rb(i) + q * S.E, ke = std::min(re(i), kb + S.E);
-          for (int k = kb; k < ke; ++k) {
-            const int j = jaf[k], cj = chainOf[j];
-            if (cj >= c0 && cj < c) {
-              sk = std::max<long long>(sk, S.laneSkew[(size_t)b * L + (cj - c0)] + posOf[j] - p + 1);
-            } else if (align && cj < c0 && doneAt[j] >= 0) {
-              sk = std::max<long long>(sk, doneAt[j] + kImportLatency - off0 - p);
+        for (int p = 0; p < cLen[c]; ++p)
+          for (int g = 0; g < G; ++g) {
+            int q, kb, ke;
+            if (part(c, p, g, q, kb, ke) < 0) continue;
+            for (int k = kb; k < ke; ++k) {
+              const int j = jaf[k], cj = chainOf[j];
+              if (cj >= c0 && cj < c) {
+                sk = std::max<long long>(sk, S.laneSkew[(size_t)b * L + (cj - c0)] + posOf[j] - p + 1);
+              } else if (align && cj < c0 && doneAt[j] >= 0) {
+                sk = std::max<long long>(sk, doneAt[j] + kImportLatency - off0 - p);
+              }
             }
           }
-        }
         if (sk > kChainLenCap) sk = kChainLenCap;
         S.laneSkew[(size_t)b * L + l] = (int)sk;
         minSk = std::min(minSk, (int)sk);
@@ -112,19 +144,23 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
         const int c = c0 + l, sk = S.laneSkew[(size_t)b * L + l];
         T = std::max(T, sk + cLen[c]);
         if (!align)  // the band waits for its late imports
-          for (int p = 0; p < cLen[c]; ++p) {
-            const int i = rowAt(c, p), q = p % cNs[c];
-            const int kb = rb(i) + q * S.E, ke = std::min(re(i), kb + S.E);
-            for (int k = kb; k < ke; ++k) {
-              const int j = jaf[k];
-              if (chainOf[j] < c0 && doneAt[j] >= 0) off = std::max(off, doneAt[j] + kImportLatency - (p + sk));
+          for (int p = 0; p < cLen[c]; ++p)
+            for (int g = 0; g < G; ++g) {
+              int q, kb, ke;
+              if (part(c, p, g, q, kb, ke) < 0) continue;
+              for (int k = kb; k < ke; ++k) {
+                const int j = jaf[k];
+                if (chainOf[j] < c0 && doneAt[j] >= 0) off = std::max(off, doneAt[j] + kImportLatency - (p + sk));
+              }
             }
-          }
       }
       offset[b] = off;
       for (int l = 0; l < nl; ++l) {
         const int c = c0 + l, sk = S.laneSkew[(size_t)b * L + l];
-        for (int p = cNs[c] - 1; p < cLen[c]; p += cNs[c]) doneAt[rowAt(c, p)] = off + p + sk + 1;
+        for (int r = 0; r < cRows[c]; ++r) {
+          const int i = fwd ? cStart[c] + r : cStart[c] - r;
+          doneAt[i] = off + posOf[i] + sk + 1;
+        }
       }
       S.bandT[b] = T;
       est = std::max(est, off + T);
@@ -145,49 +181,51 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
     }
     S.estIters = est;
   }
-  // lane arrays, slots, ring distances
+  // lane arrays, slots, ring distances (a ring slot of a lane is written again R / G positions
+  // after it is written)
   int maxDist = 1;
   for (int b = 0; b < S.nbands; ++b) {
     const int c0 = b * L, nl = std::min(L, C - c0);
     for (int l = 0; l < nl; ++l) {
       const int c = c0 + l, sk = S.laneSkew[(size_t)b * L + l];
       S.laneStart[(size_t)b * L + l] = cStart[c];
-      S.laneLen[(size_t)b * L + l] = cLen[c];
+      S.laneLen[(size_t)b * L + l] = (G == 2) ? cRows[c] : cLen[c];  // pairs: rows; else positions
       S.laneNs[(size_t)b * L + l] = cNs[c];
       S.maxSkew = std::max(S.maxSkew, sk);
       S.maxLen = std::max(S.maxLen, cLen[c]);
     }
     for (int l = 0; l < nl; ++l) {
       const int c = c0 + l, skl = S.laneSkew[(size_t)b * L + l];
-      for (int p = 0; p < cLen[c]; ++p) {
-        const int i = rowAt(c, p), q = p % cNs[c];
-        const int kb = rb(i) + q * S.E, ke = std::min(re(i), kb + S.E);
-        for (int k = kb; k < ke; ++k) {
-          const int cj = chainOf[jaf[k]];
-          if (cj < c0 || cj > c) continue;
-          const int d = (p + skl) - (posOf[jaf[k]] + S.laneSkew[(size_t)b * L + (cj - c0)]);
-          if (d <= kChainRingMax) maxDist = std::max(maxDist, d);
+      for (int p = 0; p < cLen[c]; ++p)
+        for (int g = 0; g < G; ++g) {
+          int q, kb, ke;
+          if (part(c, p, g, q, kb, ke) < 0) continue;
+          for (int k = kb; k < ke; ++k) {
+            const int j = jaf[k], cj = chainOf[j];
+            if (cj < c0 || cj > c) continue;
+            const int d = (p + skl) - (posOf[j] + S.laneSkew[(size_t)b * L + (cj - c0)]);
+            if (d >= 1 && d * G <= kChainRingMax) maxDist = std::max(maxDist, d * G);
+          }
         }
-      }
     }
     S.bandSlot[b] = (int)S.slots;
     S.slots += S.bandT[b];
     S.maxT = std::max(S.maxT, S.bandT[b]);
   }
-  if (S.slots * L * S.E > (long long)INT32_MAX) {
+  if (S.slots * L * EE > (long long)INT32_MAX) {
     S.why = "schedule too large";
     return S;
   }
-  S.R = std::max(2, pow2_at_least(maxDist));
+  S.R = std::max(2 * G, pow2_at_least(maxDist));
   const int R = S.R;
 
   // pass 2: codes, value sources, imports
-  const size_t ne = (size_t)S.slots * L * S.E;
+  const size_t ne = (size_t)S.slots * L * EE;
   S.code.assign(ne, kChainPad);
   S.impNeed.assign((size_t)S.slots, -1);
   S.bandE.assign(S.nbands, 4);
   S.src.assign(ne, -1);
-  if (!fwd) S.dsrc.assign((size_t)S.slots * L, -1);
+  if (!fwd) S.dsrc.assign((size_t)S.slots * G * L, -1);
   std::vector<int> impOf(n, -1), first, last, rows;
   std::vector<std::vector<int>> srcBands(S.nbands);  // bands each band imports from
   // the importer runs at most RI imports ahead of the compute wave: it takes the whole ring (a
@@ -205,40 +243,46 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
     std::vector<Use> impUses;
     for (int l = 0; l < nl; ++l) {
       const int c = c0 + l, skl = S.laneSkew[(size_t)b * L + l];
-      for (int p = 0; p < cLen[c]; ++p) {
-        const int i = rowAt(c, p), t = p + skl, q = p % cNs[c];
-        const size_t base = ((size_t)(S.bandSlot[b] + t) * S.E) * L + l;  // [slot][e][lane]
-        if (!fwd && q == cNs[c] - 1) S.dsrc[(size_t)(S.bandSlot[b] + t) * L + l] = dg[i];
-        const int kb = rb(i) + q * S.E, ke = std::min(re(i), kb + S.E);
-        int e = 0;
-        S.bandE[b] = std::max(S.bandE[b], (std::max(ke - kb, 0) + 3) / 4 * 4);
-        for (int k = kb; k < ke; ++k, ++e) {
-          const int j = jaf[k], cj = chainOf[j];
-          const size_t x = base + (size_t)e * L;
-          S.src[x] = k;
-          bool ring = false;
-          if (cj >= c0 && cj <= c) {
-            const int lj = cj - c0, qj = posOf[j];
-            const int d = t - (qj + S.laneSkew[(size_t)b * L + lj]);
-            if (d <= R) {
-              S.code[x] = lj * (R + 1) + (qj & (R - 1));
+      for (int p = 0; p < cLen[c]; ++p)
+        for (int g = 0; g < G; ++g) {
+          int q, kb, ke;
+          const int i = part(c, p, g, q, kb, ke);
+          if (i < 0) continue;
+          const int t = p + skl;
+          const size_t base = ((size_t)(S.bandSlot[b] + t) * EE + (size_t)g * E) * L + l;  // [slot][g][e][lane]
+          if (!fwd && q == cNs[c] - 1) S.dsrc[((size_t)(S.bandSlot[b] + t) * G + g) * L + l] = dg[i];
+          int e = 0;
+          S.bandE[b] = std::max(S.bandE[b], (std::max(ke - kb, 0) + 3) / 4 * 4);
+          for (int k = kb; k < ke; ++k, ++e) {
+            const int j = jaf[k], cj = chainOf[j];
+            const size_t x = base + (size_t)e * L;
+            S.src[x] = k;
+            bool ring = false;
+            if (cj == c && posOf[j] == p) {  // the pair's first row, taken from the register
+              S.code[x] = kChainFwd;
               ring = true;
+            } else if (cj >= c0 && cj <= c) {
+              const int lj = cj - c0;
+              const int d = t - (posOf[j] + S.laneSkew[(size_t)b * L + lj]);
+              if (d * G <= R) {
+                S.code[x] = lj * (R + 1) + (ringOf[j] & (R - 1));
+                ring = true;
+              }
             }
-          }
-          if (!ring) {
-            int& id = impOf[j];
-            if (id < 0) {
-              id = (int)rows.size();
-              rows.push_back(j);
-              first.push_back(t);
-              last.push_back(t);
+            if (!ring) {
+              int& id = impOf[j];
+              if (id < 0) {
+                id = (int)rows.size();
+                rows.push_back(j);
+                first.push_back(t);
+                last.push_back(t);
+              }
+              first[id] = std::min(first[id], t);
+              last[id] = std::max(last[id], t);
+              impUses.push_back({x, j});
             }
-            first[id] = std::min(first[id], t);
-            last[id] = std::max(last[id], t);
-            impUses.push_back({x, j});
           }
         }
-      }
     }
     // imports in order of first use
     std::vector<int> ord(rows.size());
@@ -284,7 +328,7 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
     for (const Use& u : impUses) {
       const int k = rank[impOf[u.row]];
       S.code[u.slot] = -(slotOf[k] + 1);
-      const size_t it = u.slot / ((size_t)S.E * L);  // slot (iteration) of the use
+      const size_t it = u.slot / ((size_t)EE * L);  // slot (iteration) of the use
       S.impNeed[it] = std::max(S.impNeed[it], k);
     }
     S.bandImp[b] = (int)S.impRow.size();
@@ -333,9 +377,11 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
       return S;
     }
   }
-  // codes -> LDS indices: 0 zero cell, 1 + ring index, 1 + 64 (R + 1) + import slot
+  // codes -> LDS indices: 0 zero cell, 1 + ring index, 1 + 64 (R + 1) + import slot; the pair's
+  // forwarded entry: the cell after the import slots (never read: the kernel takes the register)
   const int impBase = 1 + L * (R + 1);
-  for (int& c : S.code) c = (c == kChainPad) ? 0 : (c >= 0 ? 1 + c : impBase + (-c - 1));
+  for (int& c : S.code)
+    c = (c == kChainPad) ? 0 : (c == kChainFwd) ? impBase + RI : (c >= 0 ? 1 + c : impBase + (-c - 1));
   S.ok = true;
   return S;
 }
@@ -343,26 +389,33 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
 std::string validate_chain_schedule(const ChainSchedule& S, int n, const std::vector<int>& iaf,
                                     const std::vector<int>& jaf, const std::vector<int>& dg) {
   if (!S.ok) return "schedule not built: " + S.why;
-  const int L = kChainLanes, E = S.E, R = S.R;
+  const int L = kChainLanes, E = S.E, R = S.R, G = S.G, EE = E * G;
   const bool fwd = S.fwd;
-  // where every row is computed: band, lane, position of its last segment, iteration
-  std::vector<int> bandOf(n, -1), laneOf(n, -1), posOf(n, -1), iterOf(n, -1), nsOf(n, 1);
+  if (G != 1 && G != 2) return "bad rows per position";
+  if (G == 2 && S.seg) return "pairs of segmented rows";
+  // where every row is computed: band, lane, position of its final value, ring sequence number,
+  // part (pair half), segments
+  std::vector<int> bandOf(n, -1), laneOf(n, -1), posOf(n, -1), ringOf(n, -1), partOf(n, 0), iterOf(n, -1),
+      nsOf(n, 1);
   if (S.laneNs.size() != S.laneLen.size()) return "segment counts missing";
   for (int b = 0; b < S.nbands; ++b)
     for (int l = 0; l < L; ++l) {
       const size_t g = (size_t)b * L + l;
       const int ns = S.laneNs[g];
       if (ns < 1 || ns > kChainSegMax || (ns > 1 && !S.seg)) return "bad segment count";
-      if (S.laneLen[g] % ns) return "lane length not a whole number of rows";
-      for (int p = ns - 1; p < S.laneLen[g]; p += ns) {
-        const int i = fwd ? S.laneStart[g] + p / ns : S.laneStart[g] - p / ns;
+      if (G == 1 && S.laneLen[g] % ns) return "lane length not a whole number of rows";
+      const int nrows = (G == 2) ? S.laneLen[g] : S.laneLen[g] / ns;
+      for (int r = 0; r < nrows; ++r) {
+        const int i = fwd ? S.laneStart[g] + r : S.laneStart[g] - r;
         if (i < 0 || i >= n) return "row out of range";
         if (bandOf[i] >= 0) return "row " + std::to_string(i) + " scheduled twice";
         bandOf[i] = b;
         laneOf[i] = l;
-        posOf[i] = p;
+        posOf[i] = (G == 2) ? r / 2 : r * ns + ns - 1;
+        ringOf[i] = (G == 2) ? r : posOf[i];
+        partOf[i] = (G == 2) ? r % 2 : 0;
         nsOf[i] = ns;
-        iterOf[i] = p + S.laneSkew[g];
+        iterOf[i] = posOf[i] + S.laneSkew[g];
         if (iterOf[i] >= S.bandT[b]) return "row beyond its band's iterations";
       }
     }
@@ -401,15 +454,17 @@ std::string validate_chain_schedule(const ChainSchedule& S, int n, const std::ve
       lastInSlot[S.impSlot[g]] = q;
     }
   }
+  const int impBase = 1 + L * (R + 1), fwdCell = impBase + S.RI;
   for (int i = 0; i < n; ++i) {
-    const int b = bandOf[i], l = laneOf[i], ns = nsOf[i];
+    const int b = bandOf[i], l = laneOf[i], ns = nsOf[i], gp = partOf[i];
     const int kb0 = fwd ? iaf[i] : dg[i] + 1, ke0 = fwd ? dg[i] : iaf[i + 1];
     if (ke0 - kb0 > E * ns) return "row wider than its segments";
     for (int sg = 0; sg < ns; ++sg) {
       const int t = iterOf[i] - (ns - 1) + sg;  // segment sg of the row
-      const size_t base = ((size_t)(S.bandSlot[b] + t) * E) * L + l;
+      const size_t base = ((size_t)(S.bandSlot[b] + t) * EE + (size_t)gp * E) * L + l;
       const int kb = kb0 + sg * E, ke = std::min(ke0, kb + E);
-      if (!fwd && S.dsrc[(size_t)(S.bandSlot[b] + t) * L + l] != (sg == ns - 1 ? dg[i] : -1)) return "diagonal source";
+      if (!fwd && S.dsrc[((size_t)(S.bandSlot[b] + t) * G + gp) * L + l] != (sg == ns - 1 ? dg[i] : -1))
+        return "diagonal source";
       for (int e = 0; e < E; ++e) {
         const size_t x = base + (size_t)e * L;
         const int k = kb + e;
@@ -420,15 +475,21 @@ std::string validate_chain_schedule(const ChainSchedule& S, int n, const std::ve
         if (e >= S.bandE[b]) return "entry beyond the band's entry count";
         if (S.src[x] != k) return "entry order differs from the reference";
         const int j = jaf[k], c = S.code[x];
-        const int impBase = 1 + L * (R + 1);
         if (c <= 0) return "missing entry";
-        if (c < impBase) {
+        if (c == fwdCell) {  // the pair's first row, from the register
+          if (gp != 1 || bandOf[j] != b || laneOf[j] != l || posOf[j] != posOf[i] || partOf[j] != 0)
+            return "forwarded entry is not the pair's first row";
+        } else if (c < impBase) {
           const int r = c - 1, lp = r / (R + 1), slot = r % (R + 1);
-          if (bandOf[j] != b || laneOf[j] != lp || (posOf[j] & (R - 1)) != slot) return "ring slot of another row";
+          if (bandOf[j] != b || laneOf[j] != lp || (ringOf[j] & (R - 1)) != slot) return "ring slot of another row";
           if (iterOf[j] >= t) return "ring value read before it is written";
-          const size_t gp = (size_t)b * L + lp;
-          const int over = posOf[j] + R;  // next write to the same slot
-          if (over < S.laneLen[gp] && over + S.laneSkew[gp] < t) return "ring value overwritten before it is read";
+          // the slot is written again by the lane's row with ring number ringOf[j] + R, at its
+          // position; a read in that same iteration comes first
+          const size_t gl = (size_t)b * L + lp;
+          const int over = ringOf[j] + R;
+          const int overPos = (G == 2) ? over / 2 : over;
+          const int lenRows = (G == 2) ? S.laneLen[gl] : S.laneLen[gl];
+          if (over < lenRows && overPos + S.laneSkew[gl] < t) return "ring value overwritten before it is read";
         } else {
           // the import: the one of this band whose slot matches and whose row is j
           const int slot = c - impBase;
@@ -449,6 +510,302 @@ std::string validate_chain_schedule(const ChainSchedule& S, int n, const std::ve
         }
       }
     }
+  }
+  return "";
+}
+
+FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const std::vector<int>& jaf,
+                                     const std::vector<int>& dg) {
+  FactorSchedule F;
+  for (int i = 0; i < n; ++i) {
+    const int W = iaf[i + 1] - iaf[i], nl = dg[i] - iaf[i];
+    if (W > kFacWF || nl > kFacNL || W - nl > kFacWU) {
+      F.why = "row " + std::to_string(i) + " wider than the factor's row layout";
+      return F;
+    }
+  }
+  F.geo = build_chain_schedule(n, iaf, jaf, dg, true, 1);
+  ChainSchedule& S = F.geo;
+  if (!S.ok) {
+    F.why = "forward chain schedule: " + S.why;
+    return F;
+  }
+  if (S.seg || S.G != 1) {
+    F.why = "segmented schedule";
+    return F;
+  }
+  S.code.clear();
+  S.code.shrink_to_fit();
+  S.src.clear();
+  S.src.shrink_to_fit();
+  const int L = kChainLanes;
+  const char* fr = getenv("MMX_FAC_R");
+  const int R = std::min(std::min(S.R, kFacRMax), fr ? atoi(fr) : kFacRMax);  // ring slots per lane (rows)
+  F.R = R;
+  F.slots = S.slots;
+  // where every row is: band, lane, position, iteration
+  std::vector<int> bandOf(n, -1), laneOf(n, -1), posOf(n, -1);
+  for (int b = 0; b < S.nbands; ++b)
+    for (int l = 0; l < L; ++l) {
+      const size_t g = (size_t)b * L + l;
+      for (int p = 0; p < S.laneLen[g]; ++p) {
+        const int i = S.laneStart[g] + p;
+        bandOf[i] = b;
+        laneOf[i] = l;
+        posOf[i] = p;
+      }
+    }
+  const size_t nslot = (size_t)S.slots;
+  F.code.assign(nslot * kFacNSC * L, 0);
+  F.vsrc.assign(nslot * kFacWF * L, -1);
+  F.meta.assign(nslot * L, 0);
+  F.rowStart.assign(nslot * L, 0);
+  F.impNeed.assign(nslot, -1);
+  F.bandImp.assign(S.nbands, 0);
+  F.bandNImp.assign(S.nbands, 0);
+  const char* fri = getenv("MMX_FAC_RI");
+  const int RI = fri ? atoi(fri) : kFacImpRows;
+  F.RI = RI;
+  const int impBase = 1 + L * (R + 1) * kFacWU;
+  std::unordered_map<int, int> impOf;  // imported row -> import id (this band)
+  std::vector<int> rows, first, last;  // per import id: row, first and last use
+  struct Use {
+    size_t cell;
+    int id, u;  // import, offset in the row's diagonal + upper part
+  };
+  for (int b = 0; b < S.nbands; ++b) {
+    impOf.clear();
+    rows.clear();
+    first.clear();
+    last.clear();
+    std::vector<Use> uses;
+    for (int l = 0; l < L; ++l) {
+      const size_t g = (size_t)b * L + l;
+      const int skl = S.laneSkew[g];
+      for (int p = 0; p < S.laneLen[g]; ++p) {
+        const int i = S.laneStart[g] + p, t = p + skl;
+        const size_t slot = (size_t)S.bandSlot[b] + t;
+        const int kb = iaf[i], W = iaf[i + 1] - kb, nl = dg[i] - kb;
+        F.meta[slot * L + l] = W | (nl << 8) | (1 << 16);
+        F.rowStart[slot * L + l] = kb;
+        for (int e = 0; e < W; ++e) F.vsrc[fac_vidx(slot, e, l)] = kb + e;
+        // the LDS index of U(j, c) for the row at iteration t
+        auto value = [&](int j, int c, size_t cell) {
+          const int* ub = jaf.data() + dg[j];
+          const int* ue = jaf.data() + iaf[j + 1];
+          const int* f = std::lower_bound(ub, ue, c);
+          const int pos = (int)(f - jaf.data());  // the caller checked that the entry exists
+          if (bandOf[j] == b && laneOf[j] <= l) {
+            const size_t gj = (size_t)b * L + laneOf[j];
+            const int d = t - (posOf[j] + S.laneSkew[gj]);
+            if (d >= 1 && d <= R) {
+              F.code[cell] = (uint16_t)(1 + (laneOf[j] * (R + 1) + (posOf[j] & (R - 1))) * kFacWU + (pos - dg[j]));
+              return;
+            }
+          }
+          auto it = impOf.find(j);
+          int id;
+          if (it == impOf.end()) {
+            id = (int)rows.size();
+            impOf.emplace(j, id);
+            rows.push_back(j);
+            first.push_back(t);
+            last.push_back(t);
+          } else {
+            id = it->second;
+          }
+          first[id] = std::min(first[id], t);
+          last[id] = std::max(last[id], t);
+          uses.push_back({cell, id, pos - dg[j]});
+        };
+        for (int q = 0; q < nl; ++q) {
+          const int j = jaf[kb + q];
+          value(j, j, fac_cidx(slot, kFacNUpd + q, l));  // the pivot U(j, j)
+          // the targets of pivot q: entries e > q whose column lies in row j's upper part
+          const int* ub = jaf.data() + dg[j] + 1;
+          const int* ue = jaf.data() + iaf[j + 1];
+          for (int e = q + 1; e < W; ++e) {
+            const int c = jaf[kb + e];
+            if (c <= j) continue;
+            const int* f = std::lower_bound(ub, ue, c);
+            if (f != ue && *f == c) value(j, c, fac_cidx(slot, fac_slot(e, q), l));
+          }
+        }
+      }
+    }
+    // imports in order of first use, slots by interval colouring (as build_chain_schedule)
+    std::vector<int> ord(rows.size());
+    for (size_t q = 0; q < ord.size(); ++q) ord[q] = (int)q;
+    std::sort(ord.begin(), ord.end(), [&](int a, int c) { return first[a] != first[c] ? first[a] < first[c] : rows[a] < rows[c]; });
+    std::vector<int> rank(rows.size()), slotOf(ord.size()), waitOf(ord.size()), slotLast;
+    for (size_t q = 0; q < ord.size(); ++q) rank[ord[q]] = (int)q;
+    {
+      typedef std::pair<int, int> P;
+      std::priority_queue<P, std::vector<P>, std::greater<P>> busy;
+      std::priority_queue<int, std::vector<int>, std::greater<int>> freeSlots;
+      for (size_t q = 0; q < ord.size(); ++q) {
+        const int f = first[ord[q]];
+        while (!busy.empty() && busy.top().first < f) {
+          freeSlots.push(busy.top().second);
+          busy.pop();
+        }
+        int sl;
+        if (!freeSlots.empty()) {
+          sl = freeSlots.top();
+          freeSlots.pop();
+        } else {
+          sl = (int)slotLast.size();
+          if (sl == RI) {
+            F.why = "import slots too few for band " + std::to_string(b);
+            return F;
+          }
+          slotLast.push_back(-1);
+        }
+        slotOf[q] = sl;
+        waitOf[q] = slotLast[sl];
+        slotLast[sl] = last[ord[q]];
+        busy.push({last[ord[q]], sl});
+      }
+    }
+    F.maxImpSlots = std::max(F.maxImpSlots, (int)slotLast.size());
+    for (const Use& u : uses) {
+      const int k = rank[u.id];
+      F.code[u.cell] = (uint16_t)(impBase + slotOf[k] * kFacWU + u.u);
+      const size_t it = u.cell / ((size_t)kFacNSC * L);
+      F.impNeed[it] = std::max(F.impNeed[it], k);
+    }
+    F.bandImp[b] = (int)F.impRow.size();
+    F.bandNImp[b] = (int)ord.size();
+    for (size_t q = 0; q < ord.size(); ++q) {
+      F.impRow.push_back(rows[ord[q]]);
+      F.impFree.push_back(last[ord[q]]);
+      F.impSlot.push_back(slotOf[q]);
+      F.impWait.push_back(waitOf[q]);
+    }
+  }
+  if (impBase + RI * kFacWU >= 65536) {
+    F.why = "LDS indices exceed 16 bits";
+    return F;
+  }
+  // a band imports only from bands with earlier tickets (the forward sweep's order already puts
+  // every band after the bands its rows depend on, which are the bands its imports come from)
+  {
+    std::vector<int> ticketOf(S.nbands);
+    for (int q = 0; q < S.nbands; ++q) ticketOf[S.bandOrder[q]] = q;
+    for (int b = 0; b < S.nbands; ++b)
+      for (int q = 0; q < F.bandNImp[b]; ++q) {
+        const int j = F.impRow[(size_t)F.bandImp[b] + q];
+        if (bandOf[j] != b && ticketOf[bandOf[j]] > ticketOf[b]) {
+          F.why = "factor band imports from a later ticket";
+          return F;
+        }
+      }
+  }
+  F.nImports = (long long)F.impRow.size();
+  F.ok = true;
+  return F;
+}
+
+std::string validate_factor_schedule(const FactorSchedule& F, int n, const std::vector<int>& iaf,
+                                     const std::vector<int>& jaf, const std::vector<int>& dg) {
+  if (!F.ok) return "factor schedule not built: " + F.why;
+  const ChainSchedule& S = F.geo;
+  const int L = kChainLanes, R = F.R;
+  const int impBase = 1 + L * (R + 1) * kFacWU;
+  std::vector<int> bandOf(n, -1), laneOf(n, -1), posOf(n, -1), iterOf(n, -1);
+  for (int b = 0; b < S.nbands; ++b)
+    for (int l = 0; l < L; ++l) {
+      const size_t g = (size_t)b * L + l;
+      for (int p = 0; p < S.laneLen[g]; ++p) {
+        const int i = S.laneStart[g] + p;
+        if (i < 0 || i >= n || bandOf[i] >= 0) return "row scheduled twice or out of range";
+        bandOf[i] = b;
+        laneOf[i] = l;
+        posOf[i] = p;
+        iterOf[i] = p + S.laneSkew[g];
+      }
+    }
+  for (int i = 0; i < n; ++i)
+    if (bandOf[i] < 0) return "row never scheduled";
+  std::vector<std::unordered_map<int, int>> impOfRow(S.nbands);
+  std::vector<int> nextInSlot(F.impRow.size(), -1);
+  for (int b = 0; b < S.nbands; ++b) {
+    std::unordered_map<int, int> lastInSlot;
+    for (int q = 0; q < F.bandNImp[b]; ++q) {
+      const size_t g = (size_t)F.bandImp[b] + q;
+      if (!impOfRow[b].emplace(F.impRow[g], q).second) return "row imported twice by one band";
+      auto ls = lastInSlot.find(F.impSlot[g]);
+      if (ls != lastInSlot.end()) {
+        nextInSlot[(size_t)F.bandImp[b] + ls->second] = q;
+        if (F.impWait[g] != F.impFree[(size_t)F.bandImp[b] + ls->second]) return "import does not wait for its slot";
+      } else if (F.impWait[g] != -1) {
+        return "first import of a slot waits";
+      }
+      lastInSlot[F.impSlot[g]] = q;
+    }
+  }
+  // the cell that must hold U(j, c) for a reader at (band b, lane l, iteration t)
+  auto check = [&](int j, int c, int b, int l, int t, int cell) -> std::string {
+    const int* ub = jaf.data() + dg[j];
+    const int* ue = jaf.data() + iaf[j + 1];
+    const int* f = std::lower_bound(ub, ue, c);
+    if (f == ue || *f != c) return "value of an entry the pivot row does not hold";
+    const int pos = (int)(f - jaf.data());
+    if (cell <= 0) return "missing value";
+    if (cell < impBase) {
+      const int r = (cell - 1) / kFacWU, u = (cell - 1) % kFacWU, lp = r / (R + 1), sl = r % (R + 1);
+      if (bandOf[j] != b || laneOf[j] != lp || (posOf[j] & (R - 1)) != sl || u != pos - dg[j]) return "ring cell of another value";
+      if (iterOf[j] >= t) return "ring value read before it is written";
+      const size_t gl = (size_t)b * L + lp;
+      const int over = posOf[j] + R;
+      if (over < S.laneLen[gl] && over + S.laneSkew[gl] < t) return "ring value overwritten before it is read";
+      return "";
+    }
+    const int slot = (cell - impBase) / kFacWU, u = (cell - impBase) % kFacWU;
+    if (slot >= F.RI) return "import slot out of range";
+    auto it = impOfRow[b].find(j);
+    if (it == impOfRow[b].end()) return "import of a row the band does not import";
+    const size_t q = (size_t)F.bandImp[b] + it->second;
+    if (F.impSlot[q] != slot || u != pos - dg[j]) return "import read from another slot";
+    if (F.impNeed[(size_t)S.bandSlot[b] + t] < it->second) return "iteration does not wait for its import";
+    if (F.impFree[q] < t) return "import read after its slot is released";
+    if (F.impWait[q] >= t) return "import delivered only after it is read";
+    const int nx = nextInSlot[q];
+    if (nx >= 0 && F.impWait[(size_t)F.bandImp[b] + nx] < t) return "import read after its slot is taken again";
+    if (bandOf[j] == b && iterOf[j] >= t) return "import read before it is written";
+    return "";
+  };
+  for (int i = 0; i < n; ++i) {
+    const int b = bandOf[i], l = laneOf[i], t = iterOf[i];
+    const size_t slot = (size_t)S.bandSlot[b] + t;
+    const int kb = iaf[i], W = iaf[i + 1] - kb, nl = dg[i] - kb;
+    if (F.meta[slot * L + l] != (W | (nl << 8) | (1 << 16))) return "row metadata";
+    for (int e = 0; e < kFacWF; ++e)
+      if (F.vsrc[fac_vidx(slot, e, l)] != (e < W ? kb + e : -1)) return "row values";
+    for (int q = 0; q < kFacNL; ++q) {
+      const int cell = F.code[fac_cidx(slot, kFacNUpd + q, l)];
+      if (q >= nl) {
+        if (cell) return "pivot beyond the lower entries";
+        continue;
+      }
+      const std::string r = check(jaf[kb + q], jaf[kb + q], b, l, t, cell);
+      if (!r.empty()) return "pivot: " + r;
+    }
+    for (int e = 1; e < kFacWF; ++e)
+      for (int q = 0; q < std::min(e, kFacNL); ++q) {
+        const int cell = F.code[fac_cidx(slot, fac_slot(e, q), l)];
+        bool upd = false;
+        if (e < W && q < nl) {  // the reference updates entry e from pivot q iff row j_q holds col(e) above j_q
+          const int j = jaf[kb + q], c = jaf[kb + e];
+          if (c > j) upd = std::binary_search(jaf.begin() + dg[j] + 1, jaf.begin() + iaf[j + 1], c);
+        }
+        if (!upd) {
+          if (cell) return "update the reference does not make";
+          continue;
+        }
+        const std::string r = check(jaf[kb + q], jaf[kb + e], b, l, t, cell);
+        if (!r.empty()) return "update: " + r;
+      }
   }
   return "";
 }

@@ -10,6 +10,9 @@
 //     dependency inside the band, whose values pass through a per-lane LDS ring;
 //   * segments: a row wider than 32 entries (3D) takes ns consecutive positions of its lane, 32
 //     entries each, its partial sum carried in a register; every row of a chain has the same ns;
+//   * pairs (G = 2, rows of at most 16 entries): a position computes two consecutive rows of the
+//     chain, the second taking the first's value from the register (its entry's code is the cell
+//     after the import slots, never read); the lane's ring holds R rows, R / 2 positions;
 //   * imports: values from other bands (or too old for the ring) are copied from the global
 //     granules into LDS import slots by a helper wavefront, in order of first use (slots assigned
 //     by interval colouring: the slot whose previous import's last use has passed); it publishes
@@ -18,6 +21,7 @@
 // the sign of a zero), [1, 1 + 64 (R+1)) the lane rings, then RI import slots.
 // Every row is computed by exactly the arithmetic of the level sweep (same entries, same order).
 #pragma once
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -27,6 +31,7 @@ constexpr int kChainLanes = 64;
 constexpr int kChainRingMax = 32;    // LDS ring slots per lane (doubles) -- chain_sweep.hip kRingMax
 constexpr int kChainImpMax = 2048;   // LDS import slots (16-byte granules) -- chain_sweep.hip kImpMax
 constexpr int kChainPad = -2147483647 - 1;  // empty entry slot (schedule building only)
+constexpr int kChainFwd = -2147483647;      // entry whose value is the pair's first row (building only)
 constexpr int kChainSegMax = 4;      // segments of E = 32 entries a row may take (rows up to 128 entries)
 
 struct ChainSchedule {
@@ -35,6 +40,7 @@ struct ChainSchedule {
   bool fwd = true;
   int E = 0;            // entry slots per row segment (8, 16 or 32)
   bool seg = false;     // rows wider than 32 entries: split into segments at consecutive positions
+  int G = 1;            // rows per position (2: consecutive chain rows as a pair, narrow rows only)
   int R = 0;            // ring slots per lane (power of two); ring stride R + 1
   int RI = 0;           // import slots (power of two)
   int nbands = 0, nchains = 0, maxLen = 0, maxSkew = 0, maxT = 0;
@@ -43,11 +49,11 @@ struct ChainSchedule {
   long long estIters = 0;   // simulated critical path (iterations)
   bool aligned = false;     // lane skews also wait for the lane's imports (chain_sched.cpp pass 1)
   std::vector<int> bandSlot, bandT, bandImp, bandNImp;  // per band
-  std::vector<int> laneStart, laneLen, laneSkew;        // per band * 64 + lane (laneLen in positions)
+  std::vector<int> laneStart, laneLen, laneSkew;        // per band * 64 + lane (laneLen: rows if G = 2, else positions)
   std::vector<int> laneNs;                              // per band * 64 + lane: segments per row
-  std::vector<int> code;   // per (slot * E + e) * 64 + lane: LDS index of the value (0 for pads)
+  std::vector<int> code;   // per ((slot * G + g) * E + e) * 64 + lane: LDS index of the value (0 for pads)
   std::vector<int> src;    // same shape: index of the value in the factor (af), -1 for pads
-  std::vector<int> dsrc;   // backward: per slot * 64 + lane, index of the diagonal in af (-1 idle)
+  std::vector<int> dsrc;   // backward: per (slot * G + g) * 64 + lane, index of the diagonal in af (-1 idle)
   std::vector<int> impRow, impFree;  // per import: producer row; last iteration it is read
   std::vector<int> impSlot, impWait; // per import: LDS slot; iterations to complete before it is
                                      // delivered (the slot's previous import's last use, -1 none)
@@ -59,8 +65,53 @@ struct ChainSchedule {
 };
 
 // fwd: unit-lower sweep over the entries [iaf[i], dg[i]); !fwd: upper sweep over (dg[i], iaf[i+1]).
+// forceG: rows per position (0: automatic).
 ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std::vector<int>& jaf,
-                                   const std::vector<int>& dg, bool fwd);
+                                   const std::vector<int>& dg, bool fwd, int forceG = 0);
+
+// ---- the numeric ILU(0) factor on the same chain/band schedule (chain_factor.hip) ----------------
+// Row i of the factor (scaler_ILU::factor, ILU_class.cpp:300-527, IKJ order) restated target by
+// target: entry e of the row (ascending column) receives, for each lower entry q < e in ascending
+// order whose pivot row j_q holds column col(e) above its diagonal, w_e -= m_q * U(j_q, col e);
+// then a lower entry becomes m_e = w_e / U(j_e, j_e).  Every entry gets exactly the reference's
+// operations in the reference's order.  The values U(j, c) come from the lane rings (a row's
+// diagonal and upper part, kFacWU values per ring slot) or are imported one by one.
+constexpr int kFacWF = 18;   // entries per row (2D mesh rows: <= 18)
+constexpr int kFacNL = 9;    // lower entries per row
+constexpr int kFacWU = 14;   // diagonal + upper entries per row
+constexpr int kFacNSC = 128; // 16-bit codes per row: the (e, q) update slots, then the kFacNL pivots (padded)
+constexpr int kFacImpRows = 384;  // LDS import slots (rows; 2D meshes need <= ~330 live at once)
+constexpr int kFacRMax = 4;       // ring slots per lane (rows)
+// update slot of (e, q), q < min(e, kFacNL): sum over e' < e of min(e', kFacNL), plus q
+constexpr int fac_slot(int e, int q) { return (e <= kFacNL ? e * (e - 1) / 2 : kFacNL * (kFacNL - 1) / 2 + (e - kFacNL) * kFacNL) + q; }
+constexpr int kFacNUpd = fac_slot(kFacWF, 0);  // 117
+// layouts of the per-iteration arrays as the kernel DMA-s them: 16-byte chunks per lane
+inline size_t fac_vidx(size_t slot, int e, int l) { return ((slot * (kFacWF / 2) + e / 2) * 64 + l) * 2 + e % 2; }
+inline size_t fac_cidx(size_t slot, int k, int l) { return ((slot * (kFacNSC / 8) + k / 8) * 64 + l) * 8 + k % 8; }
+static_assert(kFacNUpd + kFacNL <= kFacNSC, "factor codes per row");
+
+struct FactorSchedule {
+  bool ok = false;
+  std::string why;
+  ChainSchedule geo;               // bands, lanes, skews, ticket order (forward, one row per position)
+  int R = 0, RI = 0;
+  long long slots = 0;
+  std::vector<uint16_t> code;      // [slot][kFacNSC][lane]: LDS index of each (e, q) value / pivot (0: none)
+  std::vector<int> vsrc;           // [slot][kFacWF][lane]: factor position of the row's entry e (-1: pad)
+  std::vector<int> meta;           // [slot][lane]: W | nlow << 8 | 1 << 16 for a row, 0 idle
+  std::vector<int> rowStart;       // [slot][lane]: factor position of the row's first entry
+  // imports are whole rows (their diagonal + upper part, kFacWU cells per slot), otherwise as in
+  // ChainSchedule
+  std::vector<int> impRow, impFree, impSlot, impWait, impNeed, bandImp, bandNImp;
+  long long nImports = 0;
+  int maxImpSlots = 0;
+};
+FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const std::vector<int>& jaf,
+                                     const std::vector<int>& dg);
+// Replays the schedule: every row's update and pivot values are the reference's (ring cells of the
+// right row, written before and not overwritten; imports of the right position, delivered in time).
+std::string validate_factor_schedule(const FactorSchedule& F, int n, const std::vector<int>& iaf,
+                                     const std::vector<int>& jaf, const std::vector<int>& dg);
 
 // Replays the lockstep execution of S: every row once, its entries in the reference's order, every
 // ring read served by its producer's value written at an earlier iteration and not yet

@@ -196,6 +196,17 @@ struct SparseMatrix {
   };
   ChainDir chf, chb;
   bool useChain = false;
+  // the numeric factor on the forward chain/band schedule (chain_factor.hip): 2D rows; the level
+  // schedule otherwise or with MMX_FACTOR=level / global
+  struct FactorDir {
+    DevBuf<int> bandSlot, bandT, laneLen, laneSkew, bandOrder, bandImp, bandNImp, impPos, impCnt, impSlot, impWait,
+        impNeed, meta, rowStart, vsrc;
+    DevBuf<uint16_t> code;
+    DevBuf<double> val, af0;
+    DevBuf<uint64_t> gU;
+    FactorArgs args{};
+  } chfac;
+  bool useChainFactor = false;
   DevBuf<unsigned long long> d_cprof;  // MMX_CHAIN_PROF: 2 x 512 counters (forward, backward)
   // numeric factor cache: the ILU of unchanged values is the same, so a solve re-factors only
   // after set_values / sfac (the reference re-factors in every solve, MatrixIter.cpp:684)
@@ -366,6 +377,17 @@ struct SparseMatrix {
         useChain = true;
       }
     }
+    useChainFactor = false;
+    {
+      const char* fm = getenv("MMX_FACTOR");
+      if (useChain && !(fm && (std::strcmp(fm, "level") == 0 || std::strcmp(fm, "global") == 0))) {
+        const FactorSchedule FS = build_factor_schedule(n, iaf, jaf, dg);
+        if (FS.ok) {
+          upload_factor(FS, dg);
+          useChainFactor = true;
+        }
+      }
+    }
     MMX_HIP(hipStreamSynchronize(st));
     MMX_HIP(hipStreamSynchronize(st));
     symbolic = true;
@@ -409,8 +431,50 @@ struct SparseMatrix {
     }
     c.args = ChainArgs{c.bandSlot.p, c.bandT.p, c.bandImp.p, c.bandNImp.p, c.laneStart.p, c.laneLen.p, c.laneSkew.p,
                        c.laneNs.p, c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impSlot.p, c.impWait.p, c.impNeed.p,
-                       c.bandOrder.p, S.nbands, S.R, S.RI, S.seg ? 1 : 0,
+                       c.bandOrder.p, S.nbands, S.R, S.RI, S.seg ? 1 : 0, S.G,
                        d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr, (pe && atoi(pe) >= 2) ? 1 : 0};
+  }
+
+  void upload_factor(const FactorSchedule& F, const std::vector<int>& dg) {
+    auto up = [&](DevBuf<int>& d, const std::vector<int>& h) {
+      if (h.empty()) {
+        const int z = 0;
+        d.upload(&z, 1, st);
+      } else {
+        d.upload(h.data(), h.size(), st);
+      }
+    };
+    FactorDir& c = chfac;
+    const ChainSchedule& S = F.geo;
+    up(c.bandSlot, S.bandSlot);
+    up(c.bandT, S.bandT);
+    up(c.laneLen, S.laneLen);
+    up(c.laneSkew, S.laneSkew);
+    up(c.bandOrder, S.bandOrder);
+    up(c.bandImp, F.bandImp);
+    up(c.bandNImp, F.bandNImp);
+    std::vector<int> pos(F.impRow.size()), cnt(F.impRow.size());
+    for (size_t k = 0; k < F.impRow.size(); ++k) {
+      const int j = F.impRow[k];
+      pos[k] = dg[j];
+      cnt[k] = iaf[j + 1] - dg[j];
+    }
+    up(c.impPos, pos);
+    up(c.impCnt, cnt);
+    up(c.impSlot, F.impSlot);
+    up(c.impWait, F.impWait);
+    up(c.impNeed, F.impNeed);
+    up(c.meta, F.meta);
+    up(c.rowStart, F.rowStart);
+    up(c.vsrc, F.vsrc);
+    c.code.upload(F.code.data(), F.code.size(), st);
+    c.val.alloc(std::max<size_t>(F.vsrc.size(), 1));
+    c.af0.alloc(std::max<size_t>(jaf.size(), 1));
+    c.gU.alloc(2 * std::max<size_t>(jaf.size(), 1));
+    MMX_HIP(hipMemsetAsync(c.gU.p, 0, c.gU.n * sizeof(uint64_t), st));
+    c.args = FactorArgs{c.bandSlot.p, c.bandT.p, c.laneLen.p, c.laneSkew.p, c.bandOrder.p, c.bandImp.p, c.bandNImp.p,
+                        c.impPos.p, c.impCnt.p, c.impSlot.p, c.impWait.p, c.impNeed.p, c.val.p, c.code.p, c.meta.p,
+                        c.rowStart.p, S.nbands, F.R};
   }
 
   void begin(int t) {
@@ -445,10 +509,16 @@ struct SparseMatrix {
     MMX_HIP(hipMemsetAsync(tickets(), 0, 8 * sizeof(unsigned), st));
     if (++fepoch == 0) {
       MMX_HIP(hipMemsetAsync(d_flags.p, 0, sizeof(unsigned) * n, st));
+      if (useChainFactor) MMX_HIP(hipMemsetAsync(chfac.gU.p, 0, chfac.gU.n * sizeof(uint64_t), st));
       fepoch = 1;
     }
     begin(2);
-    if (facLds)
+    if (useChainFactor) {  // A into the factor pattern, the rows' values in schedule order, the factor
+      MMX_HIP(hipMemsetAsync(chfac.af0.p, 0, chfac.af0.n * sizeof(double), st));
+      launch_scatter_a((long long)nnz, d_amap.p, d_a.p, chfac.af0.p, st);
+      launch_chain_fill((long long)chfac.vsrc.n, chfac.vsrc.p, chfac.af0.p, chfac.val.p, 0.0, st);
+      launch_chain_factor(chfac.args, d_af.p, chfac.gU.p, fepoch, tickets(), errw(), st);
+    } else if (facLds)
       launch_ilu_factor_lds(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_toff.p, d_tgt.p, d_permf.p, nchf,
                             d_af.p, d_flags.p, fepoch, tickets(), errw(), st);
     else
@@ -943,6 +1013,7 @@ int mmx_matrix_stats_get(mmx_matrix m, mmx_sparse_stats* out) {
     if (out) {
       *out = M.stats;
       out->sweep_mode = M.useChain ? 1 : 0;
+      out->factor_mode = M.useChainFactor ? 1 : 0;
       out->sweep_e = M.useChain ? M.chf.E : 0;
     }
   });

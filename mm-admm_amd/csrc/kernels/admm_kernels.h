@@ -26,7 +26,8 @@ struct DeviceMesh {
   double* gcache;         // per simplex K+1: unregularised gradient and energy at the current z
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
-  unsigned* tieStale;     // the previous steady prox's counter, cleared by this prox's recomputation
+  unsigned* tieStale;
+  int xupSweep;           // 3D slot-term x-update as a per-XCD sweep: workgroups per CU (0: one node per lane)     // the previous steady prox's counter, cleared by this prox's recomputation
   int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
   const int* nodeOrder;   // x-update processing order (nodes by first incident simplex) or nullptr
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)

@@ -228,16 +228,12 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
 // are requested before the first is added (branch-free: lanes past the end re-read the last
 // slot, a slot of another rank reads its gathered row), then summed in ascending order.
 template <int D, bool RESID, bool TS>
-__global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
-                                                     const double* __restrict__ xBar,
-                                                     const double* __restrict__ z,
-                                                     const double* __restrict__ u, double* __restrict__ x,
-                                                     double* __restrict__ partials, int xcd) {
+__device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepScalars& sc,
+                                             const double* __restrict__ xBar, const double* __restrict__ z,
+                                             const double* __restrict__ u, double* __restrict__ x, int idx,
+                                             double (&pv)[3]) {
   constexpr int CH = 8;
-  const int lb = logical_block(xcd);
-  const int idx = lb * kBlock + threadIdx.x;
-  double pv[3] = {0, 0, 0};
-  if (idx < m.nP) {
+  {
     // processing order: nodes by first incident simplex, so a workgroup's nodes share simplices
     const int v = m.nodeOrder ? m.nodeOrder[idx] : idx;
     double acc[D];
@@ -316,7 +312,31 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
       pv[2] = r2;
     }
   }
+}
+template <int D, bool RESID, bool TS>
+__global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
+                                                     const double* __restrict__ xBar,
+                                                     const double* __restrict__ z,
+                                                     const double* __restrict__ u, double* __restrict__ x,
+                                                     double* __restrict__ partials, int xcd) {
+  const int lb = logical_block(xcd);
+  const int idx = lb * kBlock + threadIdx.x;
+  double pv[3] = {0, 0, 0};
+  if (idx < m.nP) xupdate_node<D, RESID, TS>(m, sc, xBar, z, u, x, idx, pv);
   if constexpr (RESID) block_partials<3>(pv, partials, lb);
+}
+// The slot-term x-update (no residual) as a sweep: XCD c (= blockIdx % 8) takes the node-order
+// positions [c n8, (c + 1) n8) and its gridDim / 8 workgroups walk them in rounds, so the slot
+// terms a round gathers are mostly still in that XCD's L2 for the neighbouring rounds.
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_xupdate_sweep(DeviceMesh<D> m, StepScalars sc,
+                                                           const double* __restrict__ xBar, double* __restrict__ x,
+                                                           int n8) {
+  const int c = (int)(blockIdx.x % 8), w = (int)(blockIdx.x / 8), per = (int)(gridDim.x / 8);
+  const int lo = c * n8, hi = min(lo + n8, m.nP);
+  double pv[3];
+  for (int idx = lo + w * kBlock + (int)threadIdx.x; idx < hi; idx += per * kBlock)
+    xupdate_node<D, false, true>(m, sc, xBar, nullptr, nullptr, x, idx, pv);
 }
 
 // k x k inverse: unblocked partial-pivot LU + substitution (mirrors the oracle's restatement
@@ -1892,6 +1912,11 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   *nblocks = nblk_xcd(m.nP);
   if (m.nP == 0) return;
   const bool ts = useTslot && m.tslot;
+  if (ts && !resid && m.xupSweep > 0) {  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU
+    const int n8 = ((m.nP + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
+    hipLaunchKernelGGL((k_xupdate_sweep<D>), dim3(256 * m.xupSweep), dim3(kBlock), 0, st, m, sc, xBar, x, n8);
+    return;
+  }
 #define MMX_XU(R, T)                                                                                               \
   hipLaunchKernelGGL((k_xupdate<D, R, T>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x, partials, \
                      xcd_map())

@@ -15,7 +15,9 @@
 // Every row is x_i = (b_i - sum_k a_k x_jk) [/ d_i] with the terms subtracted in ascending column
 // order, exactly as the level-scheduled k_sweep and the reference.  SEG: a lane's rows take ns
 // positions each (32 entries per position, the partial sum carried in a register), for triangles
-// with rows wider than 32 entries (3D).
+// with rows wider than 32 entries (3D).  G = 2: a position computes two consecutive rows of the
+// chain (rows of at most 16 entries, 2D), the second taking the first's value from the register,
+// which halves the iterations on the critical path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -72,12 +74,18 @@ template <int E>
 struct Geo {
   static constexpr int DL = (E <= 16) ? 8 : 4;  // stages in the LDS ring
 };
-template <bool FWD, int PRO>
+template <bool FWD, int PRO, int G>
 struct AuxN {  // DMA instructions for the right-hand-side operands of one stage (+1: impNeed)
-  static constexpr int n = (FWD ? (PRO == 0 ? 2 : PRO == 1 ? 6 : 4) : 2) + 1;  // bwd: y granule + diagonal
+  static constexpr int n = G * (FWD ? (PRO == 0 ? 2 : PRO == 1 ? 6 : 4) : 2) + 1;  // bwd: y granule + diagonal
 };
-constexpr int kAuxWords = 448;  // per stage: operands (<= 384 words) + impNeed (64 copies)
-constexpr int kDepCells = 1 + 64 * (kRingMax + 1) + kImpMax;
+// per stage: the operands of each of the G rows of a position (<= 384 words each), then impNeed
+// (64 copies)
+template <int G>
+struct Aux {
+  static constexpr int need = 384 * G;
+  static constexpr int words = need + 64;
+};
+constexpr int kDepCells = 1 + 64 * (kRingMax + 1) + kImpMax + 1;  // + the pairs' forwarded cell
 
 // abort protocol: a bounded wait that gives up sets err; everyone polls err now and then
 __device__ __forceinline__ bool aborted(unsigned* err) {
@@ -102,20 +110,23 @@ __device__ __forceinline__ void prof_add(unsigned long long* prof, int i, unsign
   if (prof) atomicAdd(prof + i, v);
 }
 
-template <bool FWD, int PRO, int E, bool SEG>
+template <bool FWD, int PRO, int E, bool SEG, int G>
 __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double* __restrict__ src,
                                                      double* __restrict__ pvec, const double* __restrict__ res,
                                                      const double* __restrict__ avbar, const CgsScalars* __restrict__ sc,
                                                      const uint64_t* __restrict__ gin, uint64_t* gout,
                                                      double* __restrict__ out, unsigned epoch, unsigned* ticket,
                                                      unsigned* err) {
-  constexpr int DL = Geo<E>::DL;
-  constexpr int NAUX = AuxN<FWD, PRO>::n;
-  constexpr int NI = E / 2 + E / 4 + NAUX;          // DMA instructions per stage
+  static_assert(G == 1 || !SEG, "pairs of segmented rows");
+  constexpr int EE = E * G;  // entry slots per position
+  constexpr int DL = Geo<EE>::DL;
+  constexpr int NAUX = AuxN<FWD, PRO, G>::n;
+  constexpr int kAuxWords = Aux<G>::words;
+  constexpr int NI = EE / 2 + EE / 4 + NAUX;          // DMA instructions per stage
   constexpr int LAG0 = 63 / NI < 1 ? 1 : 63 / NI;
   constexpr int LAG = LAG0 < DL / 2 ? LAG0 : DL / 2;  // own stages in flight per loader
-  __shared__ double s_val[DL * E * 64];
-  __shared__ int s_code[DL * E * 64];
+  __shared__ double s_val[DL * EE * 64];
+  __shared__ int s_code[DL * EE * 64];
   __shared__ uint32_t s_aux[DL * kAuxWords];
   __shared__ double s_dep[kDepCells];  // [0] = +0.0, lane rings, import slots
   __shared__ int s_tag[DL];
@@ -124,6 +135,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int R = ca.R;
   const int impBase = 1 + 64 * (R + 1);
+  const int fwdCell = impBase + ca.RI;  // G = 2: the entry whose value is the pair's first row
   double beta = 0.0, omega = 0.0, alpha = 0.0;
   if (FWD && PRO == 1) {
     beta = sc->beta;
@@ -162,41 +174,47 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       unsigned long long c0 = ca.prof ? clk() : 0, cstage = 0, cimp = 0;
       bool ok = true;
       struct Fetched {
-        double a[E];
-        int c[E];
-        double init, diag;
+        double a[EE];
+        int c[EE];
+        double init[G], diag[G];
         int need;
       };
       auto load_stage = [&](int st, Fetched& f) {
-        const uint32_t* sa = s_aux + st * kAuxWords;
-        f.need = (int)sa[384 + lane];  // the same in every lane; made scalar where it is used
-        const double* sv = s_val + st * E * 64;
-        const int* scd = s_code + st * E * 64;
+        const uint32_t* sa0 = s_aux + st * kAuxWords;
+        f.need = (int)sa0[Aux<G>::need + lane];  // the same in every lane; made scalar where it is used
+        const double* sv = s_val + st * EE * 64;
+        const int* scd = s_code + st * EE * 64;
 #pragma unroll
-        for (int e0 = 0; e0 < E; e0 += 4)
-          if (e0 < Eb) {
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              f.a[e0 + q] = sv[(e0 + q) * 64 + lane];
-              f.c[e0 + q] = scd[(e0 + q) * 64 + lane];
+          for (int e0 = 0; e0 < E; e0 += 4)
+            if (e0 < Eb) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                f.a[g * E + e0 + q] = sv[(g * E + e0 + q) * 64 + lane];
+                f.c[g * E + e0 + q] = scd[(g * E + e0 + q) * 64 + lane];
+              }
             }
-          }
-        if (FWD) {
-          const double r0 = join_words(sa[lane], sa[64 + lane]);
-          if (PRO == 0) {
-            f.init = r0;
-          } else if (PRO == 1) {
-            const double pv = join_words(sa[128 + lane], sa[192 + lane]);
-            const double av = join_words(sa[256 + lane], sa[320 + lane]);
-            f.init = r0 + beta * (pv - omega * av);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint32_t* sa = sa0 + g * 384;
+          if (FWD) {
+            const double r0 = join_words(sa[lane], sa[64 + lane]);
+            if (PRO == 0) {
+              f.init[g] = r0;
+            } else if (PRO == 1) {
+              const double pv = join_words(sa[128 + lane], sa[192 + lane]);
+              const double av = join_words(sa[256 + lane], sa[320 + lane]);
+              f.init[g] = r0 + beta * (pv - omega * av);
+            } else {
+              const double av = join_words(sa[128 + lane], sa[192 + lane]);
+              f.init[g] = r0 - alpha * av;
+            }
+            f.diag[g] = 1.0;
           } else {
-            const double av = join_words(sa[128 + lane], sa[192 + lane]);
-            f.init = r0 - alpha * av;
+            f.init[g] = join_words(sa[4 * lane], sa[4 * lane + 2]);  // granule {tag|lo, tag|hi}
+            f.diag[g] = join_words(sa[256 + 2 * lane], sa[256 + 2 * lane + 1]);
           }
-          f.diag = 1.0;
-        } else {
-          f.init = join_words(sa[4 * lane], sa[4 * lane + 2]);  // granule {tag|lo, tag|hi}
-          f.diag = join_words(sa[256 + 2 * lane], sa[256 + 2 * lane + 1]);
         }
       };
       auto fetch = [&](int t, Fetched& f) {  // blocking: wait for stage t, then read it
@@ -223,13 +241,15 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           if (ca.profIter) cimp += clk() - i0;
           if (!ok) return;
         }
-        double v[E];
+        double v[EE];
 #pragma unroll
-        for (int e0 = 0; e0 < E; e0 += 4)
-          if (e0 < Eb) {
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[e0 + q] = s_dep[f.c[e0 + q]];
-          }
+          for (int e0 = 0; e0 < E; e0 += 4)
+            if (e0 < Eb) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[g * E + e0 + q] = s_dep[f.c[g * E + e0 + q]];
+            }
         const bool hasNext = t + 1 < T;
         const int stn = (t + 1) & (DL - 1);
         const int tagN = __hip_atomic_load(&s_tag[stn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -237,33 +257,43 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
         asm volatile("" ::: "memory");  // keep the stage reads behind the tag read (LDS serves them in order)
         if (hasNext) load_stage(stn, nx);
         const int p = t - skew;
-        if (p >= 0 && p < len) {
-          int ri = p, sg = 0;  // row of the chain, segment of the row
-          if constexpr (SEG) {
-            ri = p / ns;
-            sg = p - ri * ns;
-          }
-          const int row = FWD ? cst + ri : cst - ri;
-          // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
-          double acc = (SEG && sg != 0) ? carry : f.init;
+        double prev = 0.0;  // G = 2: the pair's first row
 #pragma unroll
-          for (int e0 = 0; e0 < E; e0 += 4)
-            if (e0 < Eb) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) acc -= f.a[e0 + q] * v[e0 + q];
+        for (int g = 0; g < G; ++g) {
+          const bool on = (G == 2) ? (p >= 0 && 2 * p + g < len) : (p >= 0 && p < len);
+          if (on) {
+            int ri = (G == 2) ? 2 * p + g : p, sg = 0;  // row of the chain, segment of the row
+            if constexpr (SEG) {
+              ri = p / ns;
+              sg = p - ri * ns;
             }
-          if (SEG && sg != ns - 1) {
-            carry = acc;  // the row goes on at the next position
-          } else {
-            if (!FWD) acc = acc / f.diag;
-            s_dep[1 + lane * (R + 1) + (p & (R - 1))] = acc;
-            const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
-            __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            if (!FWD) out[row] = acc;
-            if (FWD && PRO != 0) pvec[row] = f.init;
+            const int row = FWD ? cst + ri : cst - ri;
+            // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
+            double acc = (SEG && sg != 0) ? carry : f.init[g];
+#pragma unroll
+            for (int e0 = 0; e0 < E; e0 += 4)
+              if (e0 < Eb) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const int e = g * E + e0 + q;
+                  const double val = (G == 2 && g == 1 && f.c[e] == fwdCell) ? prev : v[e];
+                  acc -= f.a[e] * val;
+                }
+              }
+            if (SEG && sg != ns - 1) {
+              carry = acc;  // the row goes on at the next position
+            } else {
+              if (!FWD) acc = acc / f.diag[g];
+              s_dep[1 + lane * (R + 1) + (((G == 2) ? ri : p) & (R - 1))] = acc;
+              const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
+              __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              if (!FWD) out[row] = acc;
+              if (FWD && PRO != 0) pvec[row] = f.init[g];
+              prev = acc;
+            }
           }
         }
         if (lane == 0) lds_write(&s_prog, t + 1);
@@ -314,34 +344,40 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           if (!ok) break;
         }
         const size_t slot = (size_t)(sb + t);
-        const double* gv = ca.val + slot * E * 64;
+        const double* gv = ca.val + slot * EE * 64;
 #pragma unroll
-        for (int i = 0; i < E / 2; ++i) dma16(gv + i * 128 + lane * 2, s_val + st * E * 64 + i * 128);
-        const int* gc = ca.code + slot * E * 64;
+        for (int i = 0; i < EE / 2; ++i) dma16(gv + i * 128 + lane * 2, s_val + st * EE * 64 + i * 128);
+        const int* gc = ca.code + slot * EE * 64;
 #pragma unroll
-        for (int i = 0; i < E / 4; ++i) dma16(gc + i * 256 + lane * 4, s_code + st * E * 64 + i * 256);
+        for (int i = 0; i < EE / 4; ++i) dma16(gc + i * 256 + lane * 4, s_code + st * EE * 64 + i * 256);
         const int p = t - skew;
-        const int ri = SEG ? p / ns : p;  // the row's operands at each of its segments
-        const int row = (p >= 0 && p < len) ? (FWD ? cst + ri : cst - ri) : 0;
-        uint32_t* sa = s_aux + st * kAuxWords;
-        if (FWD) {
-          const double* v0 = (PRO == 0) ? src : res;
-          dma4((const char*)(v0 + row), sa);
-          dma4((const char*)(v0 + row) + 4, sa + 64);
-          if (PRO == 1) {
-            dma4((const char*)(pvec + row), sa + 128);
-            dma4((const char*)(pvec + row) + 4, sa + 192);
-            dma4((const char*)(avbar + row), sa + 256);
-            dma4((const char*)(avbar + row) + 4, sa + 320);
-          } else if (PRO == 2) {
-            dma4((const char*)(avbar + row), sa + 128);
-            dma4((const char*)(avbar + row) + 4, sa + 192);
+        uint32_t* sa0 = s_aux + st * kAuxWords;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          // the row's operands (at each of its segments; a missing second row of a pair: row 0)
+          const int ri = (G == 2) ? 2 * p + g : (SEG ? p / ns : p);
+          const bool on = (G == 2) ? (p >= 0 && ri < len) : (p >= 0 && p < len);
+          const int row = on ? (FWD ? cst + ri : cst - ri) : 0;
+          uint32_t* sa = sa0 + g * 384;
+          if (FWD) {
+            const double* v0 = (PRO == 0) ? src : res;
+            dma4((const char*)(v0 + row), sa);
+            dma4((const char*)(v0 + row) + 4, sa + 64);
+            if (PRO == 1) {
+              dma4((const char*)(pvec + row), sa + 128);
+              dma4((const char*)(pvec + row) + 4, sa + 192);
+              dma4((const char*)(avbar + row), sa + 256);
+              dma4((const char*)(avbar + row) + 4, sa + 320);
+            } else if (PRO == 2) {
+              dma4((const char*)(avbar + row), sa + 128);
+              dma4((const char*)(avbar + row) + 4, sa + 192);
+            }
+          } else {
+            dma16(gin + 2 * (size_t)row, sa);  // 64 x 16 B: words 0..255
+            if (lane < 32) dma16(ca.dval + (slot * G + g) * 64 + lane * 2, sa + 256);  // 64 diagonals: words 256..383
           }
-        } else {
-          dma16(gin + 2 * (size_t)row, sa);  // 64 x 16 B: words 0..255
-          if (lane < 32) dma16(ca.dval + slot * 64 + lane * 2, sa + 256);  // 64 diagonals: words 256..383
         }
-        dma4(ca.impNeed + slot, sa + 384);  // the same word in every lane
+        dma4(ca.impNeed + slot, sa0 + Aux<G>::need);  // the same word in every lane
         if ((t - nextPub) / 2 + 1 > LAG) {
           const unsigned long long l0 = ca.prof ? clk() : 0;
           wait_vm<NI * LAG>();
@@ -437,19 +473,23 @@ void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const dou
                         unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st) {
   if (ca.nbands <= 0) return;
   const dim3 grid(ca.nbands < 256 ? ca.nbands : 256), block(256);
-#define MMX_CHAIN(F, P, EE, SG)                                                                                    \
-  hipLaunchKernelGGL((k_chain_sweep<F, P, EE, SG>), grid, block, 0, st, ca, src, p, res, avbar, sc, gin, gout, \
+#define MMX_CHAIN(F, P, EE, SG, GG)                                                                            \
+  hipLaunchKernelGGL((k_chain_sweep<F, P, EE, SG, GG>), grid, block, 0, st, ca, src, p, res, avbar, sc, gin, gout, \
                      out, epoch, ticket, err)
-#define MMX_CHAIN_E(F, P)      \
-  do {                         \
-    if (ca.seg)                \
-      MMX_CHAIN(F, P, 32, true); \
-    else if (E == 8)           \
-      MMX_CHAIN(F, P, 8, false); \
-    else if (E == 16)          \
-      MMX_CHAIN(F, P, 16, false); \
-    else                       \
-      MMX_CHAIN(F, P, 32, false); \
+#define MMX_CHAIN_E(F, P)                \
+  do {                                   \
+    if (ca.seg)                          \
+      MMX_CHAIN(F, P, 32, true, 1);      \
+    else if (ca.G == 2 && E == 8)        \
+      MMX_CHAIN(F, P, 8, false, 2);      \
+    else if (ca.G == 2)                  \
+      MMX_CHAIN(F, P, 16, false, 2);     \
+    else if (E == 8)                     \
+      MMX_CHAIN(F, P, 8, false, 1);      \
+    else if (E == 16)                    \
+      MMX_CHAIN(F, P, 16, false, 1);     \
+    else                                 \
+      MMX_CHAIN(F, P, 32, false, 1);     \
   } while (0)
   if (!fwd)
     MMX_CHAIN_E(false, 0);
@@ -470,6 +510,17 @@ __global__ void k_chain_fill(long long n, const int* __restrict__ srcIdx, const 
     const int s = srcIdx[x];
     val[x] = s >= 0 ? af[s] : padValue;
   }
+}
+
+__global__ void k_scatter_a(long long nnz, const int* __restrict__ amap, const double* __restrict__ a,
+                            double* __restrict__ af) {
+  const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (k < nnz) af[amap[k]] = a[k];
+}
+
+void launch_scatter_a(long long nnz, const int* amap, const double* a, double* af, hipStream_t st) {
+  if (nnz <= 0) return;
+  hipLaunchKernelGGL(k_scatter_a, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, st, nnz, amap, a, af);
 }
 
 void launch_chain_fill(long long n, const int* srcIdx, const double* af, double* val, double padValue,

@@ -84,13 +84,40 @@ struct ChainArgs {
   const int* impNeed;  // per slot: highest import index read at that iteration (-1: none)
   const int* bandOrder;  // per ticket: the band taken
   int nbands, R, RI;
-  int seg;             // the schedule splits rows into segments of 32 entries (k_chain_sweep<..., 32, true>)
+  int seg;             // the schedule splits rows into segments of 32 entries (k_chain_sweep<..., 32, true, 1>)
+  int G;               // rows per position (2: pairs of consecutive chain rows)
   unsigned long long* prof;  // optional cycle counters (MMX_CHAIN_PROF), see chain_sweep.hip
   int profIter;              // MMX_CHAIN_PROF=2: also time the waits inside iterations (perturbs them)
 };
 void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const double* src, double* p, const double* res,
                         const double* avbar, const CgsScalars* sc, const uint64_t* gin, uint64_t* gout, double* out,
                         unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
+// the numeric ILU(0) factor on the forward chain/band schedule (chain_factor.hip; host/chain_sched.h
+// build_factor_schedule)
+struct FactorArgs {
+  const int* bandSlot;
+  const int* bandT;
+  const int* laneLen;
+  const int* laneSkew;
+  const int* bandOrder;
+  const int* bandImp;
+  const int* bandNImp;
+  const int* impPos;    // per import: factor position of the row's diagonal
+  const int* impCnt;    //   its diagonal + upper entries
+  const int* impSlot;
+  const int* impWait;
+  const int* impNeed;   // per slot
+  const double* val;    // [slot][kFacWF / 2][64][2] the row's initial values (launch_chain_fill)
+  const uint16_t* code; // [slot][kFacNSC / 8][64][8] LDS indices of the update and pivot values
+  const int* meta;      // [slot][64] W | nlow << 8 | 1 << 16
+  const int* rowStart;  // [slot][64] factor position of the row's first entry
+  int nbands, R;
+};
+void launch_chain_factor(const FactorArgs& fa, double* af, uint64_t* gU, unsigned epoch, unsigned* ticket,
+                         unsigned* err, hipStream_t st);
+// af[amap[k]] = a[k] over the nnz entries of A (af zeroed before: the fill entries start at 0)
+void launch_scatter_a(long long nnz, const int* amap, const double* a, double* af, hipStream_t st);
+
 // val[x] = af[srcIdx[x]] (padValue where srcIdx < 0)
 void launch_chain_fill(long long n, const int* srcIdx, const double* af, double* val, double padValue,
                        hipStream_t st);

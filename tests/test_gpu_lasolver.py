@@ -226,10 +226,15 @@ def _sweep_run(la, ia, ja, a, b, mode, monkeypatch):
 
 @pytest.mark.parametrize("mesh", [("rect", 2, 45), ("hexdisc", 40), ("circle", "CircleEx24"), ("rect", 2, 300),
                                   ("rect", 3, 12), ("rect", 3, 30)])
-def test_chain_sweeps_equal_level_sweeps(la, mesh, monkeypatch):
+@pytest.mark.parametrize("pair", ["1", "0"])
+def test_chain_sweeps_equal_level_sweeps(la, mesh, pair, monkeypatch):
     """The chain/band-scheduled sweeps (chain_sweep.hip) and the level-scheduled ones compute every
     row with the same operations in the same order: ILU solves and CG-STAB iterates are identical.
-    3D: the upper rows (up to 44 entries) run as two 32-entry segments (k_chain_sweep<..., SEG>)."""
+    3D: the upper rows (up to 44 entries) run as two 32-entry segments (k_chain_sweep<..., SEG>);
+    2D: two chain rows per iteration (pair 1, the default) or one."""
+    if mesh[1] == 3 and pair == "0":
+        pytest.skip("3D schedules have one row per position")
+    monkeypatch.setenv("MMX_CHAIN_PAIR", pair)
     import mmadmm_amd as mx
     from conftest import circle_mesh
     if mesh[0] == "rect":
@@ -298,3 +303,49 @@ def test_full_size_factor_sweeps_and_solve_bitwise(la, shift):
     xo, io, _ = L.solve(ia, ja, a, b)
     assert abs(it - io) <= 1 and _rel(x, xo) <= p.resid_reduc, (it, io, _rel(x, xo))
     A.close()
+
+
+def _factor_run(la, ia, ja, a, mode, monkeypatch):
+    if mode:
+        monkeypatch.setenv("MMX_FACTOR", mode)
+    else:
+        monkeypatch.delenv("MMX_FACTOR", raising=False)
+    A = _matrix(la, ia, ja, a, np.ones(len(ia) - 1))
+    A.sfac(la.ParamIter.mesh())
+    A.factor()
+    af = A.get_factor()[2]
+    fm = A.stats()["factor_mode"]
+    A.close()
+    return af, fm
+
+
+@pytest.mark.parametrize("mesh", [("rect", 2, 12), ("rect", 2, 45), ("hexdisc", 40), ("circle", "CircleEx24"),
+                                  ("rect", 2, 300)])
+def test_chain_factor_equals_level_factor(la, mesh, monkeypatch):
+    """The numeric ILU(0) factor on the forward chain/band schedule (chain_factor.hip: each entry's
+    updates target by target, pivots from the lane rings or imported rows) is bit-identical to the
+    level-scheduled k_ilu_factor_lds and, at small sizes, to the restatement of the reference."""
+    import mmadmm_amd as mx
+    from conftest import circle_mesh
+    if mesh[0] == "rect":
+        m = oracle_py.Mesh.rect(mesh[1], mesh[2])
+        dim, F, nP = mesh[1], m.F, m.nP
+    elif mesh[0] == "hexdisc":
+        md = mx.MeshData.hexdisc(mesh[1], 0.5, 0.5, 0.5)
+        dim, F, nP = 2, md.F, md.nP
+    else:
+        c = circle_mesh(mesh[1])
+        dim, F, nP = 2, c.F, c.Vp.shape[0]
+    ia, ja = L.mesh_pattern(dim, nP, F)
+    N = len(ia) - 1
+    rng = np.random.default_rng(11)
+    a = rng.uniform(-1, 1, len(ja))
+    rows = np.repeat(np.arange(N), np.diff(ia))
+    d = np.nonzero(ja == rows)[0]
+    a[d] = np.add.reduceat(np.abs(a), ia[:-1]) * 0.3 + 1.0
+    af_c, fm_c = _factor_run(la, ia, ja, a, None, monkeypatch)
+    af_l, fm_l = _factor_run(la, ia, ja, a, "level", monkeypatch)
+    assert fm_c == 1 and fm_l == 0
+    assert _bit(af_c, af_l)
+    if N < 20000:
+        assert _bit(af_c, L.ilu0(ia, ja, a))

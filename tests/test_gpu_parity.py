@@ -267,3 +267,25 @@ def test_quad_lane_prox_equals_wave_at_c4(monkeypatch):
     assert Q.stats()["bfgs_iters"] == W.stats()["bfgs_iters"]
     W.close()
     Q.close()
+
+
+@pytest.mark.parametrize("order,sweep", [(0, 0), (1, 0), (0, 2), (1, 4)])
+def test_xupdate_order_and_sweep_bitwise(order, sweep, monkeypatch):
+    """The 3D slot-term x-update in its forms -- nodes by first incident simplex (order 0) or in eight
+    y slabs, one per XCD group (order 1, the default); one node per lane (sweep 0) or walked as a
+    per-XCD sweep by a persistent grid of `sweep` workgroups per CU (default 1) -- sums every
+    node's slots in the same ascending order: positions bit-identical to the default."""
+    m = mx.MeshData.rect(3, 24)
+    M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 6), rho=2000.0, tau=0.5)
+    W = mx.Engine(M, 0.025)
+    W.step(10, -1.0)
+    W.step(10, -1.0)
+    monkeypatch.setenv("MMX_XUP_ORDER", str(order))
+    monkeypatch.setenv("MMX_XUP_SWEEP", str(sweep))
+    Q = mx.Engine(M, 0.025)
+    Q.step(10, -1.0)
+    Q.step(10, -1.0)
+    for f in ("x", "z", "u"):
+        np.testing.assert_array_equal(Q.get(f), W.get(f), err_msg=f)
+    W.close()
+    Q.close()

@@ -88,10 +88,12 @@ def _schedule_info(ia, ja, level, fwd):
 @pytest.mark.parametrize("mesh,level", [(("rect", 2, 20), 0), (("rect", 2, 57), 0), (("rect", 2, 20), 1),
                                         (("hexdisc", 30), 0), (("circle", "CircleEx24"), 0), (("rect", 3, 6), 0),
                                         (("rect", 3, 14), 0)])
-def test_chain_schedule_is_valid(mesh, level):
+@pytest.mark.parametrize("pair", ["1", "0"])
+def test_chain_schedule_is_valid(mesh, level, pair, monkeypatch):
     """The chain/band sweep schedule (host/chain_sched.cpp) replays correctly on the host: every row
-    once with the reference's entry order, ring values live when read, imports right and ordered
-    (validate_chain_schedule, which mmx_sweep_schedule_info runs and fails on)."""
+    once with the reference's entry order, ring values live when read, imports right and ordered,
+    a pair's forwarded entry its first row (validate_chain_schedule, which mmx_sweep_schedule_info
+    runs and fails on)."""
     import mmadmm_amd as mx
     from conftest import circle_mesh
     if mesh[0] == "rect":
@@ -104,6 +106,7 @@ def test_chain_schedule_is_valid(mesh, level):
         c = circle_mesh(mesh[1])
         dim, F, nP = 2, c.F, c.Vp.shape[0]
     ia, ja = L.mesh_pattern(dim, nP, F)
+    monkeypatch.setenv("MMX_CHAIN_PAIR", pair)  # 2D: two rows per position (default) or one
     for fwd in (True, False):
         info = _schedule_info(ia, ja, level, fwd)
         assert info["ok"] == 1, info
@@ -111,6 +114,9 @@ def test_chain_schedule_is_valid(mesh, level):
             # 3D: the upper rows (up to 44 entries) take two 32-entry segments, and each band's lanes
             # wait for imports from several planes; the modelled path stays within a few DAG depths
             assert info["E"] == 32 and info["estIters"] <= 4 * info["levels"] + 64, info
+        elif pair == "1":
+            # two chain rows per iteration: the critical path is about half the DAG's depth
+            assert info["estIters"] <= 0.7 * info["levels"] + 64, info
         else:
             # the critical path stays close to the dependency DAG's depth
             assert info["estIters"] <= 1.3 * info["levels"] + 64, info
