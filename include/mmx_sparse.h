@@ -126,6 +126,10 @@ int mmx_ilu_symbolic(int n, const int32_t* ia, const int32_t* ja, int level, lon
  * forward 0..511, backward 512..1023; layout in chain_sweep.hip); reset != 0 zeroes them. */
 int mmx_matrix_chain_prof(mmx_matrix m, unsigned long long* out, int reset);
 int mmx_sweep_schedule_info(int n, const int32_t* ia, const int32_t* ja, int level, int fwd, long long* info);
+/* Diagnostics: the chain/band schedule of the numeric factor (chain_factor.hip) for the pattern,
+ * replayed on the host (fails with the reason when invalid).  info[0..7]: ok, bands, slots, ring
+ * slots R, imports (rows), most import slots a band uses, modelled critical path, DAG levels. */
+int mmx_factor_schedule_info(int n, const int32_t* ia, const int32_t* ja, int level, long long* info);
 
 /* Measurement utility (no reference counterpart): the achievable HBM ceiling.  Copies n doubles
  * (n even, device pointers, 16-byte aligned) reps times with a 16-B-per-lane streaming kernel

@@ -567,18 +567,23 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
   const int RI = fri ? atoi(fri) : kFacImpRows;
   F.RI = RI;
   const int impBase = 1 + L * (R + 1) * kFacWU;
-  std::unordered_map<int, int> impOf;  // imported row -> import id (this band)
-  std::vector<int> rows, first, last;  // per import id: row, first and last use
   struct Use {
     size_t cell;
     int id, u;  // import, offset in the row's diagonal + upper part
   };
+  struct BandOut {  // per band: its imports in order, or why it failed
+    std::vector<int> row, free, slot, wait;
+    int slots = 0;
+    bool bad = false;
+  };
+  std::vector<BandOut> out(S.nbands);
+  // bands are independent (disjoint slots of the code arrays; imports per band): in parallel
+#pragma omp parallel for schedule(dynamic, 16)
   for (int b = 0; b < S.nbands; ++b) {
-    impOf.clear();
-    rows.clear();
-    first.clear();
-    last.clear();
+    std::unordered_map<int, int> impOf;  // imported row -> import id (this band)
+    std::vector<int> rows, first, last;  // per import id: row, first and last use
     std::vector<Use> uses;
+    BandOut& bo = out[b];
     for (int l = 0; l < L; ++l) {
       const size_t g = (size_t)b * L + l;
       const int skl = S.laneSkew[g];
@@ -656,8 +661,8 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
         } else {
           sl = (int)slotLast.size();
           if (sl == RI) {
-            F.why = "import slots too few for band " + std::to_string(b);
-            return F;
+            bo.bad = true;
+            break;
           }
           slotLast.push_back(-1);
         }
@@ -667,21 +672,34 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
         busy.push({last[ord[q]], sl});
       }
     }
-    F.maxImpSlots = std::max(F.maxImpSlots, (int)slotLast.size());
+    if (bo.bad) continue;
+    bo.slots = (int)slotLast.size();
     for (const Use& u : uses) {
       const int k = rank[u.id];
       F.code[u.cell] = (uint16_t)(impBase + slotOf[k] * kFacWU + u.u);
       const size_t it = u.cell / ((size_t)kFacNSC * L);
       F.impNeed[it] = std::max(F.impNeed[it], k);
     }
-    F.bandImp[b] = (int)F.impRow.size();
-    F.bandNImp[b] = (int)ord.size();
     for (size_t q = 0; q < ord.size(); ++q) {
-      F.impRow.push_back(rows[ord[q]]);
-      F.impFree.push_back(last[ord[q]]);
-      F.impSlot.push_back(slotOf[q]);
-      F.impWait.push_back(waitOf[q]);
+      bo.row.push_back(rows[ord[q]]);
+      bo.free.push_back(last[ord[q]]);
+      bo.slot.push_back(slotOf[q]);
+      bo.wait.push_back(waitOf[q]);
     }
+  }
+  for (int b = 0; b < S.nbands; ++b) {
+    const BandOut& bo = out[b];
+    if (bo.bad) {
+      F.why = "import slots too few for band " + std::to_string(b);
+      return F;
+    }
+    F.maxImpSlots = std::max(F.maxImpSlots, bo.slots);
+    F.bandImp[b] = (int)F.impRow.size();
+    F.bandNImp[b] = (int)bo.row.size();
+    F.impRow.insert(F.impRow.end(), bo.row.begin(), bo.row.end());
+    F.impFree.insert(F.impFree.end(), bo.free.begin(), bo.free.end());
+    F.impSlot.insert(F.impSlot.end(), bo.slot.begin(), bo.slot.end());
+    F.impWait.insert(F.impWait.end(), bo.wait.begin(), bo.wait.end());
   }
   if (impBase + RI * kFacWU >= 65536) {
     F.why = "LDS indices exceed 16 bits";

@@ -196,8 +196,8 @@ struct SparseMatrix {
   };
   ChainDir chf, chb;
   bool useChain = false;
-  // the numeric factor on the forward chain/band schedule (chain_factor.hip): 2D rows; the level
-  // schedule otherwise or with MMX_FACTOR=level / global
+  // the numeric factor on the forward chain/band schedule (chain_factor.hip, 2D rows) with
+  // MMX_FACTOR=chain; the level schedule otherwise
   struct FactorDir {
     DevBuf<int> bandSlot, bandT, laneLen, laneSkew, bandOrder, bandImp, bandNImp, impPos, impCnt, impSlot, impWait,
         impNeed, meta, rowStart, vsrc;
@@ -379,8 +379,10 @@ struct SparseMatrix {
     }
     useChainFactor = false;
     {
+      // opt-in (MMX_FACTOR=chain): bit-identical, but 30.8 ms against 25.0 ms for the level
+      // schedule at n = 2 M (profiles/r03/lasolver2d_factor.jsonl)
       const char* fm = getenv("MMX_FACTOR");
-      if (useChain && !(fm && (std::strcmp(fm, "level") == 0 || std::strcmp(fm, "global") == 0))) {
+      if (useChain && fm && std::strcmp(fm, "chain") == 0) {
         const FactorSchedule FS = build_factor_schedule(n, iaf, jaf, dg);
         if (FS.ok) {
           upload_factor(FS, dg);
@@ -1076,6 +1078,31 @@ int mmx_sweep_schedule_info(int n, const int32_t* ia, const int32_t* ja, int lev
     if (!bad.empty()) throw Error(MMADMM_ERR_INVALID, "chain schedule invalid: " + bad);
     const long long v[16] = {S.ok ? 1 : 0, S.E, S.R, S.RI, S.nbands, S.nchains, S.maxLen, S.maxSkew,
                              S.maxT, S.slots, S.nImports, S.estIters, nlev, 0, 0, 0};
+    std::memcpy(info, v, sizeof(v));
+  });
+}
+
+int mmx_factor_schedule_info(int n, const int32_t* ia, const int32_t* ja, int level, long long* info) {
+  return guarded([&] {
+    if (n <= 0 || !ia || !ja || level < 0 || !info) throw Error(MMADMM_ERR_INVALID, "bad arguments");
+    std::vector<int> via(ia, ia + n + 1), vja(ja, ja + ia[n]), fia, fja, dgRel;
+    mmx::symbolic_ilu(n, via, vja, level, fia, fja, dgRel);
+    std::vector<int> dg(n);
+    for (int i = 0; i < n; ++i) dg[i] = fia[i] + dgRel[i];
+    const mmx::FactorSchedule F = mmx::build_factor_schedule(n, fia, fja, dg);
+    int nlev = 0;
+    {
+      std::vector<int> lev(n, 0);
+      for (int i = 0; i < n; ++i) {
+        int l = 0;
+        for (int k = fia[i]; k < dg[i]; ++k) l = std::max(l, lev[fja[k]] + 1);
+        lev[i] = l;
+        nlev = std::max(nlev, l + 1);
+      }
+    }
+    const std::string bad = F.ok ? mmx::validate_factor_schedule(F, n, fia, fja, dg) : std::string();
+    if (!bad.empty()) throw Error(MMADMM_ERR_INVALID, "factor schedule invalid: " + bad);
+    const long long v[8] = {F.ok ? 1 : 0, F.geo.nbands, F.slots, F.R, F.nImports, F.maxImpSlots, F.geo.estIters, nlev};
     std::memcpy(info, v, sizeof(v));
   });
 }

@@ -120,3 +120,38 @@ def test_chain_schedule_is_valid(mesh, level, pair, monkeypatch):
         else:
             # the critical path stays close to the dependency DAG's depth
             assert info["estIters"] <= 1.3 * info["levels"] + 64, info
+
+
+@pytest.mark.parametrize("mesh", [("rect", 2, 20), ("rect", 2, 57), ("hexdisc", 30), ("circle", "CircleEx24"),
+                                  ("rect", 3, 4)])
+def test_factor_schedule_is_valid(mesh):
+    """The numeric factor's chain/band schedule (build_factor_schedule) replays correctly on the
+    host: every (entry, pivot) update the reference makes reads U(j_q, col e) from the right ring
+    cell or imported row, written before and not overwritten; no update the reference does not
+    make (validate_factor_schedule).  3D rows exceed the factor's row layout: no schedule."""
+    import ctypes
+    import mmadmm_amd as mx
+    from conftest import circle_mesh
+    if mesh[0] == "rect":
+        m = oracle_py.Mesh.rect(mesh[1], mesh[2])
+        dim, F, nP = mesh[1], m.F, m.nP
+    elif mesh[0] == "hexdisc":
+        md = mx.MeshData.hexdisc(mesh[1], 0.5, 0.5, 0.5)
+        dim, F, nP = 2, md.F, md.nP
+    else:
+        c = circle_mesh(mesh[1])
+        dim, F, nP = 2, c.F, c.Vp.shape[0]
+    ia, ja = L.mesh_pattern(dim, nP, F)
+    L_ = la.lib()
+    L_.mmx_factor_schedule_info.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    ia = np.ascontiguousarray(ia, np.int32)
+    ja = np.ascontiguousarray(ja, np.int32)
+    out = np.zeros(8, np.int64)
+    rc = L_.mmx_factor_schedule_info(len(ia) - 1, ia.ctypes.data, ja.ctypes.data, 0, out.ctypes.data)
+    assert rc == 0
+    info = dict(zip("ok bands slots R imports maxslots estIters levels".split(), out.tolist()))
+    if dim == 3:
+        assert info["ok"] == 0
+    else:
+        assert info["ok"] == 1 and info["maxslots"] <= 384, info
+        assert info["estIters"] <= 1.3 * info["levels"] + 64, info
