@@ -210,8 +210,8 @@ class Engine final : public EngineBase {
       std::vector<int32_t> ord(nl);
       for (int v = 0; v < nl; ++v) ord[v] = v;
       const char* xo = getenv("MMX_XUP_ORDER");  // 3D default: y slabs (C4 x-update 0.174 -> 0.152 ms with the sweep)
-      if ((xo ? atoi(xo) == 1 : true) && D == 3) {
-        // eight slabs across the y axis, one per XCD group of the node order (the x-update's
+      if (xo ? atoi(xo) == 1 : D == 3) {
+        // eight slabs across the y axis (2D: opt-in), one per XCD group of the node order (the x-update's
         // XCD-contiguous blocks), each by first incident simplex: an XCD's share of every z
         // layer is one slab, so its live slot terms are an eighth of a layer
         const int n8 = ((nl + 255) / 256 + 7) / 8 * 256;

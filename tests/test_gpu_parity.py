@@ -289,3 +289,22 @@ def test_xupdate_order_and_sweep_bitwise(order, sweep, monkeypatch):
         np.testing.assert_array_equal(Q.get(f), W.get(f), err_msg=f)
     W.close()
     Q.close()
+
+
+@pytest.mark.parametrize("order,sweep", [(1, 0), (0, 1), (1, 1), (1, 2)])
+def test_xupdate_order_and_sweep_bitwise_2d(order, sweep, monkeypatch):
+    """The 2D x-update (z and u gathered) in the same forms (opt-in in 2D): bit-identical."""
+    m = mx.MeshData.hexdisc(60, 0.5, 0.5, 0.5)
+    M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5)
+    W = mx.Engine(M, 0.055)
+    W.step(10, -1.0)
+    W.step(10, -1.0)
+    monkeypatch.setenv("MMX_XUP_ORDER", str(order))
+    monkeypatch.setenv("MMX_XUP_SWEEP", str(sweep))
+    Q = mx.Engine(M, 0.055)
+    Q.step(10, -1.0)
+    Q.step(10, -1.0)
+    for f in ("x", "z", "u"):
+        np.testing.assert_array_equal(Q.get(f), W.get(f), err_msg=f)
+    W.close()
+    Q.close()
