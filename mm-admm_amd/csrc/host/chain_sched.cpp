@@ -18,6 +18,43 @@ int pow2_at_least(int v) {
   while (r < v) r <<= 1;
   return r;
 }
+// Import slots for imports in order of first use (first[ord[q]] ascending): every one of the RI
+// slots is used once before any is taken again, and then the slot whose last reader passed
+// longest ago is taken (it waits for the compute wave to pass that reader): the importer may run
+// as far ahead as the slots allow, and a band needs at most as many slots as it has imports live
+// at once.  False when RI slots are too few.
+bool assign_import_slots(const std::vector<int>& first, const std::vector<int>& last, const std::vector<int>& ord,
+                         int RI, std::vector<int>& slotOf, std::vector<int>& waitOf, int& used) {
+  typedef std::pair<int, int> P;  // (last use, slot)
+  std::priority_queue<P, std::vector<P>, std::greater<P>> busy;
+  std::queue<int> freed;  // slots whose last reader has passed, in the order they were freed
+  std::vector<int> slotLast;
+  slotOf.assign(ord.size(), 0);
+  waitOf.assign(ord.size(), -1);
+  for (size_t q = 0; q < ord.size(); ++q) {
+    const int f = first[ord[q]];
+    while (!busy.empty() && busy.top().first < f) {
+      freed.push(busy.top().second);
+      busy.pop();
+    }
+    int sl;
+    if ((int)slotLast.size() < RI) {
+      sl = (int)slotLast.size();
+      slotLast.push_back(-1);
+    } else if (!freed.empty()) {
+      sl = freed.front();
+      freed.pop();
+    } else {
+      return false;
+    }
+    slotOf[q] = sl;
+    waitOf[q] = slotLast[sl];
+    slotLast[sl] = last[ord[q]];
+    busy.push({last[ord[q]], sl});
+  }
+  used = (int)slotLast.size();
+  return true;
+}
 }  // namespace
 
 ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std::vector<int>& jaf,
@@ -292,39 +329,13 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
     });
     std::vector<int> rank(rows.size());
     for (size_t q = 0; q < ord.size(); ++q) rank[ord[q]] = (int)q;
-    // import slots by interval colouring in order of first use: an import takes the lowest slot
-    // whose previous import's last use has passed (and waits for the compute wave to pass it), so
-    // the slots needed are the most imports live at once
-    std::vector<int> slotOf(ord.size()), waitOf(ord.size()), slotLast;
-    {
-      typedef std::pair<int, int> P;  // (last use, slot)
-      std::priority_queue<P, std::vector<P>, std::greater<P>> busy;
-      std::priority_queue<int, std::vector<int>, std::greater<int>> freeSlots;
-      for (size_t q = 0; q < ord.size(); ++q) {
-        const int f = first[ord[q]];
-        while (!busy.empty() && busy.top().first < f) {
-          freeSlots.push(busy.top().second);
-          busy.pop();
-        }
-        int sl;
-        if (!freeSlots.empty()) {
-          sl = freeSlots.top();
-          freeSlots.pop();
-        } else {
-          sl = (int)slotLast.size();
-          if (sl == RI) {
-            S.why = "import ring too small for band " + std::to_string(b);
-            return S;
-          }
-          slotLast.push_back(-1);
-        }
-        slotOf[q] = sl;
-        waitOf[q] = slotLast[sl];
-        slotLast[sl] = last[ord[q]];
-        busy.push({last[ord[q]], sl});
-      }
+    std::vector<int> slotOf, waitOf;
+    int used = 0;
+    if (!assign_import_slots(first, last, ord, RI, slotOf, waitOf, used)) {
+      S.why = "import ring too small for band " + std::to_string(b);
+      return S;
     }
-    S.maxImpSlots = std::max(S.maxImpSlots, (int)slotLast.size());
+    S.maxImpSlots = std::max(S.maxImpSlots, used);
     for (const Use& u : impUses) {
       const int k = rank[impOf[u.row]];
       S.code[u.slot] = -(slotOf[k] + 1);
@@ -638,42 +649,16 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
         }
       }
     }
-    // imports in order of first use, slots by interval colouring (as build_chain_schedule)
+    // imports in order of first use, slots as in build_chain_schedule
     std::vector<int> ord(rows.size());
     for (size_t q = 0; q < ord.size(); ++q) ord[q] = (int)q;
     std::sort(ord.begin(), ord.end(), [&](int a, int c) { return first[a] != first[c] ? first[a] < first[c] : rows[a] < rows[c]; });
-    std::vector<int> rank(rows.size()), slotOf(ord.size()), waitOf(ord.size()), slotLast;
+    std::vector<int> rank(rows.size()), slotOf, waitOf;
     for (size_t q = 0; q < ord.size(); ++q) rank[ord[q]] = (int)q;
-    {
-      typedef std::pair<int, int> P;
-      std::priority_queue<P, std::vector<P>, std::greater<P>> busy;
-      std::priority_queue<int, std::vector<int>, std::greater<int>> freeSlots;
-      for (size_t q = 0; q < ord.size(); ++q) {
-        const int f = first[ord[q]];
-        while (!busy.empty() && busy.top().first < f) {
-          freeSlots.push(busy.top().second);
-          busy.pop();
-        }
-        int sl;
-        if (!freeSlots.empty()) {
-          sl = freeSlots.top();
-          freeSlots.pop();
-        } else {
-          sl = (int)slotLast.size();
-          if (sl == RI) {
-            bo.bad = true;
-            break;
-          }
-          slotLast.push_back(-1);
-        }
-        slotOf[q] = sl;
-        waitOf[q] = slotLast[sl];
-        slotLast[sl] = last[ord[q]];
-        busy.push({last[ord[q]], sl});
-      }
-    }
+    int used = 0;
+    bo.bad = !assign_import_slots(first, last, ord, RI, slotOf, waitOf, used);
     if (bo.bad) continue;
-    bo.slots = (int)slotLast.size();
+    bo.slots = used;
     for (const Use& u : uses) {
       const int k = rank[u.id];
       F.code[u.cell] = (uint16_t)(impBase + slotOf[k] * kFacWU + u.u);

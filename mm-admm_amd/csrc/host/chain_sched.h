@@ -14,9 +14,10 @@
 //     chain, the second taking the first's value from the register (its entry's code is the cell
 //     after the import slots, never read); the lane's ring holds R rows, R / 2 positions;
 //   * imports: values from other bands (or too old for the ring) are copied from the global
-//     granules into LDS import slots by a helper wavefront, in order of first use (slots assigned
-//     by interval colouring: the slot whose previous import's last use has passed); it publishes
-//     how many it has delivered, and iteration t waits for impNeed[t] (the highest it reads).
+//     granules into LDS import slots by a helper wavefront, in order of first use (every slot
+//     once, then the slot whose previous import's last reader passed longest ago, delivered once
+//     the compute wave has passed that reader); it publishes how many it has delivered, and
+//     iteration t waits for impNeed[t] (the highest it reads).
 // Entries address one LDS array: [0] = +0.0 (pads: value 0 times +0.0 changes nothing, not even
 // the sign of a zero), [1, 1 + 64 (R+1)) the lane rings, then RI import slots.
 // Every row is computed by exactly the arithmetic of the level sweep (same entries, same order).

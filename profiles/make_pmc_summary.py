@@ -6,8 +6,11 @@ coalesced streaming reads (MI355X_MICROARCH.md §HBM); `hbm_bytes_per_launch` ap
 fetch side (the prox kernel's bulk read, Bkinv, is such a stream), `hbm_bytes_raw_per_launch` does
 not.  Other access widths are uncalibrated, so the truth lies between the two for mixed kernels.
 
-  python profiles/make_pmc_summary.py profiles/r01/pmc/fetch_size_counter_collection.csv \
-         profiles/r01/pmc/write_size_counter_collection.csv [profiles/r01/pmc/f64_counter_collection.csv]
+  python profiles/make_pmc_summary.py profiles/r03/pmc/fetch_counter_collection.csv.gz \
+         profiles/r03/pmc/write_counter_collection.csv.gz [profiles/r03/pmc/f64_counter_collection.csv.gz]
+
+(round 3: each pass is its own rocprofv3 run of `bench.py --steps 5 --warmup 1 --no-cpu-baseline`,
+dev/gpu_final_b.sh; the summary holds only the kernels those runs launched)
 
 The optional third pass (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, wave instructions) gives
 `fp64_flops_per_launch` = 64 lanes x (ADD + MUL + 2 FMA + TRANS): executed fp64 work, including
@@ -15,16 +18,23 @@ the correctly rounded powers' double-double arithmetic.
 """
 import collections
 import csv
+import gzip
 import json
 import os
 import re
 import sys
 
 
+def _open(path):
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+
+
 def load(path):
-    d = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    """kernel -> grid size -> counter values (a kernel launched at several sizes, e.g. the 2D prox
+    at C3 and at C2, is summarised per size)"""
+    d = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(_open(path)):
+        d[r["Kernel_Name"]][int(r["Grid_Size"])].append(float(r["Counter_Value"]))
     return d
 
 
@@ -35,11 +45,10 @@ def short(name):
 
 def load_f64(path):
     d = collections.defaultdict(lambda: collections.defaultdict(list))
-    for r in csv.DictReader(open(path)):
-        d[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for r in csv.DictReader(_open(path)):
+        d[(r["Kernel_Name"], int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for k, c in d.items():
-        n = max(len(v) for v in c.values())
         mean = {name: sum(v) / len(v) for name, v in c.items()}
         out[k] = round(64 * (mean.get("SQ_INSTS_VALU_ADD_F64", 0) + mean.get("SQ_INSTS_VALU_MUL_F64", 0) +
                              2 * mean.get("SQ_INSTS_VALU_FMA_F64", 0) + mean.get("SQ_INSTS_VALU_TRANS_F64", 0)))
@@ -49,17 +58,28 @@ def load_f64(path):
 def main(fetch, write, f64=None):
     f, w = load(fetch), load(write)
     fl = load_f64(f64) if f64 else {}
-    out = {"source": [os.path.relpath(p) for p in (fetch, write, f64) if p], "units": "bytes per launch"}
+    out = {"source": [os.path.relpath(p) for p in (fetch, write, f64) if p], "units": "bytes per launch",
+           "note": "per kernel: the launches of its largest grid (the headline-size workload); other grid "
+                   "sizes under by_grid"}
+
+    def entry(k, g):
+        fk = sum(f[k][g]) / len(f[k][g])
+        wl = w.get(k, {}).get(g, [])
+        wk = sum(wl) / max(len(wl), 1)
+        e = {"grid_size": g, "launches": len(f[k][g]), "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
+             "hbm_bytes_per_launch": round((2 * fk + wk) * 1024), "hbm_bytes_raw_per_launch": round((fk + wk) * 1024)}
+        if (k, g) in fl:
+            e["fp64_flops_per_launch"] = fl[(k, g)]
+        return e
+
     for k in f:
         if not k.startswith(("void mmx::", "mmx::")):
             continue
-        fk = sum(f[k]) / len(f[k])
-        wk = sum(w.get(k, [0.0])) / max(len(w.get(k, [])), 1)
-        out[short(k)] = {"launches": len(f[k]), "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
-                         "hbm_bytes_per_launch": round((2 * fk + wk) * 1024),
-                         "hbm_bytes_raw_per_launch": round((fk + wk) * 1024)}
-        if k in fl:
-            out[short(k)]["fp64_flops_per_launch"] = fl[k]
+        grids = sorted(f[k], reverse=True)
+        e = entry(k, grids[0])
+        if len(grids) > 1:
+            e["by_grid"] = {str(g): entry(k, g) for g in grids[1:]}
+        out[short(k)] = e
     here = os.path.dirname(os.path.abspath(__file__))
     with open(os.path.join(here, "pmc_summary.json"), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
