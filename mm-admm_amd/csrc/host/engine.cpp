@@ -891,6 +891,8 @@ class Engine final : public EngineBase {
     {
       const char* xs = getenv("MMX_XUP_SWEEP");  // 3D default: one workgroup per CU (profiles/r03/xupdate)
       m.xupSweep = xs ? std::max(0, atoi(xs)) : (D == 3 ? 1 : 0);
+      const char* xc = getenv("MMX_XUP_CH");
+      m.xupCh = xc ? atoi(xc) : 8;
     }
     {
       const char* ft = getenv("MMX_FORCE_TIE");

@@ -27,6 +27,7 @@ struct DeviceMesh {
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
   unsigned* tieStale;
+  int xupCh;              // slots requested at once per node in the sweep (8, 16, 24)
   int xupSweep;           // 3D slot-term x-update as a per-XCD sweep: workgroups per CU (0: one node per lane)     // the previous steady prox's counter, cleared by this prox's recomputation
   int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
   const int* nodeOrder;   // x-update processing order (nodes by first incident simplex) or nullptr

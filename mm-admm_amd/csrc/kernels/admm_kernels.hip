@@ -227,12 +227,11 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
 // A node's incident slots are taken 8 at a time: their offsets, then all their z and u values
 // are requested before the first is added (branch-free: lanes past the end re-read the last
 // slot, a slot of another rank reads its gathered row), then summed in ascending order.
-template <int D, bool RESID, bool TS>
+template <int D, bool RESID, bool TS, int CH = 8>
 __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepScalars& sc,
                                              const double* __restrict__ xBar, const double* __restrict__ z,
                                              const double* __restrict__ u, double* __restrict__ x, int idx,
                                              double (&pv)[3]) {
-  constexpr int CH = 8;
   {
     // processing order: nodes by first incident simplex, so a workgroup's nodes share simplices
     const int v = m.nodeOrder ? m.nodeOrder[idx] : idx;
@@ -328,7 +327,9 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
 // The slot-term x-update (no residual) as a sweep: XCD c (= blockIdx % 8) takes the node-order
 // positions [c n8, (c + 1) n8) and its gridDim / 8 workgroups walk them in rounds, so the slot
 // terms a round gathers are mostly still in that XCD's L2 for the neighbouring rounds.
-template <int D, bool TS>
+// CH: incident slots requested at once per node (3D slot terms: 24 covers a grid vertex's
+// tetrahedra in one batch)
+template <int D, bool TS, int CH>
 __global__ void __launch_bounds__(kBlock) k_xupdate_sweep(DeviceMesh<D> m, StepScalars sc,
                                                            const double* __restrict__ xBar,
                                                            const double* __restrict__ z, const double* __restrict__ u,
@@ -337,7 +338,7 @@ __global__ void __launch_bounds__(kBlock) k_xupdate_sweep(DeviceMesh<D> m, StepS
   const int lo = c * n8, hi = min(lo + n8, m.nP);
   double pv[3];
   for (int idx = lo + w * kBlock + (int)threadIdx.x; idx < hi; idx += per * kBlock)
-    xupdate_node<D, false, TS>(m, sc, xBar, z, u, x, idx, pv);
+    xupdate_node<D, false, TS, CH>(m, sc, xBar, z, u, x, idx, pv);
 }
 
 // k x k inverse: unblocked partial-pivot LU + substitution (mirrors the oracle's restatement
@@ -1971,10 +1972,15 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   const bool ts = useTslot && m.tslot;
   if (!resid && m.xupSweep > 0) {  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU
     const int n8 = ((m.nP + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
-    if (ts)
-      hipLaunchKernelGGL((k_xupdate_sweep<D, true>), dim3(256 * m.xupSweep), dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+    const dim3 g(256 * m.xupSweep);
+    if (ts && m.xupCh >= 24)
+      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 24>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+    else if (ts && m.xupCh >= 16)
+      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 16>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+    else if (ts)
+      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 8>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
     else
-      hipLaunchKernelGGL((k_xupdate_sweep<D, false>), dim3(256 * m.xupSweep), dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+      hipLaunchKernelGGL((k_xupdate_sweep<D, false, 8>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
     return;
   }
 #define MMX_XU(R, T)                                                                                               \

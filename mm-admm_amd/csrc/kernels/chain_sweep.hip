@@ -231,6 +231,21 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       // first and served first, says the stage has landed) -- then the chain
       int seen = 0;  // import count read by the previous batch
       double carry = 0.0;  // SEG: the partial sum of a row whose next segment comes at the next position
+#ifdef MMX_CHAIN_FINE
+      // probe (dev builds only): cycles of the step's segments, each closed by a full wait
+      unsigned long long fq[5] = {0, 0, 0, 0, 0};
+#define MMX_FINE_MARK(k)                                     \
+  do {                                                       \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    const unsigned long long _c = clk();                     \
+    fq[k] += _c - fqt;                                       \
+    fqt = _c;                                                \
+  } while (0)
+#else
+#define MMX_FINE_MARK(k) \
+  do {                   \
+  } while (0)
+#endif
       auto step = [&](int t, const Fetched& f, Fetched& nx) {
         const int need = __builtin_amdgcn_readfirstlane(f.need);
         if (need >= 0 && seen <= need) {  // imports this iteration reads: wait for their delivery
@@ -241,6 +256,9 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           if (ca.profIter) cimp += clk() - i0;
           if (!ok) return;
         }
+#ifdef MMX_CHAIN_FINE
+        unsigned long long fqt = clk();
+#endif
         double v[EE];
 #pragma unroll
         for (int g = 0; g < G; ++g)
@@ -250,12 +268,14 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 #pragma unroll
               for (int q = 0; q < 4; ++q) v[g * E + e0 + q] = s_dep[f.c[g * E + e0 + q]];
             }
+        MMX_FINE_MARK(0);
         const bool hasNext = t + 1 < T;
         const int stn = (t + 1) & (DL - 1);
         const int tagN = __hip_atomic_load(&s_tag[stn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int doneN = __hip_atomic_load(&s_impDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         asm volatile("" ::: "memory");  // keep the stage reads behind the tag read (LDS serves them in order)
         if (hasNext) load_stage(stn, nx);
+        MMX_FINE_MARK(1);
         const int p = t - skew;
         double prev = 0.0;  // G = 2: the pair's first row
 #pragma unroll
@@ -284,6 +304,10 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
               carry = acc;  // the row goes on at the next position
             } else {
               if (!FWD) acc = acc / f.diag[g];
+#ifdef MMX_CHAIN_FINE
+              asm volatile("" ::"v"(acc));
+              MMX_FINE_MARK(2);
+#endif
               s_dep[1 + lane * (R + 1) + (((G == 2) ? ri : p) & (R - 1))] = acc;
               const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
               __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
@@ -297,8 +321,10 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           }
         }
         if (lane == 0) lds_write(&s_prog, t + 1);
+        MMX_FINE_MARK(3);
         seen = doneN;
         if (hasNext && __builtin_amdgcn_readfirstlane(tagN) != t + 1) fetch(t + 1, nx);  // not landed yet
+        MMX_FINE_MARK(4);
       };
       Fetched fa, fb;
       if (T > 0) fetch(0, fa);
@@ -314,6 +340,9 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
         prof_add(ca.prof, 2, cimp);
         prof_add(ca.prof, 3, (unsigned long long)T);
         prof_add(ca.prof, 8, 1ull);
+#ifdef MMX_CHAIN_FINE
+        for (int k = 0; k < 5; ++k) prof_add(ca.prof, 9 + k, fq[k]);
+#endif
         const int pi = b < 32 ? b : (b >= ca.nbands - 32 ? 64 + b - ca.nbands : -1);
         if (pi >= 0) {
           prof_add(ca.prof, 16 + 4 * pi, tot);

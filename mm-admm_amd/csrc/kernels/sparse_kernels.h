@@ -8,8 +8,14 @@
 namespace mmx {
 
 // Products staged in LDS per SpMV workgroup (16 KB of fp64).
-constexpr int kSpmvTile = 2048;
-constexpr int kSpmvBlock = 256;
+#ifndef MMX_SPMV_TILE
+#define MMX_SPMV_TILE 2048
+#endif
+#ifndef MMX_SPMV_BLOCK
+#define MMX_SPMV_BLOCK 256
+#endif
+constexpr int kSpmvTile = MMX_SPMV_TILE;
+constexpr int kSpmvBlock = MMX_SPMV_BLOCK;
 // Rows per chunk of the level-scheduled factor/sweeps (one wavefront per chunk) and the size of
 // their persistent grid (wavefronts).
 constexpr int kSweepRows = 64;
