@@ -36,9 +36,6 @@ constexpr int kImpMax = 2048;   // = kChainImpMax
 #endif
 constexpr int kImpQ = MMX_IMP_Q;  // imports each importer lane polls per round
 constexpr unsigned kChainSpinMax = 1u << 22;
-#ifndef MMX_GRANULE16
-#define MMX_GRANULE16 0
-#endif
 
 template <typename T>
 __device__ __forceinline__ unsigned lds_off(T* p) {
@@ -313,20 +310,10 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 #endif
               s_dep[1 + lane * (R + 1) + (((G == 2) ? ri : p) & (R - 1))] = acc;
               const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
-#if MMX_GRANULE16
-              // the granule as one 16-byte store {lo, epoch, hi, epoch}: each 8-byte half (its tag
-              // with it) is single-copy atomic, which is all the importers' check relies on
-              {
-                typedef unsigned u4v __attribute__((ext_vector_type(4)));
-                const u4v gv = {(unsigned)(bits & 0xffffffffull), epoch, (unsigned)(bits >> 32), epoch};
-                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(gout + 2 * (size_t)row), "v"(gv) : "memory");
-              }
-#else
               __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
               __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-#endif
               if (!FWD) out[row] = acc;
               if (FWD && PRO != 0) pvec[row] = f.init[g];
               prev = acc;
