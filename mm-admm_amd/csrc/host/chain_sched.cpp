@@ -705,6 +705,20 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
       }
   }
   F.nImports = (long long)F.impRow.size();
+  // rows some band imports publish their diagonal + upper part as global granules (bit 17 of
+  // meta); the others are read through the lane rings only and skip those stores
+  {
+    std::vector<char> exported(n, 0);
+    for (int j : F.impRow) exported[j] = 1;
+    for (int b = 0; b < S.nbands; ++b)
+      for (int l = 0; l < L; ++l) {
+        const size_t g = (size_t)b * L + l;
+        for (int p = 0; p < S.laneLen[g]; ++p) {
+          const int i = S.laneStart[g] + p;
+          if (exported[i]) F.meta[((size_t)S.bandSlot[b] + p + S.laneSkew[g]) * L + l] |= 1 << 17;
+        }
+      }
+  }
   F.ok = true;
   return F;
 }
@@ -782,7 +796,7 @@ std::string validate_factor_schedule(const FactorSchedule& F, int n, const std::
     const int b = bandOf[i], l = laneOf[i], t = iterOf[i];
     const size_t slot = (size_t)S.bandSlot[b] + t;
     const int kb = iaf[i], W = iaf[i + 1] - kb, nl = dg[i] - kb;
-    if (F.meta[slot * L + l] != (W | (nl << 8) | (1 << 16))) return "row metadata";
+    if ((F.meta[slot * L + l] & 0x1FFFF) != (W | (nl << 8) | (1 << 16))) return "row metadata";
     for (int e = 0; e < kFacWF; ++e)
       if (F.vsrc[fac_vidx(slot, e, l)] != (e < W ? kb + e : -1)) return "row values";
     for (int q = 0; q < kFacNL; ++q) {

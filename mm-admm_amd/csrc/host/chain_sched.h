@@ -99,7 +99,8 @@ struct FactorSchedule {
   long long slots = 0;
   std::vector<uint16_t> code;      // [slot][kFacNSC][lane]: LDS index of each (e, q) value / pivot (0: none)
   std::vector<int> vsrc;           // [slot][kFacWF][lane]: factor position of the row's entry e (-1: pad)
-  std::vector<int> meta;           // [slot][lane]: W | nlow << 8 | 1 << 16 for a row, 0 idle
+  std::vector<int> meta;           // [slot][lane]: W | nlow << 8 | 1 << 16 for a row (| 1 << 17 when
+                                   // another band imports it: it publishes granules), 0 idle
   std::vector<int> rowStart;       // [slot][lane]: factor position of the row's first entry
   // imports are whole rows (their diagonal + upper part, kFacWU cells per slot), otherwise as in
   // ChainSchedule

@@ -476,7 +476,7 @@ struct SparseMatrix {
     MMX_HIP(hipMemsetAsync(c.gU.p, 0, c.gU.n * sizeof(uint64_t), st));
     c.args = FactorArgs{c.bandSlot.p, c.bandT.p, c.laneLen.p, c.laneSkew.p, c.bandOrder.p, c.bandImp.p, c.bandNImp.p,
                         c.impPos.p, c.impCnt.p, c.impSlot.p, c.impWait.p, c.impNeed.p, c.val.p, c.code.p, c.meta.p,
-                        c.rowStart.p, S.nbands, F.R};
+                        c.rowStart.p, S.nbands, F.R, d_cprof.p ? d_cprof.p + 480 : nullptr};
   }
 
   void begin(int t) {

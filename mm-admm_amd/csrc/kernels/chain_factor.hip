@@ -63,6 +63,7 @@ __device__ __forceinline__ void wait_vm() {
 __device__ __forceinline__ double join_words(uint32_t lo, uint32_t hi) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+__device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_memtime(); }
 __device__ __forceinline__ bool aborted(unsigned* err) {
   return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
@@ -113,12 +114,16 @@ __global__ void __launch_bounds__(256) k_chain_factor(FactorArgs fa, double* __r
       wait_vm<0>();
       bool ok = true;
       int seen = 0;
+      const unsigned long long c0 = fa.prof ? clk() : 0;
+      unsigned long long cst = 0, cim = 0;
       for (int t = 0; t < T && ok; ++t) {
         const int st = t & (DL - 1);
         {  // the stage
           unsigned spins = 0;
+          const unsigned long long w0 = fa.prof ? clk() : 0;
           while (lds_read(&s_tag[st]) != t)
             if (!(ok = spin(spins, err, 8u))) break;
+          if (fa.prof) cst += clk() - w0;
           if (!ok) break;
         }
         const int* sm = s_meta + st * 3 * 64;
@@ -126,8 +131,10 @@ __global__ void __launch_bounds__(256) k_chain_factor(FactorArgs fa, double* __r
         const int need = __builtin_amdgcn_readfirstlane(sm[128 + lane]);
         if (need >= 0 && seen <= need) {  // imports this iteration reads
           unsigned spins = 0;
+          const unsigned long long i0 = fa.prof ? clk() : 0;
           while ((seen = lds_read(&s_impDone)) <= need)
             if (!(ok = spin(spins, err, 16u))) break;
+          if (fa.prof) cim += clk() - i0;
           if (!ok) break;
         }
         const int p = t - skew;
@@ -153,19 +160,25 @@ __global__ void __launch_bounds__(256) k_chain_factor(FactorArgs fa, double* __r
               cd[c * 8 + 2 * k + 1] = (uint16_t)(w4[k] >> 16);
             }
           }
+          // every gather issued before the arithmetic, in one batch (one wait instead of one per
+          // value), and the updates branch-free: an absent update (code 0) reads the zero cell and
+          // its result is discarded by a select, so no sum sees it
+          double piv[kNL], uv[kNUpd];
+#pragma unroll
+          for (int q = 0; q < kNL; ++q) piv[q] = s_dep[cd[kNUpd + q]];
+#pragma unroll
+          for (int k = 0; k < kNUpd; ++k) uv[k] = s_dep[cd[k]];
           double m[kNL], res[kWF];
 #pragma unroll
           for (int e = 0; e < kWF; ++e) {
             double acc = a[e];
 #pragma unroll
             for (int q = 0; q < (e < kNL ? e : kNL); ++q) {
-              const int c = cd[fslot(e, q)];
-              const double u = s_dep[c];
-              acc = c ? acc - m[q] * u : acc;
+              const double t = acc - m[q] * uv[fslot(e, q)];
+              acc = (cd[fslot(e, q)] != 0) ? t : acc;
             }
             if (e < kNL) {
-              const double piv = s_dep[cd[kNUpd + e]];
-              m[e] = acc / piv;  // used only when e is a lower entry (e < nlow)
+              m[e] = acc / piv[e];  // used only when e is a lower entry (e < nlow)
               res[e] = (e < nlow) ? m[e] : acc;
             } else {
               res[e] = acc;
@@ -174,12 +187,14 @@ __global__ void __launch_bounds__(256) k_chain_factor(FactorArgs fa, double* __r
           // the row: all entries to af; the diagonal + upper part to the ring and the granules
           const int rs = 1 + (lane * (R + 1) + (p & (R - 1))) * kWU;
           const uint64_t tag = (uint64_t)epoch << 32;
+          const bool exported = (meta >> 17) & 1;  // some band imports this row
 #pragma unroll
           for (int e = 0; e < kWF; ++e)
             if (e < W) {
               af[kb + e] = res[e];
               if (e >= nlow) {
                 s_dep[rs + e - nlow] = res[e];
+                if (!exported) continue;
                 const uint64_t bits = (uint64_t)__double_as_longlong(res[e]);
                 __hip_atomic_store(gU + 2 * (size_t)(kb + e), tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -191,6 +206,20 @@ __global__ void __launch_bounds__(256) k_chain_factor(FactorArgs fa, double* __r
         if (lane == 0) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           lds_write(&s_prog, t + 1);
+        }
+      }
+      if (fa.prof && lane == 0) {
+        const unsigned long long tot = clk() - c0;
+        atomicAdd(fa.prof + 0, tot);
+        atomicAdd(fa.prof + 1, cst);
+        atomicAdd(fa.prof + 2, cim);
+        atomicAdd(fa.prof + 3, (unsigned long long)T);
+        atomicAdd(fa.prof + 4, 1ull);
+        if (b < 16) {  // the first bands (2D: the grid-line bands, the critical path)
+          atomicAdd(fa.prof + 320 + 4 * b, tot);
+          atomicAdd(fa.prof + 321 + 4 * b, cst);
+          atomicAdd(fa.prof + 322 + 4 * b, cim);
+          atomicAdd(fa.prof + 323 + 4 * b, (unsigned long long)T);
         }
       }
     } else if (wave <= 2) {
@@ -235,6 +264,7 @@ __global__ void __launch_bounds__(256) k_chain_factor(FactorArgs fa, double* __r
       // lane l delivers imports l, l + 64, ...: each the diagonal + upper part of one row (up to
       // kWU granules); the published count is the lowest import still pending over the lanes
       const int ib = fa.bandImp[b], ni = fa.bandNImp[b];
+      const unsigned long long m0 = fa.prof ? clk() : 0;
       int k = lane, published = 0;
       unsigned spins = 0;
       while (ni > 0) {
@@ -280,6 +310,7 @@ __global__ void __launch_bounds__(256) k_chain_factor(FactorArgs fa, double* __r
           break;
         }
       }
+      if (fa.prof && lane == 0) atomicAdd(fa.prof + 5, clk() - m0);
     }
     __syncthreads();
   }

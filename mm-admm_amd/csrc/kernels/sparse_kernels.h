@@ -118,6 +118,8 @@ struct FactorArgs {
   const int* meta;      // [slot][64] W | nlow << 8 | 1 << 16
   const int* rowStart;  // [slot][64] factor position of the row's first entry
   int nbands, R;
+  unsigned long long* prof;  // optional cycle counters (MMX_CHAIN_PROF): 0 compute total, 1 stage
+                             // waits, 2 import waits, 3 iterations, 4 bands, 5 importer cycles
 };
 void launch_chain_factor(const FactorArgs& fa, double* af, uint64_t* gU, unsigned epoch, unsigned* ticket,
                          unsigned* err, hipStream_t st);
