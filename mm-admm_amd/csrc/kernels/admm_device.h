@@ -136,6 +136,9 @@ __device__ __forceinline__ int findLimInf(double w, double m0, int size, double 
   return (int)guess;
 }
 
+#ifndef MMX_MON_BATCH
+#define MMX_MON_BATCH 1
+#endif
 // MeshInterpolator<D>::evalMonitorOnGrid (src/MeshInterpolator.cpp:287-342)
 template <int D>
 __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* pnt, M<D>& mv) {
@@ -174,10 +177,29 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
                             base + P, base + P + 1, base + P + nx + 1, base + P + nx + 2};
     // rows read from the 10-double padded copy: 5 16-byte loads per row instead of 9 8-byte ones
-    // (the same values; the sums below are unchanged)
+    // (the same values; the sums below are unchanged).  All eight rows are requested before the
+    // first is used: loaded row by row, the compiler waited for each corner before requesting the
+    // next (eight dependent cache round trips per vertex)
     double f[9];
 #pragma unroll
     for (int n = 0; n < 9; ++n) f[n] = 0.0;
+#if MMX_MON_BATCH
+    double r[8][10];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double2* rp = reinterpret_cast<const double2*>(g.pad + rows[q] * 10);
+#pragma unroll
+      for (int e = 0; e < 5; ++e) {
+        const double2 v = rp[e];
+        r[q][2 * e] = v.x;
+        r[q][2 * e + 1] = v.y;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int n = 0; n < 9; ++n) f[n] += c[q] * r[q][n];
+#else
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const double2* rp = reinterpret_cast<const double2*>(g.pad + rows[q] * 10);
@@ -191,6 +213,7 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
 #pragma unroll
       for (int n = 0; n < 9; ++n) f[n] += c[q] * r[n];
     }
+#endif
 #pragma unroll
     for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = f[n];
   }

@@ -402,6 +402,7 @@ struct RegB {
   static constexpr bool kCarry = false;
   static constexpr bool kRolled = false;
   static constexpr int kPipe = 0;
+  static constexpr bool kPre = false;
   double* b;
   __device__ __forceinline__ double get(int i, int j) const { return b[i * K + j]; }
   __device__ __forceinline__ double heldRow(int, int) const { return 0.0; }
@@ -419,6 +420,7 @@ struct LdsB {
   static constexpr bool kCarry = false;
   static constexpr bool kRolled = true;  // the update pass one row per trip (code size; 2D: same speed)
   static constexpr int kPipe = 0;
+  static constexpr bool kPre = false;
   double* base;  // &lds[tid], entries strided by STRIDE
   __device__ __forceinline__ double get(int i, int j) const { return base[(i * K + j) * STRIDE]; }
   __device__ __forceinline__ double heldRow(int, int) const { return 0.0; }
@@ -446,6 +448,9 @@ typedef __attribute__((address_space(3))) double ldouble;
 // access to one entry is 512 contiguous bytes).  Double-buffered across proxes: the first BFGS
 // iteration reads the previous prox's buffer `rd` and writes `wr`, later iterations work in `wr`,
 // so `rd` stays intact for an exact recomputation of the block.
+#ifndef MMX_WAVE_DMA
+#define MMX_WAVE_DMA 1
+#endif
 template <int K>
 struct WaveB {
   static constexpr bool kRowFence = true;
@@ -453,6 +458,9 @@ struct WaveB {
   static constexpr int kPipe = MMX_ROW_PIPE;
   static constexpr int kHeld = MMX_WAVE_HELD;  // rows kept in LDS from pass 1 to passes 2 and 3
   static constexpr bool kCarry = MMX_WAVE_CARRY;
+  // the held rows of the entry matrix DMA'd into LDS at the start of the block (prox_wave_block),
+  // so the first pass 1 reads them from there
+  static constexpr bool kPre = MMX_WAVE_DMA && kHeld > 0;
   const gdouble* rd;
   gdouble* wr;
   ldouble* held;  // &lds[lane], kHeld rows, entries strided by 64
@@ -607,14 +615,16 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     // (the next pass starts without waiting for their loads)
     constexpr bool kCarry = BA::kCarry && kPipe > 0;
     double rc[kPipe > 0 ? kPipe : 1][K];
-    start_rows<K, kPipe>(B, rn);
+    // kPre: the first iteration's held rows are in LDS already (DMA'd at the start of the block)
+    const bool pre = BA::kPre && iter == 0;
+    start_rows<K, kPipe>(B, rn, pre ? BA::kHeld : 0);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
       double row[K];
-      next_row<K, kPipe>(B, i, row, rn);
+      next_row<K, kPipe>(B, i, row, rn, pre);
       if constexpr (BA::kHeld > 0) {  // the first kHeld rows wait in LDS for passes 2 and 3
-        if (i < BA::kHeld)
+        if (!pre && i < BA::kHeld)
 #pragma unroll
           for (int j = 0; j < K; ++j) B.holdRow(i, j, row[j]);
       }
@@ -905,6 +915,9 @@ __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, co
 // meets a near-midpoint power the whole block writes nothing back and is queued for k_prox_fix,
 // which recomputes it exactly from the untouched inputs.
 typedef double v2nt __attribute__((ext_vector_type(2)));
+#ifndef MMX_LDS_STAGE
+#define MMX_LDS_STAGE 1
+#endif
 template <int D, int BS>
 __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                         double* __restrict__ zg, double* __restrict__ ug,
@@ -938,17 +951,26 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   }
   double* chunk = Bg + (size_t)s0 * KK;
   const int tot = nIn * KK;  // even: K*K is even
+  // the chunk is read once and written once: nontemporal (C3 prox 0.412 -> 0.399 ms)
+  constexpr int NL = KK / 2;  // 16-byte loads per lane of a full chunk
+  v2nt cv[MMX_LDS_STAGE ? NL : 1];
+  if constexpr (MMX_LDS_STAGE) {
+    // every load of the chunk in flight at once (a short last chunk re-reads its last pair: no
+    // branch, so the wait for the vertex indices below is counted exactly), the lane's gathers
+    // behind them, then the LDS image (a loop writing each load's pair to LDS waits for it before
+    // requesting the next)
+#pragma unroll
+    for (int r = 0; r < NL; ++r)
+      cv[r] = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(chunk + min(2 * (tid + r * BS), tot - 2)));
+  } else {
 #pragma unroll 4
-  for (int e = tid * 2; e < tot; e += BS * 2) {
-    // the chunk is read once and written once: nontemporal (C3 prox 0.412 -> 0.399 ms)
-    const v2nt vv = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(chunk + e));
-    double2 v;
-    v.x = vv.x;
-    v.y = vv.y;
-    const int sa = e / KK, ka = e - sa * KK;
-    const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
-    lds[ka * (BS + 1) + sa] = v.x;
-    lds[kb * (BS + 1) + sb] = v.y;
+    for (int e = tid * 2; e < tot; e += BS * 2) {
+      const v2nt vv = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(chunk + e));
+      const int sa = e / KK, ka = e - sa * KK;
+      const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
+      lds[ka * (BS + 1) + sa] = vv.x;
+      lds[kb * (BS + 1) + sb] = vv.y;
+    }
   }
   double xi[K];
   loadXi<D>(m, f, xi);
@@ -957,6 +979,18 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     gatherX<D>(x, f, dxv);
 #pragma unroll
     for (int i = 0; i < K; ++i) dx[i] = dxv[i] + dx[i];  // DXpU = D x + uBar
+  }
+  if constexpr (MMX_LDS_STAGE) {
+#pragma unroll
+    for (int r = 0; r < NL; ++r) {
+      const int e = 2 * (tid + r * BS);
+      const int sa = e / KK, ka = e - sa * KK;
+      const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
+      if (e < tot) {
+        lds[ka * (BS + 1) + sa] = cv[r].x;
+        lds[kb * (BS + 1) + sb] = cv[r].y;
+      }
+    }
   }
   __syncthreads();
   double pv[6] = {0, 0, 0, 0, 0, 0};
@@ -1063,6 +1097,20 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     gatherX<D>(x, f, dxv);
 #pragma unroll
     for (int i = 0; i < K; ++i) dx[i] = dxv[i] + dx[i];  // DXpU = D x + uBar
+    if constexpr (WaveB<K>::kPre) {
+      __builtin_amdgcn_sched_barrier(0);  // (not hoisted above the gathers' wait)
+      // the held rows of the block's matrix (contiguous in the wave-interleaved layout, and in
+      // the same order in ldsHeld) straight into LDS, 1 KB per instruction, requested once the
+      // lane's inputs are in (the wait for the gathers, requested before the DMA, would otherwise
+      // exceed the 63 loads vmcnt tracks and wait for the DMA too); the first pass 1 finds them
+      // there
+      const char* src = reinterpret_cast<const char*>(Bin + (size_t)lb * KK * 64) + tid * 16;
+      char* dst = reinterpret_cast<char*>(ldsHeld);
+#pragma unroll
+      for (int c = 0; c < WaveB<K>::kHeld * K * 64 * 8 / 1024; ++c)
+        __builtin_amdgcn_global_load_lds(src + c * 1024, (__attribute__((address_space(3))) void*)(dst + c * 1024),
+                                         16, 0, 0);
+    }
   }
   double pv[6] = {0, 0, 0, 0, 0, 0};
   bool tie = false;
@@ -1098,6 +1146,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     if (m.forceTie > 0 && tid == 0 && (int)((unsigned)lb % (unsigned)m.forceTie) == 0) tie = true;
     if (__syncthreads_or(tie ? 1 : 0)) {  // rare: leave the block to k_prox_wave_fix
       if (tid == 0) m.tieList[atomicAdd(m.tieCount, 1u)] = lb;
+      __builtin_amdgcn_s_waitcnt(0);  // (an entry tie skips pass 1: no DMA left in flight)
       return;
     }
   }
@@ -1120,7 +1169,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
                                                      const double* Bin, double* Bout, double* __restrict__ partials,
                                                      int useCache) {
   constexpr int K = D * (D + 1);
-  __shared__ double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 1];
+  __shared__ __attribute__((aligned(16))) double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 2];
   const int lb = MMX_WAVE_XCD ? logical_block_any() : (int)blockIdx.x;  // XCD-contiguous tet ranges
   prox_wave_block<D, COMP, false>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
 }
@@ -1134,7 +1183,7 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave_fix(DeviceMesh<D
                                                          double* __restrict__ ug, const double* Bin, double* Bout,
                                                          double* __restrict__ partials) {
   constexpr int K = D * (D + 1);
-  __shared__ double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 1];
+  __shared__ __attribute__((aligned(16))) double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 2];
   const unsigned n = *m.tieCount;
   for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
     prox_wave_block<D, COMP, true>(m, tol, x, zg, ug, Bin, Bout, partials, 0, m.tieList[i], ldsHeld);
