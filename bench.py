@@ -113,6 +113,7 @@ def spmv_bench(torch, la, mx, with_cpu):
     out["cgstab"] = {"nitr": nitr, "solve_ms": round(st["t_solve_ms"], 2), "factor_ms": round(st["t_factor_ms"], 2),
                      "sweep_ms": round(st["t_sweep_ms"] / max(st["n_sweep_timed"], 1), 3),
                      "sweep_kernel": "k_chain_sweep (E=%d)" % st["sweep_e"] if st["sweep_mode"] else "k_sweep",
+                     "factor_kernel": "k_chain_factor" if st["factor_mode"] else "k_ilu_factor_lds",
                      "ms_per_iter": round((st["t_solve_ms"] - st["t_factor_ms"]) / max(nitr, 1), 2)}
     def _cpu():
         import time as _t

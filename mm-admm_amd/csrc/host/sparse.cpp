@@ -196,8 +196,8 @@ struct SparseMatrix {
   };
   ChainDir chf, chb;
   bool useChain = false;
-  // the numeric factor on the forward chain/band schedule (chain_factor.hip, 2D rows) with
-  // MMX_FACTOR=chain; the level schedule otherwise
+  // the numeric factor on the forward chain/band schedule (chain_factor.hip, 2D rows); the
+  // level schedule otherwise or with MMX_FACTOR=level
   struct FactorDir {
     DevBuf<int> bandSlot, bandT, laneLen, laneSkew, bandOrder, bandImp, bandNImp, impPos, impCnt, impSlot, impWait,
         impNeed, meta, rowStart, vsrc;
@@ -379,10 +379,11 @@ struct SparseMatrix {
     }
     useChainFactor = false;
     {
-      // opt-in (MMX_FACTOR=chain): bit-identical, but 30.8 ms against 25.0 ms for the level
-      // schedule at n = 2 M (profiles/r03/lasolver2d_factor.jsonl)
+      // default where the rows fit its layout (2D): bit-identical to the level schedule and
+      // 12.3 ms against 25.0 ms at n = 2 M (profiles/r03/chain_factor/);
+      // MMX_FACTOR=level (or global) keeps the level-scheduled factor
       const char* fm = getenv("MMX_FACTOR");
-      if (useChain && fm && std::strcmp(fm, "chain") == 0) {
+      if (useChain && !(fm && (std::strcmp(fm, "level") == 0 || std::strcmp(fm, "global") == 0))) {
         const FactorSchedule FS = build_factor_schedule(n, iaf, jaf, dg);
         if (FS.ok) {
           upload_factor(FS, dg);

@@ -322,10 +322,10 @@ def _factor_run(la, ia, ja, a, mode, monkeypatch):
 @pytest.mark.parametrize("mesh", [("rect", 2, 12), ("rect", 2, 45), ("hexdisc", 40), ("circle", "CircleEx24"),
                                   ("rect", 2, 300)])
 def test_chain_factor_equals_level_factor(la, mesh, monkeypatch):
-    """The numeric ILU(0) factor on the forward chain/band schedule (chain_factor.hip, MMX_FACTOR=chain:
-    each entry's updates target by target, pivots from the lane rings or imported rows) is
-    bit-identical to the level-scheduled k_ilu_factor_lds (the default) and, at small sizes, to the
-    restatement of the reference."""
+    """The numeric ILU(0) factor on the forward chain/band schedule (chain_factor.hip, the 2D
+    default: each entry's updates target by target, pivots from the lane rings or imported rows) is
+    bit-identical to the level-scheduled k_ilu_factor_lds (MMX_FACTOR=level) and, at small sizes,
+    to the restatement of the reference."""
     import mmadmm_amd as mx
     from conftest import circle_mesh
     if mesh[0] == "rect":
@@ -344,8 +344,8 @@ def test_chain_factor_equals_level_factor(la, mesh, monkeypatch):
     rows = np.repeat(np.arange(N), np.diff(ia))
     d = np.nonzero(ja == rows)[0]
     a[d] = np.add.reduceat(np.abs(a), ia[:-1]) * 0.3 + 1.0
-    af_c, fm_c = _factor_run(la, ia, ja, a, "chain", monkeypatch)
-    af_l, fm_l = _factor_run(la, ia, ja, a, None, monkeypatch)
+    af_c, fm_c = _factor_run(la, ia, ja, a, None, monkeypatch)
+    af_l, fm_l = _factor_run(la, ia, ja, a, "level", monkeypatch)
     assert fm_c == 1 and fm_l == 0
     assert _bit(af_c, af_l)
     if N < 20000:
