@@ -402,6 +402,7 @@ struct RegB {
   static constexpr bool kCarry = false;
   static constexpr bool kRolled = false;
   static constexpr int kPipe = 0;
+  static constexpr int kPipe1 = 0, kPipe2 = 0, kPipe3 = 0;
   static constexpr bool kPre = false;
   double* b;
   __device__ __forceinline__ double get(int i, int j) const { return b[i * K + j]; }
@@ -420,6 +421,7 @@ struct LdsB {
   static constexpr bool kCarry = false;
   static constexpr bool kRolled = true;  // the update pass one row per trip (code size; 2D: same speed)
   static constexpr int kPipe = 0;
+  static constexpr int kPipe1 = 0, kPipe2 = 0, kPipe3 = 0;
   static constexpr bool kPre = false;
   double* base;  // &lds[tid], entries strided by STRIDE
   __device__ __forceinline__ double get(int i, int j) const { return base[(i * K + j) * STRIDE]; }
@@ -451,11 +453,21 @@ typedef __attribute__((address_space(3))) double ldouble;
 #ifndef MMX_WAVE_DMA
 #define MMX_WAVE_DMA 1
 #endif
+#ifndef MMX_ROW_PIPE1
+#define MMX_ROW_PIPE1 6  // pass 1: global rows requested ahead (with kPre all of rows 6-11 while 0-5 come from LDS); C4 2 -> 6: -1.1%
+#endif
+#ifndef MMX_ROW_PIPE2
+#define MMX_ROW_PIPE2 6  // pass 2: rows 8-11 requested when it starts (6, 7 carried), read after rows 0-5 (LDS)
+#endif
+#ifndef MMX_ROW_PIPE3
+#define MMX_ROW_PIPE3 2  // pass 3
+#endif
 template <int K>
 struct WaveB {
   static constexpr bool kRowFence = true;
   static constexpr bool kRolled = true;
   static constexpr int kPipe = MMX_ROW_PIPE;
+  static constexpr int kPipe1 = MMX_ROW_PIPE1, kPipe2 = MMX_ROW_PIPE2, kPipe3 = MMX_ROW_PIPE3;
   static constexpr int kHeld = MMX_WAVE_HELD;  // rows kept in LDS from pass 1 to passes 2 and 3
   static constexpr bool kCarry = MMX_WAVE_CARRY;
   // the held rows of the entry matrix DMA'd into LDS at the start of the block (prox_wave_block),
@@ -617,12 +629,14 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     double rc[kPipe > 0 ? kPipe : 1][K];
     // kPre: the first iteration's held rows are in LDS already (DMA'd at the start of the block)
     const bool pre = BA::kPre && iter == 0;
-    start_rows<K, kPipe>(B, rn, pre ? BA::kHeld : 0);
+    constexpr int kP1 = BA::kPipe1;
+    double rn1[kP1 > 0 ? kP1 : 1][K];  // pass 1's queue of requested rows
+    start_rows<K, kP1>(B, rn1, pre ? BA::kHeld : 0);
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
       double row[K];
-      next_row<K, kPipe>(B, i, row, rn, pre);
+      next_row<K, kP1>(B, i, row, rn1, pre);
       if constexpr (BA::kHeld > 0) {  // the first kHeld rows wait in LDS for passes 2 and 3
         if (!pre && i < BA::kHeld)
 #pragma unroll
@@ -662,19 +676,24 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     B.fresh();
     // one pass over B: By_i = sum_j B_ij y_j, yBy = sum_i y_i By_i, yB_j = sum_i y_i B_ij
     double yBy = 0.0, yB[K];
+    constexpr int kP2 = BA::kPipe2 > kPipe ? BA::kPipe2 : kPipe;
+    double rn2[kP2 > 0 ? kP2 : 1][K];
     if constexpr (kCarry) {
 #pragma unroll
       for (int d = 0; d < kPipe; ++d)
 #pragma unroll
-        for (int j = 0; j < K; ++j) rn[d][j] = rc[d][j];
+        for (int j = 0; j < K; ++j) rn2[d][j] = rc[d][j];
+#pragma unroll
+      for (int d = kPipe; d < kP2; ++d)
+        if (BA::kHeld + d < K) load_row<K>(B, BA::kHeld + d, rn2[d]);
     } else {
-      start_rows<K, kPipe>(B, rn, BA::kHeld);
+      start_rows<K, kP2>(B, rn2, BA::kHeld);
     }
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       MMX_ROW_FENCE(BA);
       double row[K];
-      next_row<K, kPipe>(B, i, row, rn, true);
+      next_row<K, kP2>(B, i, row, rn2, true);
       if constexpr (kCarry) {
         if (i >= BA::kHeld && i < BA::kHeld + kPipe)
 #pragma unroll
@@ -700,13 +719,18 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     if constexpr (BA::kRolled) {
       // one row per trip (3D: the unrolled pass is ~60 KB of code, more than the instruction
       // cache; measured C4 prox 3.12 -> 2.93 ms), rows requested kPipe ahead
+      constexpr int kP3 = BA::kPipe3 > kPipe ? BA::kPipe3 : kPipe;
+      double rn3[kP3 > 0 ? kP3 : 1][K];
       if constexpr (kCarry) {
 #pragma unroll
         for (int d = 0; d < kPipe; ++d)
 #pragma unroll
-          for (int j = 0; j < K; ++j) rn[d][j] = rc[d][j];
+          for (int j = 0; j < K; ++j) rn3[d][j] = rc[d][j];
+#pragma unroll
+        for (int d = kPipe; d < kP3; ++d)
+          if (BA::kHeld + d < K) load_row<K>(B, BA::kHeld + d, rn3[d]);
       } else {
-        start_rows<K, kPipe>(B, rn, BA::kHeld);
+        start_rows<K, kP3>(B, rn3, BA::kHeld);
       }
       constexpr int UR = (D == 3 && K % MMX_UPD_ROWS == 0) ? MMX_UPD_ROWS : 1;
       if constexpr (UR == 1) {
@@ -716,7 +740,7 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
 #pragma unroll
           for (int k = 1; k < K; ++k) pki = (i == k) ? pk[k] : pki;
           double row[K];
-          next_row<K, kPipe>(B, i, row, rn, true);
+          next_row<K, kP3>(B, i, row, rn3, true);
           bfgs_update_row<D, EXACT>(B, i, pki, row, yk, pk, yB, c1, c2, rc2, eBy, fin);
         }
       } else {
@@ -728,7 +752,7 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
             pki[u] = pk[0];
 #pragma unroll
             for (int k = 1; k < K; ++k) pki[u] = (i + u == k) ? pk[k] : pki[u];
-            next_row<K, kPipe>(B, i + u, rows[u], rn, true);
+            next_row<K, kP3>(B, i + u, rows[u], rn3, true);
           }
           bfgs_update_rows<D, EXACT, UR>(B, i, pki, rows, yk, pk, yB, c1, c2, rc2, eBy, fin);
         }
