@@ -139,6 +139,62 @@ __device__ __forceinline__ int findLimInf(double w, double m0, int size, double 
 #ifndef MMX_MON_BATCH
 #define MMX_MON_BATCH 1
 #endif
+#ifndef MMX_MON_PIPE
+#define MMX_MON_PIPE 1
+#endif
+// 3D evalMonitorOnGrid in two halves, the loads of one point (monLoad3: the cell's coordinates
+// and its eight corner rows) and the trilinear interpolation (monEval3), so blockGrad can request
+// the next vertex's cell while it interpolates the current one: the same operations as the 3D
+// branch of evalMonitor below
+struct MonIn3 {
+  double x0, x1, y0, y1, z0, z1;
+  double r[8][9];
+};
+__device__ __forceinline__ void monLoad3(const GridView<3>& g, const double* pnt, MonIn3& in) {
+  const int xInd = findLimInf(pnt[0], g.ax, g.nx + 1, g.hx, g.rhx);
+  const int yInd = findLimInf(pnt[1], g.ay, g.ny + 1, g.hy, g.rhy);
+  const int zInd = findLimInf(pnt[2], g.az, g.nz + 1, g.hz, g.rhz);
+  const int nx = g.nx;
+  in.x0 = g.gx[xInd];
+  in.x1 = g.gx[xInd + 1];
+  in.y0 = g.gy[yInd];
+  in.y1 = g.gy[yInd + 1];
+  in.z0 = g.gz[zInd];
+  in.z1 = g.gz[zInd + 1];
+  const size_t P = (size_t)(nx + 1) * (g.ny + 1);
+  const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
+  const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
+                          base + P, base + P + 1, base + P + nx + 1, base + P + nx + 2};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const double2* rp = reinterpret_cast<const double2*>(g.pad + rows[q] * 10);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double2 v = rp[e];
+      in.r[q][2 * e] = v.x;
+      in.r[q][2 * e + 1] = v.y;
+    }
+    in.r[q][8] = g.pad[rows[q] * 10 + 8];
+  }
+}
+__device__ __forceinline__ void monEval3(const MonIn3& in, const double* pnt, M<3>& mv) {
+  const double xd = (pnt[0] - in.x0) / (in.x1 - in.x0);
+  const double yd = (pnt[1] - in.y0) / (in.y1 - in.y0);
+  const double zd = (pnt[2] - in.z0) / (in.z1 - in.z0);
+  const double c[8] = {(1 - xd) * (1 - yd) * (1 - zd), xd * (1 - yd) * (1 - zd),
+                       (1 - xd) * yd * (1 - zd),       xd * yd * (1 - zd),
+                       (1 - xd) * (1 - yd) * zd,       xd * (1 - yd) * zd,
+                       (1 - xd) * yd * zd,             xd * yd * zd};
+  double f[9];
+#pragma unroll
+  for (int n = 0; n < 9; ++n) f[n] = 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+#pragma unroll
+    for (int n = 0; n < 9; ++n) f[n] += c[q] * in.r[q][n];
+#pragma unroll
+  for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = f[n];
+}
 // MeshInterpolator<D>::evalMonitorOnGrid (src/MeshInterpolator.cpp:287-342)
 template <int D>
 __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* pnt, M<D>& mv) {
@@ -247,9 +303,20 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
   constexpr int K = D * (D + 1);
   const double dFact = (D == 2) ? 2.0 : 6.0;
   M<D> mPre[D + 1], Msum;
+  if constexpr (D == 3 && MMX_MON_PIPE) {  // vertex i + 1's cell requested while vertex i interpolates
+    MonIn3 ia, ib;
+    monLoad3(g, &z[0], ia);
+    monLoad3(g, &z[3], ib);
+    monEval3(ia, &z[0], mPre[0]);
+    monLoad3(g, &z[6], ia);
+    monEval3(ib, &z[3], mPre[1]);
+    monLoad3(g, &z[9], ib);
+    monEval3(ia, &z[6], mPre[2]);
+    monEval3(ib, &z[9], mPre[3]);
+  }
 #pragma unroll
   for (int i = 0; i < D + 1; i++) {
-    evalMonitor<D>(g, &z[i * D], mPre[i]);
+    if constexpr (!(D == 3 && MMX_MON_PIPE)) evalMonitor<D>(g, &z[i * D], mPre[i]);
 #pragma unroll
     for (int r = 0; r < D; ++r)
 #pragma unroll
