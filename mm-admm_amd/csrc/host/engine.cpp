@@ -254,13 +254,13 @@ class Engine final : public EngineBase {
     gs_.alloc((size_t)nF_ * K);
     MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
     {
-      // hessInvs = I (src/Mesh.cpp:456-464).  2D: simplex-major; 3D: wave-interleaved and
-      // double-buffered (k_prox_wave), padded to whole groups of 64 simplices
-      const size_t nB = (D == 2) ? (size_t)nF_ * K * K : (size_t)((nF_ + 63) / 64) * 64 * K * K;
+      // hessInvs = I (src/Mesh.cpp:456-464), wave-interleaved (bidx) and padded to whole chunks of
+      // 256 simplices (the 2D prox copies whole chunks); 3D double-buffered (k_prox_wave)
+      const size_t nB = (size_t)((nF_ + 255) / 256) * 256 * K * K;
       B_.alloc(nB);
       MMX_HIP(hipMemsetAsync(B_.p, 0, nB * sizeof(double), st_));
       launch_bkinv_identity<D>(nF_, B_.p, st_);
-      if (D == 3) B2_.alloc(nB);
+      if (prox_double_buffered(D)) B2_.alloc(nB);
     }
     // prox workgroups take 16 (3D quad) to 256 simplices; node kernels pad their grid to a multiple of 8 (XCD map)
     // (k_prox_quad: 16 tets per workgroup)
@@ -330,7 +330,7 @@ class Engine final : public EngineBase {
         MMX_HIP(hipEventRecord(a0, st_));
       }
       const bool firstProx = !hessComputed_;          // another kernel, another partial count
-      const bool swapB = (D == 3) && hessComputed_;  // 3D steady state: B_ -> B2_, then swap
+      const bool swapB = prox_double_buffered(D) && hessComputed_;  // steady state B_ -> B2_, then swap
       if (hessComputed_) {  // fast + exact pair: flip the tie queue
         tiePar_ ^= 1;
         std::swap(m_.tieCount, m_.tieStale);
@@ -552,7 +552,7 @@ class Engine final : public EngineBase {
     } else {
       throw Error(MMADMM_ERR_INVALID, "mmadmm_get: unknown field '" + what + "'");
     }
-    if (b == &B_ && D == 3) {  // wave-interleaved on the device: return simplex-major
+    if (b == &B_) {  // wave-interleaved on the device: return simplex-major
       std::vector<double> h(b->n);
       MMX_HIP(hipMemcpyAsync(h.data(), b->p, b->n * sizeof(double), hipMemcpyDeviceToHost, st_));
       MMX_HIP(hipStreamSynchronize(st_));
@@ -566,7 +566,6 @@ class Engine final : public EngineBase {
 
   // host mirror of bidx<D> (admm_kernels.hip)
   static size_t bIndex(int s, int ij) {
-    if (D == 2) return (size_t)s * K * K + ij;
     return ((size_t)(s >> 6) * K * K + ij) * 64 + (s & 63);
   }
 

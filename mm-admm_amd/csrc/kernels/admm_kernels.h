@@ -72,6 +72,9 @@ void launch_pad_rows(const double* vals, long long rows, double* pad, hipStream_
 template <int D>
 void launch_bkinv_identity(int nF, double* B, hipStream_t st);
 
+// the steady-state prox reads one Bkinv buffer and writes the other (the engine swaps them):
+// always in 3D (k_prox_wave), in 2D when MMX_PROX2D=wave selects k_prox_wave<2>
+bool prox_double_buffered(int D);
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z,
                  double* u, const double* Bin, double* Bout, double* partials, int* nblocks, hipStream_t st);

@@ -462,14 +462,16 @@ typedef __attribute__((address_space(3))) double ldouble;
 #ifndef MMX_ROW_PIPE3
 #define MMX_ROW_PIPE3 2  // pass 3
 #endif
+// 2D (K = 6, k_prox_wave<2>): every row held in LDS, so no streamed-row queues
 template <int K>
 struct WaveB {
+  static constexpr bool k2 = (K == 6);
   static constexpr bool kRowFence = true;
   static constexpr bool kRolled = true;
-  static constexpr int kPipe = MMX_ROW_PIPE;
-  static constexpr int kPipe1 = MMX_ROW_PIPE1, kPipe2 = MMX_ROW_PIPE2, kPipe3 = MMX_ROW_PIPE3;
-  static constexpr int kHeld = MMX_WAVE_HELD;  // rows kept in LDS from pass 1 to passes 2 and 3
-  static constexpr bool kCarry = MMX_WAVE_CARRY;
+  static constexpr int kPipe = k2 ? 0 : MMX_ROW_PIPE;
+  static constexpr int kPipe1 = k2 ? 0 : MMX_ROW_PIPE1, kPipe2 = k2 ? 0 : MMX_ROW_PIPE2, kPipe3 = k2 ? 0 : MMX_ROW_PIPE3;
+  static constexpr int kHeld = k2 ? K : MMX_WAVE_HELD;  // rows kept in LDS from pass 1 to passes 2 and 3
+  static constexpr bool kCarry = !k2 && MMX_WAVE_CARRY;
   // the held rows of the entry matrix DMA'd into LDS at the start of the block (prox_wave_block),
   // so the first pass 1 reads them from there
   static constexpr bool kPre = MMX_WAVE_DMA && kHeld > 0;
@@ -489,13 +491,12 @@ struct WaveB {
   __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(rd), "+v"(wr)::"memory"); }
 };
 
-// index of Bkinv entry ij of simplex s: 2D simplex-major (the LDS kernel's chunks), 3D
-// wave-interleaved (WaveB)
+// index of Bkinv entry ij of simplex s, wave-interleaved in 2D and 3D: the 2D LDS kernel's chunk
+// is then its LDS image (a straight copy), and WaveB's accesses are 512 contiguous bytes
 template <int D>
 __device__ __forceinline__ size_t bidx(int s, int ij) {
   constexpr int KK = D * (D + 1) * D * (D + 1);
-  if constexpr (D == 2) return (size_t)s * KK + ij;
-  else return ((size_t)(s >> 6) * KK + ij) * 64 + (s & 63);
+  return ((size_t)(s >> 6) * KK + ij) * 64 + (s & 63);
 }
 
 #define MMX_ROW_FENCE(BA) \
@@ -907,9 +908,8 @@ __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, co
 // per CU at most) stride over the list, so a prox with many ties is not serialised on one CU (with
 // no ties each workgroup only reads the counter).  The queue counters are double-buffered over the
 // steady proxes: this prox's recomputation clears the previous prox's counter (whose recomputation
-// has finished, stream order), which the next prox appends to -- a plain store, no atomics.  The queue counters are double-buffered over the steady proxes: this prox's
-// recomputation clears the previous prox's counter (whose recomputation has finished, stream
-// order), which the next prox appends to -- a plain store, no completion atomics.
+// has finished, stream order), which the next prox appends to -- a plain store, no completion
+// atomics.
 __device__ __forceinline__ void rearm_tie_queue(unsigned* tieStale) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *tieStale = 0u;
 }
@@ -930,17 +930,18 @@ __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, co
 }
 
 // Steady-state prox (every prox after the first), Bkinv staged through LDS.  The workgroup's
-// BS simplices own one contiguous Bkinv chunk (BS x K*K doubles): it is read and written back
-// with 16-byte-per-lane fully coalesced accesses and held in LDS as a padded structure-of-arrays
-// image [K*K][BS+1], so each lane's BFGS reads its own matrix conflict-free and the registers it
-// frees give two waves per SIMD.  Each lane's own inputs (vertices, z, u, the cached gradient)
-// are requested before the chunk, so their latency hides under it.
+// BS simplices own one contiguous Bkinv chunk of BS/64 wave blocks (bidx: [block][K*K][64]), which
+// is also the LDS image: entry ij of a lane's matrix sits 64 doubles after entry ij-1, so each
+// lane's BFGS reads its own matrix conflict-free, and the chunk moves in and out as a straight
+// 16-byte-per-lane copy (in: DMA'd to LDS, no registers; out: nontemporal stores).  The
+// registers this frees give two waves per SIMD.  Each lane's own inputs (vertices, z, u, the
+// cached gradient) are requested around the chunk, so their latency hides under it.
 // Fast path: the powers are not tie-resolved here (EXACT = false).  If any lane of the block
 // meets a near-midpoint power the whole block writes nothing back and is queued for k_prox_fix,
 // which recomputes it exactly from the untouched inputs.
 typedef double v2nt __attribute__((ext_vector_type(2)));
-#ifndef MMX_LDS_STAGE
-#define MMX_LDS_STAGE 1
+#ifndef MMX_LDS_DMA
+#define MMX_LDS_DMA 0  // 1: the chunk DMA'd to LDS after the gathers (C3 prox 0.380 ms); 0: through registers, requested before them (0.370 ms)
 #endif
 template <int D, int BS>
 __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol, const double* __restrict__ x,
@@ -948,7 +949,8 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
                                                         double* __restrict__ Bg, double* __restrict__ partials,
                                                         int useCache) {
   constexpr int K = D * (D + 1), KK = K * K;
-  __shared__ __attribute__((aligned(16))) double lds[KK * (BS + 1)];
+  static_assert(BS % 64 == 0, "whole wave blocks per chunk");
+  __shared__ __attribute__((aligned(16))) double lds[KK * BS];
   const int tid = threadIdx.x;
   const int lb = (int)blockIdx.x;  // (an XCD-contiguous mapping measured no gain: a 2D workgroup's simplices already share lines)
   const int s0 = lb * BS;
@@ -973,49 +975,38 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 #pragma unroll
     for (int i = 0; i <= K; ++i) gcv[i] = gc[i];
   }
+  // the chunk: BS/64 whole wave blocks (the buffer is padded to whole chunks of 256 simplices, so a
+  // short last chunk copies -- and writes back unchanged -- its padding)
   double* chunk = Bg + (size_t)s0 * KK;
-  const int tot = nIn * KK;  // even: K*K is even
-  // the chunk is read once and written once: nontemporal (C3 prox 0.412 -> 0.399 ms)
-  constexpr int NL = KK / 2;  // 16-byte loads per lane of a full chunk
-  v2nt cv[MMX_LDS_STAGE ? NL : 1];
-  if constexpr (MMX_LDS_STAGE) {
-    // every load of the chunk in flight at once (a short last chunk re-reads its last pair: no
-    // branch, so the wait for the vertex indices below is counted exactly), the lane's gathers
-    // behind them, then the LDS image (a loop writing each load's pair to LDS waits for it before
-    // requesting the next)
+  constexpr int NL = KK / 2;  // 16-byte pieces per lane; piece r of lane tid at 16 (tid + r BS)
+  v2nt cv[MMX_LDS_DMA ? 1 : NL];
+  if constexpr (!MMX_LDS_DMA) {
+    // the chunk is read once and written once: nontemporal (C3 prox 0.412 -> 0.399 ms)
+#pragma unroll
+    for (int r = 0; r < NL; ++r) cv[r] = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(chunk) + tid + r * BS);
+  }
+  double xi[K], dxv[K];
+  loadXi<D>(m, f, xi);
+  gatherX<D>(x, f, dxv);
+  if constexpr (MMX_LDS_DMA) {
+    // requested after the gathers (a wait for loads issued before an LDS DMA waits for the DMA
+    // too): wave w's lanes fill bytes [16 (r BS + 64 w), +1 KB) of the image, a wave-uniform base
+    __builtin_amdgcn_sched_barrier(0);
+    const char* src = reinterpret_cast<const char*>(chunk) + tid * 16;
+    const int wofs = __builtin_amdgcn_readfirstlane((tid >> 6) * 1024);
 #pragma unroll
     for (int r = 0; r < NL; ++r)
-      cv[r] = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(chunk + min(2 * (tid + r * BS), tot - 2)));
+      __builtin_amdgcn_global_load_lds(src + r * BS * 16,
+                                       (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + wofs + r * BS * 16),
+                                       16, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // (the DMA issued as one batch: nothing that waits moves into it)
+    __builtin_amdgcn_s_waitcnt(0);      // this wave's DMA has landed (the barrier then covers the workgroup's)
   } else {
-#pragma unroll 4
-    for (int e = tid * 2; e < tot; e += BS * 2) {
-      const v2nt vv = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(chunk + e));
-      const int sa = e / KK, ka = e - sa * KK;
-      const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
-      lds[ka * (BS + 1) + sa] = vv.x;
-      lds[kb * (BS + 1) + sb] = vv.y;
-    }
-  }
-  double xi[K];
-  loadXi<D>(m, f, xi);
-  {
-    double dxv[K];
-    gatherX<D>(x, f, dxv);
 #pragma unroll
-    for (int i = 0; i < K; ++i) dx[i] = dxv[i] + dx[i];  // DXpU = D x + uBar
+    for (int r = 0; r < NL; ++r) reinterpret_cast<v2nt*>(lds)[tid + r * BS] = cv[r];
   }
-  if constexpr (MMX_LDS_STAGE) {
 #pragma unroll
-    for (int r = 0; r < NL; ++r) {
-      const int e = 2 * (tid + r * BS);
-      const int sa = e / KK, ka = e - sa * KK;
-      const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
-      if (e < tot) {
-        lds[ka * (BS + 1) + sa] = cv[r].x;
-        lds[kb * (BS + 1) + sb] = cv[r].y;
-      }
-    }
-  }
+  for (int i = 0; i < K; ++i) dx[i] = dxv[i] + dx[i];  // DXpU = D x + uBar
   __syncthreads();
   double pv[6] = {0, 0, 0, 0, 0, 0};
   bool tie = false;
@@ -1027,9 +1018,9 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     entry_grad<D, false>(g, fc, z, xi, dx, gcv, useCache != 0, G, Igt, bad, &tie);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
-    LdsB<K, BS + 1> Bacc{lds + tid};
+    LdsB<K, 64> Bacc{lds + (tid >> 6) * KK * 64 + (tid & 63)};
     const int its =
-        tie ? 0 : bfgs_iterations<D, LdsB<K, BS + 1>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+        tie ? 0 : bfgs_iterations<D, LdsB<K, 64>, false>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -1057,18 +1048,9 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     }
     write_tslot<D>(m, s, z, un);
   }
-#pragma unroll 4
-  for (int e = tid * 2; e < tot; e += BS * 2) {
-    const int sa = e / KK, ka = e - sa * KK;
-    const int sb = (e + 1) / KK, kb = (e + 1) - sb * KK;
-    double2 v;
-    v.x = lds[ka * (BS + 1) + sa];
-    v.y = lds[kb * (BS + 1) + sb];
-    v2nt vs;
-    vs.x = v.x;
-    vs.y = v.y;
-    __builtin_nontemporal_store(vs, reinterpret_cast<v2nt*>(chunk + e));
-  }
+#pragma unroll
+  for (int r = 0; r < NL; ++r)
+    __builtin_nontemporal_store(reinterpret_cast<const v2nt*>(lds)[tid + r * BS], reinterpret_cast<v2nt*>(chunk) + tid + r * BS);
   block_partials<6, BS>(pv, partials, lb);
 }
 
@@ -1080,6 +1062,9 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 // by k_prox_wave_fix from the untouched inputs, as in the 2D kernel.
 #ifndef MMX_WAVE_OCC
 #define MMX_WAVE_OCC 1  // measured: one wave per SIMD (310 VGPRs); two (12-53 spills, p/G/DXpU parked in LDS) gain < 2%
+#endif
+#ifndef MMX_WAVE_OCC2
+#define MMX_WAVE_OCC2 2  // k_prox_wave<2> (MMX_PROX2D=wave): waves per SIMD
 #endif
 #ifndef MMX_WAVE_XCD
 #define MMX_WAVE_XCD 1  // measured C4: prox 3.42 -> 3.29 ms (neighbouring tets share x and monitor-grid lines in one L2)
@@ -1188,12 +1173,12 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
 }
 
 template <int D, bool COMP>
-__global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
+__global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                      double* __restrict__ zg, double* __restrict__ ug,
                                                      const double* Bin, double* Bout, double* __restrict__ partials,
                                                      int useCache) {
   constexpr int K = D * (D + 1);
-  __shared__ __attribute__((aligned(16))) double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 2];
+  __shared__ __attribute__((aligned(16))) double ldsHeld[WaveB<K>::kHeld > 0 ? WaveB<K>::kHeld * K * 64 : 2];
   const int lb = MMX_WAVE_XCD ? logical_block_any() : (int)blockIdx.x;  // XCD-contiguous tet ranges
   prox_wave_block<D, COMP, false>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
 }
@@ -1202,12 +1187,12 @@ __global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m,
 // generic one-lane k_prox_fix holds a tet's 144 Bkinv entries in registers and spills: ~0.3 ms
 // for one block).  A fixed grid strides over the queue, as k_prox_fix.
 template <int D, bool COMP>
-__global__ void __launch_bounds__(64, MMX_WAVE_OCC) k_prox_wave_fix(DeviceMesh<D> m, double tol,
+__global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_prox_wave_fix(DeviceMesh<D> m, double tol,
                                                          const double* __restrict__ x, double* __restrict__ zg,
                                                          double* __restrict__ ug, const double* Bin, double* Bout,
                                                          double* __restrict__ partials) {
   constexpr int K = D * (D + 1);
-  __shared__ __attribute__((aligned(16))) double ldsHeld[MMX_WAVE_HELD > 0 ? MMX_WAVE_HELD * K * 64 : 2];
+  __shared__ __attribute__((aligned(16))) double ldsHeld[WaveB<K>::kHeld > 0 ? WaveB<K>::kHeld * K * 64 : 2];
   const unsigned n = *m.tieCount;
   for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
     prox_wave_block<D, COMP, true>(m, tol, x, zg, ug, Bin, Bout, partials, 0, m.tieList[i], ldsHeld);
@@ -2118,6 +2103,17 @@ static int prox_block() {
 // 3D steady-state prox kernel: k_prox_wave (one lane per tet, default: C4 2.77 ms) or k_prox_quad
 // (four lanes per tet, MMX_PROX3D=quad: bit-identical, C4 3.92 ms -- DESIGN.md §3).  Read at every
 // launch, so a test can switch kernels between steps.
+// 2D steady-state prox kernel: k_prox_lds (default) or k_prox_wave<2> (MMX_PROX2D=wave: one wave
+// per workgroup, every Bkinv row held in LDS, double-buffered, rows written as the update forms
+// them).  Read once: the engine's buffer swap must match for the whole run.
+static int prox2d_wave() {
+  static int v = [] {
+    const char* e = getenv("MMX_PROX2D");
+    return (e && std::string(e) == "wave") ? 1 : 0;
+  }();
+  return v;
+}
+bool prox_double_buffered(int D) { return D == 3 || prox2d_wave(); }
 static int prox3d_quad() {
   const char* e = getenv("MMX_PROX3D");
   return (e && std::string(e) == "quad") ? 1 : 0;
@@ -2136,6 +2132,16 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
   if (m.nF == 0) return;
   if (first) {
     hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+  } else if (D == 2 && prox2d_wave()) {
+    *nblocks = (m.nF + 63) / 64;
+    const dim3 fg(std::min(*nblocks, kFixGrid));
+    if (m.compMesh) {
+      hipLaunchKernelGGL((k_prox_wave<D, true>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
+      hipLaunchKernelGGL((k_prox_wave_fix<D, true>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+    } else {
+      hipLaunchKernelGGL((k_prox_wave<D, false>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
+      hipLaunchKernelGGL((k_prox_wave_fix<D, false>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+    }
   } else if constexpr (D == 2) {
     double* B = Bout;  // in place (LDS image)
     const int bs = prox_block();
