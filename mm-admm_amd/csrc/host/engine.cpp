@@ -260,7 +260,8 @@ class Engine final : public EngineBase {
       B_.alloc(nB);
       MMX_HIP(hipMemsetAsync(B_.p, 0, nB * sizeof(double), st_));
       launch_bkinv_identity<D>(nF_, B_.p, st_);
-      if (prox_double_buffered(D)) B2_.alloc(nB);
+      wave2d_ = D == 2 && prox2d_wave_requested();
+      if (prox_double_buffered(D, wave2d_)) B2_.alloc(nB);
     }
     // prox workgroups take 16 (3D quad) to 256 simplices; node kernels pad their grid to a multiple of 8 (XCD map)
     // (k_prox_quad: 16 tets per workgroup)
@@ -330,7 +331,7 @@ class Engine final : public EngineBase {
         MMX_HIP(hipEventRecord(a0, st_));
       }
       const bool firstProx = !hessComputed_;          // another kernel, another partial count
-      const bool swapB = prox_double_buffered(D) && hessComputed_;  // steady state B_ -> B2_, then swap
+      const bool swapB = prox_double_buffered(D, wave2d_) && hessComputed_;  // steady state B_ -> B2_, then swap
       if (hessComputed_) {  // fast + exact pair: flip the tie queue
         tiePar_ ^= 1;
         std::swap(m_.tieCount, m_.tieStale);
@@ -887,6 +888,7 @@ class Engine final : public EngineBase {
     m.tieCount = tieCount_.p + tiePar_;  // keep the queue's parity across a rebuilt view (regrid)
     m.tieStale = tieCount_.p + (tiePar_ ^ 1);
     m.nodeOrder = nodeOrder_.p;
+    m.prox2dWave = wave2d_ ? 1 : 0;
     {
       const char* xs = getenv("MMX_XUP_SWEEP");  // 3D default: one workgroup per CU (profiles/r03/xupdate)
       m.xupSweep = xs ? std::max(0, atoi(xs)) : (D == 3 ? 1 : 0);
@@ -976,6 +978,7 @@ class Engine final : public EngineBase {
   DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_, gpad_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
   DevBuf<int32_t> expOff_, tieList_, nodeOrder_;
+  bool wave2d_ = false;  // 2D prox through k_prox_wave<2> (double-buffered Bkinv)
   DevBuf<unsigned> tieCount_;
   int tiePar_ = 0;
   PartitionPlan plan_;

@@ -46,6 +46,7 @@ struct DeviceMesh {
   double Ehat[9];
   double powd, w;
   int compMesh;
+  int prox2dWave;  // 2D steady-state prox through k_prox_wave<2> (engine set-up: MMX_PROX2D=wave)
 };
 
 struct StepScalars {
@@ -73,8 +74,9 @@ template <int D>
 void launch_bkinv_identity(int nF, double* B, hipStream_t st);
 
 // the steady-state prox reads one Bkinv buffer and writes the other (the engine swaps them):
-// always in 3D (k_prox_wave), in 2D when MMX_PROX2D=wave selects k_prox_wave<2>
-bool prox_double_buffered(int D);
+// always in 3D (k_prox_wave), in 2D with k_prox_wave<2> (DeviceMesh::prox2dWave)
+bool prox_double_buffered(int D, bool wave2d);
+bool prox2d_wave_requested();  // MMX_PROX2D=wave
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z,
                  double* u, const double* Bin, double* Bout, double* partials, int* nblocks, hipStream_t st);

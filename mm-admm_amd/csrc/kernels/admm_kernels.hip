@@ -2103,17 +2103,14 @@ static int prox_block() {
 // 3D steady-state prox kernel: k_prox_wave (one lane per tet, default: C4 2.77 ms) or k_prox_quad
 // (four lanes per tet, MMX_PROX3D=quad: bit-identical, C4 3.92 ms -- DESIGN.md §3).  Read at every
 // launch, so a test can switch kernels between steps.
-// 2D steady-state prox kernel: k_prox_lds (default) or k_prox_wave<2> (MMX_PROX2D=wave: one wave
-// per workgroup, every Bkinv row held in LDS, double-buffered, rows written as the update forms
-// them).  Read once: the engine's buffer swap must match for the whole run.
-static int prox2d_wave() {
-  static int v = [] {
-    const char* e = getenv("MMX_PROX2D");
-    return (e && std::string(e) == "wave") ? 1 : 0;
-  }();
-  return v;
+// 2D steady-state prox kernel: k_prox_lds (default) or k_prox_wave<2> (DeviceMesh::prox2dWave, set
+// from MMX_PROX2D=wave when the engine is built: one wave per workgroup, every Bkinv row held in
+// LDS, double-buffered, rows written as the update forms them; measured slower)
+bool prox_double_buffered(int D, bool wave2d) { return D == 3 || wave2d; }
+bool prox2d_wave_requested() {
+  const char* e = getenv("MMX_PROX2D");
+  return e && std::string(e) == "wave";
 }
-bool prox_double_buffered(int D) { return D == 3 || prox2d_wave(); }
 static int prox3d_quad() {
   const char* e = getenv("MMX_PROX3D");
   return (e && std::string(e) == "quad") ? 1 : 0;
@@ -2132,7 +2129,7 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
   if (m.nF == 0) return;
   if (first) {
     hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
-  } else if (D == 2 && prox2d_wave()) {
+  } else if (D == 2 && m.prox2dWave) {
     *nblocks = (m.nF + 63) / 64;
     const dim3 fg(std::min(*nblocks, kFixGrid));
     if (m.compMesh) {

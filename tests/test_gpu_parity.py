@@ -269,6 +269,28 @@ def test_quad_lane_prox_equals_wave_at_c4(monkeypatch):
     Q.close()
 
 
+@pytest.mark.parametrize("name", ["C1_circle24_mex5", "hexdisc12_mex1"])
+@pytest.mark.parametrize("force_tie", [0, 2])
+def test_prox2d_wave_bitwise(name, force_tie, monkeypatch):
+    """The 2D prox through k_prox_wave<2> (MMX_PROX2D=wave: one wave per workgroup, all six Bkinv
+    rows held in LDS, Bkinv double-buffered) against the oracle bit for bit, alone and with every
+    second block sent down its exact instance (MMX_FORCE_TIE=2)."""
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    monkeypatch.setenv("MMX_PROX2D", "wave")
+    if force_tie:
+        monkeypatch.setenv("MMX_FORCE_TIE", str(force_tie))
+    O, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    for s in range(3):
+        ih_o = O.step(5, -1.0)[0]
+        ih_g = G.step(5, -1.0)[0]
+        assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
+        for f in ("x", "z", "u"):
+            np.testing.assert_array_equal(G.get(f), O.get(f), err_msg=f"{f} step {s}")
+    np.testing.assert_array_equal(G.get("hess"), O.get("hess"))
+    assert G.stats()["bfgs_iters"] == O.bfgs_iters()
+
+
 @pytest.mark.parametrize("order,sweep", [(0, 0), (1, 0), (0, 2), (1, 4)])
 def test_xupdate_order_and_sweep_bitwise(order, sweep, monkeypatch):
     """The 3D slot-term x-update in its forms -- nodes by first incident simplex (order 0) or in eight
