@@ -17,6 +17,10 @@
  *   mmadmm_backward_euler_step MeshIntegrator<D>::backwardsEulerStep (src/MeshIntegrator.h:19,
  *                            .cpp:68-76) -> Mesh<D>::backwardsEulerStep (src/Mesh.cpp:1263-1341)
  *   mmadmm_get_jacobian      Mesh<D>::jac after buildEulerJac (src/Mesh.cpp:1112-1136)
+ *   mmadmm_be_begin / _residual / _fsubjac / _add
+ *                            the pieces of Mesh<D>::backwardsEulerStep (src/Mesh.cpp:1266-1273,
+ *                            1289-1294, 1112-1124 + 1232-1258, 1329), so a host loop can drive
+ *                            the Newton iteration through the LASolver classes (MatrixIter.h)
  *   mmadmm_energy            MeshIntegrator<D>::getEnergy (src/MeshIntegrator.h:20, .cpp:79-81)
  *   mmadmm_done              MeshIntegrator<D>::done (src/MeshIntegrator.h:23, .cpp:193-196)
  *   mmadmm_get("x"|"z")      MeshIntegrator<D>::outputX / outputZ (src/MeshIntegrator.h:21-22)
@@ -44,6 +48,9 @@ extern "C" {
 #define MMADMM_ERR_IO 4       /* file not readable / writable */
 #define MMADMM_ERR_RCCL 5     /* collective failure */
 #define MMADMM_ERR_NOCONV 6   /* linear solve did not converge: the reference's assert(cgIter > 0) */
+#define MMADMM_ERR_NONFINITE 7 /* non-finite energy with no inverted element: a monitor value that is not
+                                  finite (element partition + time-varying monitor: an evaluation outside
+                                  the rank's rebuilt grid box) */
 
 /* Node types (src/NodeType.h:4-8); mask arrays use these values. */
 #define MMADMM_BOUNDARY_FREE 0
@@ -140,6 +147,15 @@ int mmadmm_euler_step(mmadmm_handle h, double* Ih);
 int mmadmm_backward_euler_step(mmadmm_handle h, double dt, double tol, double* Ih, int* newton_iters);
 /* the last assembled backward-Euler Jacobian (CSR over D*nP unknowns); null arrays are skipped */
 int mmadmm_get_jacobian(mmadmm_handle h, long long* nnz, int32_t* ia, int32_t* ja, double* a);
+/* backward Euler in pieces (single rank): xn = x, Ih = eulerStepMod(x), x -= (dt/tau) grad */
+int mmadmm_be_begin(mmadmm_handle h, double dt, double* Ih);
+/* F = (dt/tau) grad(x) + (x - xn) (D*nP doubles to the host), ||F||_1 and Ih = sum of energies */
+int mmadmm_be_residual(mmadmm_handle h, double dt, double* F, double* norm1, double* Ih);
+/* the FSubJac sums at the mesh positions on the buildMatrix CSR pattern (mmadmm_get_jacobian's ia,
+ * ja), before buildEulerJac's a *= dt/tau and the +1 on the diagonal */
+int mmadmm_be_fsubjac(mmadmm_handle h, double* a);
+/* x += dx (D*nP doubles) */
+int mmadmm_be_add(mmadmm_handle h, const double* dx);
 int mmadmm_energy(mmadmm_handle h, double* E);
 int mmadmm_done(mmadmm_handle h);
 /* what: "x", "xPrev", "xBar", "z", "u", "points", "hess", "grid", "Ehat" */
@@ -208,6 +224,19 @@ int mmadmm_comm_unique_id(void* out, int len);
 int mmadmm_comm_create_rccl(int nranks, int rank, const void* uid, int device, mmadmm_comm* out);
 /* one communicator shared by nranks engines driven from threads of one process (tests) */
 int mmadmm_comm_create_loopback(int nranks, mmadmm_comm* out);
+/* transfers done by the caller's host transport (one process per rank, e.g. torch.distributed over
+ * gloo or MPI): the engine stages device blocks through pinned host buffers and calls these, in the
+ * same order on every rank; each returns 0 on success.
+ *   allgather: recv[q*count .. (q+1)*count) = rank q's send block (count doubles)
+ *   exchange: for each of npeers peers, send send[send_off[i] .. + send_count[i]) to rank
+ *             peer_rank[i] and receive recv_count[i] doubles from it into recv + recv_off[i]
+ *             (called on every halo exchange, also with npeers = 0) */
+typedef int (*mmadmm_allgather_fn)(void* user, const double* send, double* recv, long long count);
+typedef int (*mmadmm_exchange_fn)(void* user, int npeers, const int* peer_rank, const double* send,
+                                  const long long* send_off, const long long* send_count, double* recv,
+                                  const long long* recv_off, const long long* recv_count);
+int mmadmm_comm_create_host(int nranks, int rank, mmadmm_allgather_fn allgather, mmadmm_exchange_fn exchange,
+                            void* user, mmadmm_comm* out);
 int mmadmm_comm_destroy(mmadmm_comm c);
 /* like mmadmm_create, given the GLOBAL mesh on every rank; p->rank / p->nranks select the
  * share.  mmadmm_get / mmadmm_get_simplices then return this rank's nodes / simplices (in

@@ -552,6 +552,10 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
   const int L = kChainLanes;
   const char* fr = getenv("MMX_FAC_R");
   const int R = std::min(std::min(S.R, kFacRMax), fr ? atoi(fr) : kFacRMax);  // ring slots per lane (rows)
+  if (R != 1 && R != 2 && R != 4) {  // the ring is indexed p & (R - 1): a power of two, at most kFacRMax
+    F.why = "factor ring size " + std::to_string(R) + " not in {1, 2, 4}";
+    return F;
+  }
   F.R = R;
   F.slots = S.slots;
   // where every row is: band, lane, position, iteration
@@ -575,7 +579,7 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
   F.bandImp.assign(S.nbands, 0);
   F.bandNImp.assign(S.nbands, 0);
   const char* fri = getenv("MMX_FAC_RI");
-  const int RI = fri ? atoi(fri) : kFacImpRows;
+  const int RI = fri ? std::max(1, std::min(atoi(fri), kFacImpRows)) : kFacImpRows;  // s_dep holds kFacImpRows
   F.RI = RI;
   const int impBase = 1 + L * (R + 1) * kFacWU;
   struct Use {

@@ -3,6 +3,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -102,6 +103,78 @@ struct LoopbackComm final : Comm {
   }
 };
 
+// Transfers done by the caller (e.g. torch.distributed over gloo, or MPI, in the host process of
+// each rank): device blocks are staged through pinned host buffers and handed to the callbacks.
+// Every rank makes the same sequence of allgather / exchange calls (the engine's schedule), so the
+// callbacks can match their messages by call order.
+struct HostComm final : Comm {
+  int rank = 0;
+  mmadmm_allgather_fn ag;
+  mmadmm_exchange_fn ex;
+  void* user;
+  double* hs = nullptr;
+  double* hr = nullptr;
+  size_t cs = 0, cr = 0;
+  HostComm(int n, int r, mmadmm_allgather_fn a, mmadmm_exchange_fn e, void* u) : rank(r), ag(a), ex(e), user(u) {
+    nranks = n;
+  }
+  ~HostComm() override {
+    if (hs) (void)hipHostFree(hs);
+    if (hr) (void)hipHostFree(hr);
+  }
+  void reserve(size_t ns, size_t nr) {
+    if (ns > cs) {
+      if (hs) MMX_HIP(hipHostFree(hs));
+      hs = nullptr;
+      MMX_HIP(hipHostMalloc((void**)&hs, ns * sizeof(double), hipHostMallocDefault));
+      cs = ns;
+    }
+    if (nr > cr) {
+      if (hr) MMX_HIP(hipHostFree(hr));
+      hr = nullptr;
+      MMX_HIP(hipHostMalloc((void**)&hr, nr * sizeof(double), hipHostMallocDefault));
+      cr = nr;
+    }
+  }
+  void allgather(int, const double* dsend, double* drecv, size_t count, hipStream_t st) override {
+    reserve(std::max<size_t>(count, 1), std::max<size_t>(count * nranks, 1));
+    if (count) MMX_HIP(hipMemcpyAsync(hs, dsend, count * sizeof(double), hipMemcpyDeviceToHost, st));
+    MMX_HIP(hipStreamSynchronize(st));
+    if (ag(user, hs, hr, (long long)count) != 0) throw Error(MMADMM_ERR_RCCL, "host transport: allgather failed");
+    if (count) MMX_HIP(hipMemcpyAsync(drecv, hr, count * nranks * sizeof(double), hipMemcpyHostToDevice, st));
+    MMX_HIP(hipStreamSynchronize(st));
+  }
+  void exchange(int, const double* dsend, double* drecv, const std::vector<HaloPeer>& peers, int rowLen,
+                hipStream_t st) override {
+    const int np = (int)peers.size();
+    std::vector<int> pr(np);
+    std::vector<long long> so(np), sc(np), ro(np), rc(np);
+    size_t ns = 1, nr = 1;
+    for (int i = 0; i < np; ++i) {
+      const HaloPeer& p = peers[i];
+      pr[i] = p.rank;
+      so[i] = (long long)p.sendOff * rowLen;
+      sc[i] = (long long)p.sendCount * rowLen;
+      ro[i] = (long long)p.recvOff * rowLen;
+      rc[i] = (long long)p.recvCount * rowLen;
+      ns = std::max(ns, (size_t)(so[i] + sc[i]));
+      nr = std::max(nr, (size_t)(ro[i] + rc[i]));
+    }
+    reserve(ns, nr);
+    for (int i = 0; i < np; ++i)
+      if (sc[i])
+        MMX_HIP(hipMemcpyAsync(hs + so[i], dsend + so[i], sc[i] * sizeof(double), hipMemcpyDeviceToHost, st));
+    MMX_HIP(hipStreamSynchronize(st));
+    // called on every exchange, also with no peers, so the callbacks see the same call sequence on all ranks
+    if (ex(user, np, pr.data(), hs, so.data(), sc.data(), hr, ro.data(), rc.data()) != 0)
+      throw Error(MMADMM_ERR_RCCL, "host transport: exchange failed");
+    for (int i = 0; i < np; ++i)
+      if (rc[i])
+        MMX_HIP(hipMemcpyAsync(drecv + ro[i], hr + ro[i], rc[i] * sizeof(double), hipMemcpyHostToDevice, st));
+    MMX_HIP(hipStreamSynchronize(st));
+  }
+};
+
 }  // namespace
 
 Comm* make_rccl_comm(int nranks, int rank, const void* uid, int device) {
@@ -149,6 +222,15 @@ int mmadmm_comm_create_loopback(int nranks, mmadmm_comm* out) {
   return mmx::guarded([&] {
     if (!out || nranks < 1) throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_comm_create_loopback: bad arguments");
     *out = new mmadmm_comm_s{mmx::make_loopback_comm(nranks)};
+  });
+}
+
+int mmadmm_comm_create_host(int nranks, int rank, mmadmm_allgather_fn allgather, mmadmm_exchange_fn exchange,
+                            void* user, mmadmm_comm* out) {
+  return mmx::guarded([&] {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || !allgather || !exchange)
+      throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_comm_create_host: bad arguments");
+    *out = new mmadmm_comm_s{new mmx::HostComm(nranks, rank, allgather, exchange, user)};
   });
 }
 

@@ -41,6 +41,8 @@ struct EngineBase {
   virtual double eulerStep() = 0;
   virtual double backwardEulerStep(double dt, double tol, int* newton) = 0;
   virtual void jacobian(long long* nnz, int32_t* ia, int32_t* ja, double* a) = 0;
+  // the pieces of Mesh::backwardsEulerStep for a host-driven Newton loop (mmadmm_be_*)
+  virtual void newtonOp(int op, double dt, const double* in, double* out, double* sc) = 0;
   virtual double energy() = 0;
   virtual void done() = 0;
   virtual void get(const std::string& what, double* out) = 0;
@@ -148,16 +150,6 @@ class Engine final : public EngineBase {
       ownLocal_.upload(mine.data(), std::max<size_t>(mine.size(), 1), st_);
       MMX_HIP(hipStreamSynchronize(st_));
     }
-    for (int s = 0; s < nF_; ++s)  // the partitioned regrid's margin: the widest local simplex per axis
-      for (int d = 0; d < D; ++d) {
-        double a = INFINITY, b = -INFINITY;
-        for (int n = 0; n < D + 1; ++n) {
-          const double c = Vp[(size_t)plan_.localNodes[plan_.Flocal[(size_t)s * (D + 1) + n]] * D + d];
-          a = std::min(a, c);
-          b = std::max(b, c);
-        }
-        extMax_[d] = std::max(extMax_[d], b - a);
-      }
     const int nl = nP_;
     // t = M + dt^2 WD_T W D is block diagonal: t_vv = tau + dt^2 * (w*w summed valence times)
     std::vector<double> invdiag(nl);
@@ -248,8 +240,10 @@ class Engine final : public EngineBase {
     z_.alloc((size_t)nF_ * K);
     gcache_.alloc((size_t)nF_ * (K + 1));
     tieList_.alloc((size_t)nF_ / 16 + 1);  // prox blocks queued for the exact recomputation
-    tieCount_.alloc(2);  // queued blocks, double-buffered over the steady proxes (k_prox_fix)
-    MMX_HIP(hipMemsetAsync(tieCount_.p, 0, 2 * sizeof(unsigned), st_));
+    // [0..1]: queued blocks, double-buffered over the steady proxes (k_prox_fix); [2]: the
+    // inverted-element flag (GridView::invFlag), cleared when a failed step reads it
+    tieCount_.alloc(3);
+    MMX_HIP(hipMemsetAsync(tieCount_.p, 0, 3 * sizeof(unsigned), st_));
     u_.alloc((size_t)nF_ * K);
     gs_.alloc((size_t)nF_ * K);
     MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
@@ -427,7 +421,7 @@ class Engine final : public EngineBase {
       evUsed_ = evMark;
     }
     stepsTaken_++;
-    if (bad) throw Error(MMADMM_ERR_INVERTED, "inverted element in prox (reference: assert(Edet > 0))");
+    if (bad) throwBad("in prox");
     if (Ih) *Ih = hostRes_[0];  // Ihstart
     if (itersOut) *itersOut = done;
   }
@@ -442,7 +436,7 @@ class Engine final : public EngineBase {
     std::vector<double> rv;
     fetchResults(results_.p, 1, rv);
     const double* r = rv.data();
-    if (r[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element (reference: assert(Edet > 0))");
+    if (r[4] > 0) throwBad("in the explicit Euler gradient");
     return r[0];
   }
 
@@ -474,7 +468,7 @@ class Engine final : public EngineBase {
       launch_be_residual<D>(m_, gs_.p, x_.p, xn_.p, dtot, rhs_.p, partB_.p, &nb2, st_);
       launch_reduce_partials2(partA_.p, nb, results_.p, partB_.p, nb2, results_.p + kNumPartials, st_);
       fetchResults(results_.p, 1, rv);
-      if (rv[4] > 0) throw Error(MMADMM_ERR_INVERTED, "inverted element in backward Euler (reference: assert(Edet > 0))");
+      if (rv[4] > 0) throwBad("in backward Euler");
       Ih = rv[0];
       const double norm = rv[kNumPartials];
       if (norm < SAFETY_FAC * tol) break;
@@ -502,6 +496,56 @@ class Engine final : public EngineBase {
     st_stats_.t_be_ms += msSince(tStep);
     if (newtonOut) *newtonOut = nIter;
     return Ih;
+  }
+
+  // Mesh::backwardsEulerStep in pieces (src/Mesh.cpp:1263-1341), so that a host loop can drive the
+  // Newton iteration and solve through the reference's LASolver interface (include/mmadmm/
+  // MatrixIter.h): op 0 xn = x, Ih = eulerStepMod(x), x -= (dt/tau) grad (1266-1273; sc[0] = Ih);
+  // op 1 F = (dt/tau) grad(x) + (x - xn) into out (1289-1294; sc[0] = Ih, sc[1] = ||F||_1 as the
+  // engine's own loop forms it); op 2 the FSubJac sums at Vp on the buildMatrix CSR pattern, before
+  // buildEulerJac's scaling and identity (1112-1124, 1232-1258); op 3 x += in (1329).
+  void newtonOp(int op, double dt, const double* in, double* out, double* sc) override {
+    if (nranks_ > 1) throw Error(MMADMM_ERR_INVALID, "backward Euler runs on one rank (no element partition)");
+    ensureJacobian();
+    const int n = nP_ * D;
+    std::vector<double> rv;
+    int nb = 0, nb2 = 0;
+    if (op == 0) {
+      MMX_HIP(hipMemcpyAsync(xn_.p, x_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st_));
+      launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
+      launch_reduce_partials(partA_.p, nb, results_.p, st_);
+      launch_euler_apply<D>(m_, gs_.p, x_.p, dt / prm_.tau, st_);
+      fetchResults(results_.p, 1, rv);
+      if (rv[4] > 0) throwBad("in backward Euler");
+      if (sc) sc[0] = rv[0];
+    } else if (op == 1) {
+      launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
+      launch_be_residual<D>(m_, gs_.p, x_.p, xn_.p, dt / prm_.tau, rhs_.p, partB_.p, &nb2, st_);
+      launch_reduce_partials2(partA_.p, nb, results_.p, partB_.p, nb2, results_.p + kNumPartials, st_);
+      fetchResults(results_.p, 1, rv);
+      if (rv[4] > 0) throwBad("in backward Euler");
+      std::vector<double> r((size_t)n);
+      MMX_HIP(hipMemcpyAsync(r.data(), rhs_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+      for (int i = 0; i < n; ++i) out[i] = -r[i];  // rhs = -F on the device: the negation is exact
+      if (sc) {
+        sc[0] = rv[0];
+        sc[1] = rv[kNumPartials];
+      }
+    } else if (op == 2) {
+      const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
+      launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
+      launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, 1.0, jval_.p, st_, false);
+      MMX_HIP(hipMemcpyAsync(out, jval_.p, jja_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+      jacVp_ = -1;  // jval_ no longer holds the engine's own Jacobian
+    } else if (op == 3) {
+      MMX_HIP(hipMemcpyAsync(dx_.p, in, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st_));
+      launch_add_inplace(n, x_.p, dx_.p, st_);
+      MMX_HIP(hipStreamSynchronize(st_));
+    } else {
+      throw Error(MMADMM_ERR_INVALID, "newtonOp: unknown op");
+    }
   }
 
   void jacobian(long long* nnz, int32_t* ia, int32_t* ja, double* a) override {
@@ -738,7 +782,7 @@ class Engine final : public EngineBase {
     const int nG = (nranks_ > 1) ? plan_.nP : nP_;  // vertices the grid is built from
     const int nb = std::max(1, std::min(256, (nG + 255) / 256));
     if (!rgPart_.p) {
-      rgPart_.alloc((size_t)512 * 2 * D);  // global bbox partials, then this rank's
+      rgPart_.alloc((size_t)512 * 2 * D + 256 * D);  // global bbox partials, this rank's, its simplex extents
       rgMon_.alloc((size_t)nG * DD);
       rgCellOf_.alloc(nG);
       rgNodes_.alloc(nG);
@@ -749,23 +793,29 @@ class Engine final : public EngineBase {
         rgSend_.alloc((size_t)maxOwned_ * D);
         rgRecv_.alloc((size_t)nranks_ * maxOwned_ * D);
       }
-      MMX_HIP(hipHostMalloc((void**)&rgHost_, sizeof(double) * 512 * 2 * D, hipHostMallocDefault));
+      MMX_HIP(hipHostMalloc((void**)&rgHost_, sizeof(double) * (512 * 2 * D + 256 * D), hipHostMallocDefault));
     }
     const double* X = Vp_.p;
     const bool part = nranks_ > 1;
     const int nbl = part ? std::max(1, std::min(256, (nP_ + 255) / 256)) : 0;  // blocks of the local bbox
+    const int nbe = part ? std::max(1, std::min(256, (nF_ + 255) / 256)) : 0;  // blocks of the simplex extents
+    double* extPart = rgPart_.p + (size_t)512 * 2 * D;
     if (part) {
       launch_rows_gather(D, ownLocal_.p, nOwned_, Vp_.p, rgSend_.p, st_);
       comm_->allgather(rank_, rgSend_.p, rgRecv_.p, (size_t)maxOwned_ * D, st_);
       launch_rows_scatter(D, ownAllGid_.p, nranks_ * maxOwned_, rgRecv_.p, rgXg_.p, st_);
       X = rgXg_.p;
       launch_bbox<D>(Vp_.p, nP_, rgPart_.p + (size_t)256 * 2 * D, nbl, st_);  // this rank's vertices
+      launch_extent<D>(Vp_.p, F_.p, nF_, extPart, nbe, st_);  // its widest simplex per axis, now
     }
     launch_bbox<D>(X, nG, rgPart_.p, nb, st_);
     MMX_HIP(hipMemcpyAsync(rgHost_, rgPart_.p, sizeof(double) * nb * 2 * D, hipMemcpyDeviceToHost, st_));
-    if (part)
+    if (part) {
       MMX_HIP(hipMemcpyAsync(rgHost_ + (size_t)256 * 2 * D, rgPart_.p + (size_t)256 * 2 * D, sizeof(double) * nbl * 2 * D,
                              hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipMemcpyAsync(rgHost_ + (size_t)512 * 2 * D, extPart, sizeof(double) * nbe * D, hipMemcpyDeviceToHost,
+                             st_));
+    }
     MMX_HIP(hipStreamSynchronize(st_));
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -779,6 +829,11 @@ class Engine final : public EngineBase {
         llo[d] = std::min(llo[d], rgHost_[(size_t)(256 + b) * 2 * D + d]);
         lhi[d] = std::max(lhi[d], rgHost_[(size_t)(256 + b) * 2 * D + D + d]);
       }
+    if (part) {  // the box margin follows the mesh: the widest local simplex per axis at these positions
+      for (int d = 0; d < D; ++d) extMax_[d] = 0.0;
+      for (int b = 0; b < nbe; ++b)
+        for (int d = 0; d < D; ++d) extMax_[d] = std::max(extMax_[d], rgHost_[(size_t)512 * 2 * D + (size_t)b * D + d]);
+    }
     grid_geometry(D, nG, lo, hi, grid_);
     gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
     gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
@@ -887,6 +942,7 @@ class Engine final : public EngineBase {
     m.tieList = tieList_.p;
     m.tieCount = tieCount_.p + tiePar_;  // keep the queue's parity across a rebuilt view (regrid)
     m.tieStale = tieCount_.p + (tiePar_ ^ 1);
+    m.invFlag = tieCount_.p + 2;
     m.nodeOrder = nodeOrder_.p;
     m.prox2dWave = wave2d_ ? 1 : 0;
     {
@@ -942,6 +998,25 @@ class Engine final : public EngineBase {
     results_.alloc((size_t)resultsCap_ * 2 * kNumPartials);
   }
 
+  // A NaN energy: an element met Edet <= 0 (the reference's assert(Edet > 0)) if a blockGrad set
+  // the inverted flag, else a monitor value that is not finite -- on an element partition with a
+  // time-varying monitor, an evaluation outside the grid box this rank rebuilt (its rows are NaN).
+  [[noreturn]] void throwBad(const char* where) {
+    unsigned flag = 0;
+    MMX_HIP(hipMemcpyAsync(&flag, tieCount_.p + 2, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    if (flag) {
+      MMX_HIP(hipMemsetAsync(tieCount_.p + 2, 0, sizeof(unsigned), st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+      throw Error(MMADMM_ERR_INVERTED, std::string("inverted element ") + where + " (reference: assert(Edet > 0))");
+    }
+    if (nranks_ > 1 && regridEachStep_)
+      throw Error(MMADMM_ERR_NONFINITE, std::string("non-finite energy ") + where +
+                                            ": a monitor evaluation left this rank's regrid box (no element inverted)");
+    throw Error(MMADMM_ERR_NONFINITE, std::string("non-finite energy ") + where +
+                                          " without an inverted element (a monitor value that is not finite)");
+  }
+
   hipEvent_t nextEvent() {
     if (evUsed_ == evPool_.size()) {
       hipEvent_t e;
@@ -963,7 +1038,7 @@ class Engine final : public EngineBase {
   void* monUser_ = nullptr;
   bool regridEachStep_ = false, gridOnDevice_ = false;
   DevBuf<double> rgPart_, rgMon_, rgTmp_, rgTmp2_, rgXg_, rgSend_, rgRecv_;
-  double extMax_[3] = {0.0, 0.0, 0.0};  // largest extent of a local simplex per axis (partitioned regrid box)
+  double extMax_[3] = {0.0, 0.0, 0.0};  // widest local simplex per axis (partitioned regrid box), per rebuild
   DevBuf<int> ownLocal_, ownAllGid_;  // partitioned regrid: my owned vertices (local ids), all ranks' (global ids)
   int nOwned_ = 0, maxOwned_ = 1;
   DevBuf<int> rgCellOf_, rgNodes_, rgCounts_, rgStarts_, rgFill_;
@@ -1113,6 +1188,35 @@ int mmadmm_backward_euler_step(mmadmm_handle h, double dt, double tol, double* I
     if (!(dt > 0)) throw mmx::Error(MMADMM_ERR_INVALID, "backward Euler: dt must be > 0");
     const double r = eng(h).backwardEulerStep(dt, tol, newton_iters);
     if (Ih) *Ih = r;
+  });
+}
+int mmadmm_be_begin(mmadmm_handle h, double dt, double* Ih) {
+  return guarded([&] {
+    if (!(dt > 0)) throw mmx::Error(MMADMM_ERR_INVALID, "backward Euler: dt must be > 0");
+    double sc[2] = {0.0, 0.0};
+    eng(h).newtonOp(0, dt, nullptr, nullptr, sc);
+    if (Ih) *Ih = sc[0];
+  });
+}
+int mmadmm_be_residual(mmadmm_handle h, double dt, double* F, double* norm1, double* Ih) {
+  return guarded([&] {
+    if (!F) throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_be_residual: F is NULL");
+    double sc[2] = {0.0, 0.0};
+    eng(h).newtonOp(1, dt, nullptr, F, sc);
+    if (Ih) *Ih = sc[0];
+    if (norm1) *norm1 = sc[1];
+  });
+}
+int mmadmm_be_fsubjac(mmadmm_handle h, double* a) {
+  return guarded([&] {
+    if (!a) throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_be_fsubjac: a is NULL");
+    eng(h).newtonOp(2, 0.0, nullptr, a, nullptr);
+  });
+}
+int mmadmm_be_add(mmadmm_handle h, const double* dx) {
+  return guarded([&] {
+    if (!dx) throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_be_add: dx is NULL");
+    eng(h).newtonOp(3, 0.0, dx, nullptr, nullptr);
   });
 }
 int mmadmm_get_jacobian(mmadmm_handle h, long long* nnz, int32_t* ia, int32_t* ja, double* a) {

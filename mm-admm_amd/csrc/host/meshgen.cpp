@@ -211,6 +211,11 @@ double spherePhi(double x, double y, double z) {  // main.cpp:87-97 (squared for
 // the reference hands nothing back -- `delete Vp; Vp = Vpnew;` (663-666) reassigns its own
 // pointer copies, so the caller's arrays are left deleted -- and it does not compact the mask;
 // compact = true remaps the mask to the new numbering (false: the reference's old-id indexing).
+// A third repair: the reference remaps F in place (653-661), walking the used ids in ASCENDING
+// order with the DESCENDING map, so an entry already remapped to a larger id that is itself a used
+// id yet to come is remapped again (ids {0,1,2}: 0 -> 2 -> 0, and 2 -> 0 as well); F is remapped
+// here once per entry, with pntMap as the reference intends.  (The 2D generator's map is
+// ascending, so a remapped id never exceeds its original and that loop is sound.)
 void levelset3d(int nx, int ny, int nz, double xa, double xb, double ya, double yb, double za, double zb, int bType,
                 bool compact, MeshBuf& m) {
   const double EPS = 1e-12;

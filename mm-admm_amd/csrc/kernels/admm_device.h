@@ -30,6 +30,9 @@ struct GridView {  // the smoothed monitor grid, rows of D*D doubles
   // linspace (src/MeshUtils.h:24-29) parameters: g[i] = a + (i * span) / ns, recomputed on the
   // device instead of loaded (saves a dependent load before every monitor gather)
   double ax, ay, az, spx, spy, spz, nsx, nsy, nsz, rnsx, rnsy, rnsz;
+  // set to 1 by a blockGrad that meets a finite Edet <= 0 (a NaN Edet -- NaN positions -- does
+  // not set it): tells an inverted element from a non-finite monitor value at the step's end
+  unsigned* invFlag;
 };
 
 // grid coordinate i of an axis, bit-identical to the host linspace (div_nr is exact here:
@@ -347,6 +350,7 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
   }
   const double Edet = det<D>(E);
   if (!(Edet > 0)) {
+    if (Edet <= 0 && g.invFlag) *g.invFlag = 1u;  // cold path: a vector store to global memory
     const double nan = __builtin_nan("");
     if constexpr (GRAD) {
 #pragma unroll

@@ -26,9 +26,10 @@ struct DeviceMesh {
   double* gcache;         // per simplex K+1: unregularised gradient and energy at the current z
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
-  unsigned* tieStale;
+  unsigned* tieStale;      // the previous steady prox's counter, cleared by this prox's recomputation
+  unsigned* invFlag;       // set by a blockGrad that meets Edet <= 0 (GridView::invFlag)
   int xupCh;              // slots requested at once per node in the sweep (8, 16, 24)
-  int xupSweep;           // 3D slot-term x-update as a per-XCD sweep: workgroups per CU (0: one node per lane)     // the previous steady prox's counter, cleared by this prox's recomputation
+  int xupSweep;           // 3D slot-term x-update as a per-XCD sweep: workgroups per CU (0: one node per lane)
   int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
   const int* nodeOrder;   // x-update processing order (nodes by first incident simplex) or nullptr
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)
@@ -107,10 +108,11 @@ template <int D>
 void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st);
 // Jacobian values of buildEulerJac (src/Mesh.cpp:1112-1136, 1232-1258) on the buildMatrix CSR
 // pattern (ia, ja over the D*nP unknowns): per entry, the derivative blocks of the node's incident
-// simplices in ascending id (pairsort order, +0.0 adds), scaled by dt/tau, +1 on the diagonal.
+// simplices in ascending id (pairsort order, +0.0 adds), scaled by dt/tau, +1 on the diagonal
+// (finish = false: the sums alone, before the scaling and the identity).
 template <int D>
 void launch_jac_assemble(const DeviceMesh<D>& m, const int* ia, const int* ja, const double* dv,
-                         double dt_over_tau, double* a, hipStream_t st);
+                         double dt_over_tau, double* a, hipStream_t st, bool finish = true);
 // Newton residual F = (dt/tau) grad + (x - xn) with grad the INTERIOR-only scatter of gs
 // (eulerStepMod, src/Mesh.cpp:532-579); rhs = -F; partial record v[0] = sum |F_i|.
 template <int D>

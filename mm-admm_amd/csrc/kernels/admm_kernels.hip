@@ -97,6 +97,7 @@ __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   g.rnsx = m.grnsx;
   g.rnsy = m.grnsy;
   g.rnsz = m.grnsz;
+  g.invFlag = m.invFlag;
   return g;
 }
 
@@ -1324,6 +1325,7 @@ __device__ __forceinline__ double blockGradQuad(const GridView<3>& g, const Func
   }
   const double Edet = det<3>(E);
   if (!(Edet > 0)) {
+    if (Edet <= 0 && g.invFlag) *g.invFlag = 1u;
     const double nan = __builtin_nan("");
 #pragma unroll
     for (int c = 0; c < 3; ++c) go[c] = nan;
@@ -1789,7 +1791,7 @@ __global__ void __launch_bounds__(kBlock) k_fd_jac(DeviceMesh<D> m, const double
 template <int D>
 __global__ void __launch_bounds__(kBlock) k_jac_assemble(DeviceMesh<D> m, const int* __restrict__ ia,
                                                           const int* __restrict__ ja, const double* __restrict__ dv,
-                                                          double dt_over_tau, double* __restrict__ a) {
+                                                          double dt_over_tau, int finish, double* __restrict__ a) {
   constexpr int K = D * (D + 1);
   const int r = blockIdx.x * kBlock + threadIdx.x;
   if (r >= m.nP * D) return;
@@ -1817,8 +1819,10 @@ __global__ void __launch_bounds__(kBlock) k_jac_assemble(DeviceMesh<D> m, const 
         v = v + 0.0;
       }
     }
-    v *= dt_over_tau;
-    if (col == r) v += 1.0;
+    if (finish) {  // buildEulerJac's scaling and identity (src/Mesh.cpp:1125-1134); else the FSubJac sums
+      v *= dt_over_tau;
+      if (col == r) v += 1.0;
+    }
     a[i] = v;
   }
 }
@@ -2239,9 +2243,10 @@ void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* d
 }
 template <int D>
 void launch_jac_assemble(const DeviceMesh<D>& m, const int* ia, const int* ja, const double* dv, double dt_over_tau,
-                         double* a, hipStream_t st) {
+                         double* a, hipStream_t st, bool finish) {
   if (m.nP == 0) return;
-  hipLaunchKernelGGL(k_jac_assemble<D>, dim3(nblk(m.nP * D)), dim3(kBlock), 0, st, m, ia, ja, dv, dt_over_tau, a);
+  hipLaunchKernelGGL(k_jac_assemble<D>, dim3(nblk(m.nP * D)), dim3(kBlock), 0, st, m, ia, ja, dv, dt_over_tau,
+                     finish ? 1 : 0, a);
 }
 template <int D>
 void launch_be_residual(const DeviceMesh<D>& m, const double* gs, const double* x, const double* xn,
@@ -2271,7 +2276,7 @@ void launch_add_inplace(int n, double* x, const double* dx, hipStream_t st) {
   template void launch_euler_apply<D>(const DeviceMesh<D>&, const double*, double*, double, hipStream_t);     \
   template void launch_fd_jac<D>(const DeviceMesh<D>&, const double*, double, double*, hipStream_t);          \
   template void launch_jac_assemble<D>(const DeviceMesh<D>&, const int*, const int*, const double*, double,   \
-                                       double*, hipStream_t);                                                 \
+                                       double*, hipStream_t, bool);                                                 \
   template void launch_be_residual<D>(const DeviceMesh<D>&, const double*, const double*, const double*,      \
                                       double, double*, double*, int*, hipStream_t);
 MMX_INST(2)

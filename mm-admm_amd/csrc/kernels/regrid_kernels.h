@@ -24,6 +24,10 @@ struct GridBox {
 // per-block partial bounding boxes: partials[b * 2D + d] = min_d, [b * 2D + D + d] = max_d
 template <int D>
 void launch_bbox(const double* X, int n, double* partials, int nblocks, hipStream_t st);
+// per-block widest simplex per axis: partials[b * D + d] = max over the block's simplices of the
+// extent of their vertices along axis d (F: local simplices, D+1 local vertex ids each)
+template <int D>
+void launch_extent(const double* X, const int* F, int nF, double* partials, int nblocks, hipStream_t st);
 // counting sort of the vertices into cells: starts[ncell + 1] (exclusive scan of counts),
 // cellNodes[n]; counts must hold ncell + 1 ints, fill ncell
 template <int D>

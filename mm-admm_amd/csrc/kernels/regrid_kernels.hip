@@ -54,6 +54,47 @@ __global__ void __launch_bounds__(kRB) k_bbox(const double* __restrict__ X, int 
   if (threadIdx.x < 2 * D) part[(size_t)blockIdx.x * 2 * D + threadIdx.x] = sm[threadIdx.x][0];
 }
 
+// the widest simplex per axis (max over simplices of max - min of its vertices' coordinate):
+// the partitioned regrid's margin, re-measured from the current positions at every rebuild
+template <int D>
+__global__ void __launch_bounds__(kRB) k_extent(const double* __restrict__ X, const int* __restrict__ F, int nF,
+                                                double* __restrict__ part) {
+  __shared__ double sm[D][kRB];
+  double ext[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) ext[d] = 0.0;
+  for (int s = blockIdx.x * kRB + threadIdx.x; s < nF; s += gridDim.x * kRB) {
+    int v[D + 1];
+#pragma unroll
+    for (int n = 0; n <= D; ++n) v[n] = F[(size_t)s * (D + 1) + n];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      double a = X[(size_t)v[0] * D + d], b = a;
+#pragma unroll
+      for (int n = 1; n <= D; ++n) {
+        const double c = X[(size_t)v[n] * D + d];
+        a = c < a ? c : a;
+        b = c > b ? c : b;
+      }
+      const double e = b - a;
+      ext[d] = e > ext[d] ? e : ext[d];
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) sm[d][threadIdx.x] = ext[d];
+  __syncthreads();
+  for (int w = kRB / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const double a = sm[d][threadIdx.x + w];
+        sm[d][threadIdx.x] = a > sm[d][threadIdx.x] ? a : sm[d][threadIdx.x];
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < D) part[(size_t)blockIdx.x * D + threadIdx.x] = sm[threadIdx.x][0];
+}
+
 template <int D>
 __device__ __forceinline__ int cellOf(const double* x, const CellGrid& cg, int (&c)[3]) {
   int id = 0;
@@ -252,6 +293,11 @@ void launch_bbox(const double* X, int n, double* partials, int nblocks, hipStrea
 }
 
 template <int D>
+void launch_extent(const double* X, const int* F, int nF, double* partials, int nblocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_extent<D>, dim3(nblocks), dim3(kRB), 0, st, X, F, nF, partials);
+}
+
+template <int D>
 void launch_bin(const double* X, int n, const CellGrid& cg, int* cellOfV, int* counts, int* starts, int* fill,
                 int* cellNodes, void* scanTmp, size_t scanTmpBytes, hipStream_t st) {
   const int ncell = cg.n[0] * cg.n[1] * cg.n[2];
@@ -310,6 +356,7 @@ void launch_rows_scatter(int D, const int* idx, int n, const double* in, double*
 
 #define MMX_REGRID_INST(D)                                                                                       \
   template void launch_bbox<D>(const double*, int, double*, int, hipStream_t);                                 \
+  template void launch_extent<D>(const double*, const int*, int, double*, int, hipStream_t);                    \
   template void launch_bin<D>(const double*, int, const CellGrid&, int*, int*, int*, int*, int*, void*, size_t, \
                               hipStream_t);                                                                    \
   template void launch_monitor_tv<D>(const double*, int, const double*, double*, hipStream_t);                  \

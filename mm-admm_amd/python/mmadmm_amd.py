@@ -24,6 +24,10 @@ BOUNDARY_FREE, BOUNDARY_FIXED, INTERIOR = 0, 1, 2
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int_p = ctypes.POINTER(ctypes.c_int32)
 MONITOR_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, c_double_p, c_double_p, ctypes.c_void_p)
+c_ll_p = ctypes.POINTER(ctypes.c_longlong)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, c_double_p, c_double_p, ctypes.c_longlong)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, c_int_p, c_double_p, c_ll_p, c_ll_p,
+                               c_double_p, c_ll_p, c_ll_p)
 
 
 class mmadmm_params(ctypes.Structure):
@@ -60,6 +64,12 @@ class MMADMMError(RuntimeError):
 
 class InvertedElementError(MMADMMError):
     """The reference aborts on assert(Edet > 0) (src/AdaptationFunctional.cpp:174)."""
+
+
+class NonFiniteEnergyError(MMADMMError):
+    """MMADMM_ERR_NONFINITE: a NaN energy with no inverted element -- a monitor value that is not
+    finite (on an element partition with a time-varying monitor: an evaluation outside the rank's
+    rebuilt grid box)."""
 
 
 _lib = None
@@ -123,6 +133,11 @@ def lib():
     L.mmadmm_comm_create_rccl.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.mmadmm_comm_create_loopback.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.mmadmm_comm_destroy.argtypes = [vp]
+    L.mmadmm_comm_create_host.argtypes = [ctypes.c_int, ctypes.c_int, ALLGATHER_FN, EXCHANGE_FN, vp, ctypes.POINTER(vp)]
+    L.mmadmm_be_begin.argtypes = [vp, ctypes.c_double, c_double_p]
+    L.mmadmm_be_residual.argtypes = [vp, ctypes.c_double, c_double_p, c_double_p, c_double_p]
+    L.mmadmm_be_fsubjac.argtypes = [vp, c_double_p]
+    L.mmadmm_be_add.argtypes = [vp, c_double_p]
     L.mmadmm_create_partitioned.argtypes = [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, ctypes.c_int, c_int_p,
                                             c_int_p, ctypes.POINTER(mmadmm_params), MONITOR_FN, vp, vp,
                                             ctypes.POINTER(vp)]
@@ -150,6 +165,8 @@ def _check(rc):
         msg = lib().mmadmm_last_error().decode(errors="replace")
         if rc == 3:
             raise InvertedElementError(rc, msg)
+        if rc == 7:
+            raise NonFiniteEnergyError(rc, msg)
         raise MMADMMError(rc, msg)
 
 
@@ -332,6 +349,49 @@ class Comm:
         _check(lib().mmadmm_comm_create_loopback(int(nranks), ctypes.byref(h)))
         return Comm(h)
 
+    @staticmethod
+    def host(nranks, rank, transport):
+        """A communicator over the caller's host transport (one process per rank; `transport` has
+        allgather(send, recv) and exchange(peers, sends, recvs) on numpy arrays, e.g.
+        TorchDistTransport over a gloo process group): the engine stages its blocks through pinned
+        host memory and calls the transport in the same order on every rank."""
+
+        def ag(_user, send, recv, count):
+            try:
+                n = int(count)
+                s = np.ctypeslib.as_array(send, shape=(max(n, 1),))[:n]
+                r = np.ctypeslib.as_array(recv, shape=(max(n * nranks, 1),))[: n * nranks]
+                transport.allgather(s, r)
+                return 0
+            except BaseException:  # noqa: BLE001 -- reported to the engine as a status
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def ex(_user, npeers, peer, send, so, sc, recv, ro, rc):
+            try:
+                peers, sends, recvs = [], [], []
+                for i in range(npeers):
+                    peers.append(int(peer[i]))
+                    n_s, n_r = int(sc[i]), int(rc[i])
+                    sends.append(np.ctypeslib.as_array(ctypes.cast(ctypes.byref(send.contents, 8 * int(so[i])),
+                                                                   c_double_p), shape=(max(n_s, 1),))[:n_s])
+                    recvs.append(np.ctypeslib.as_array(ctypes.cast(ctypes.byref(recv.contents, 8 * int(ro[i])),
+                                                                   c_double_p), shape=(max(n_r, 1),))[:n_r])
+                transport.exchange(peers, sends, recvs)
+                return 0
+            except BaseException:  # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        cag, cex = ALLGATHER_FN(ag), EXCHANGE_FN(ex)
+        h = ctypes.c_void_p()
+        _check(lib().mmadmm_comm_create_host(int(nranks), int(rank), cag, cex, None, ctypes.byref(h)))
+        c = Comm(h)
+        c._keep = (cag, cex, transport)  # the callbacks must outlive the communicator
+        return c
+
     def close(self):
         if getattr(self, "h", None):
             lib().mmadmm_comm_destroy(self.h)
@@ -339,6 +399,43 @@ class Comm:
 
     def __del__(self):
         _close_at_exit(self)
+
+
+class TorchDistTransport:
+    """Host transport over an initialised torch.distributed CPU process group (gloo): all_gather
+    for the block all-gathers, tagged isend/irecv with the neighbouring ranks for the halo
+    exchange (messages matched by the engine's call order, which is the same on every rank)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.world = dist.get_world_size(group)
+        self.calls = 0
+        self.bytes_sent = 0
+
+    def allgather(self, send, recv):
+        t = self.torch
+        n = send.size
+        out = t.from_numpy(recv).view(self.world, n) if n else None
+        if n:
+            self.dist.all_gather(list(out.unbind(0)), t.from_numpy(send.copy()), group=self.group)
+            self.bytes_sent += 8 * n
+
+    def exchange(self, peers, sends, recvs):
+        t, d = self.torch, self.dist
+        tag = self.calls % (1 << 20)
+        self.calls += 1
+        reqs = []
+        for q, s, r in zip(peers, sends, recvs):
+            if s.size:
+                reqs.append(d.isend(t.from_numpy(s.copy()), q, group=self.group, tag=tag))
+                self.bytes_sent += 8 * s.size
+            if r.size:
+                reqs.append(d.irecv(t.from_numpy(r), q, group=self.group, tag=tag))
+        for q in reqs:
+            q.wait()
 
 
 def partition_plan(dim, Xp, F, nranks, rank, method="rcb"):

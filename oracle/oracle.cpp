@@ -512,15 +512,19 @@ static double spherePhi(double x, double y, double z) {  // main.cpp:87-97 (squa
   return xv * xv + yv * yv + zv * zv - r * r;
 }
 
-// MeshUtils.h:540-667 (3D meshFromLevelSetFun with spherePhi, main.cpp:363) restated, with the two
+// MeshUtils.h:540-667 (3D meshFromLevelSetFun with spherePhi, main.cpp:363) restated, with the three
 // defects that make the reference's 3D generator unusable repaired:
 //  * its result never reaches the caller: `delete Vc; Vc = Vcnew; delete Vp; Vp = Vpnew;`
 //    (663-666) reassigns the function's own pointer copies, leaving the caller's Vp/Vc deleted
 //    (dangling) while F has been remapped -- here Vp and F are the remapped mesh;
 //  * the mask is not compacted (written at the pre-compaction ids, 595-597); compactMask != 0
-//    remaps it (the evident intent, as for 2D), 0 keeps the reference's indexing.
+//    remaps it (the evident intent, as for 2D), 0 keeps the reference's indexing;
+//  * F is remapped in place (653-661) by walking the used ids in ASCENDING order with the
+//    DESCENDING map, so an entry remapped to a larger used id still to come is remapped again
+//    (used ids {0,1,2}: 0 -> 2 -> 0, and 2 -> 0 too) and the reference's F is corrupted -- here
+//    each entry is remapped exactly once (the 2D loop, 510-518, maps ids downwards and is sound).
 // The node numbering is the reference's: pntMap maps the i-th LARGEST used id to i (645-651, the
-// reversed rank) and F is remapped with it, consistently with Vp.  No final |phi| < EPS pass (the
+// reversed rank) and F is remapped with it once, consistently with Vp.  No final |phi| < EPS pass (the
 // 2D generator has one, 531-537; the 3D one does not).  The interior-side projection is
 // interpolateBoundaryLocation 3D (388-402): a central-difference gradient of spherePhi with
 // h = 2 sqrt(eps), normalised (Eigen normalize: divided by sqrt of the squared norm), and

@@ -114,6 +114,51 @@ def test_dropin_driver_reproduces_monitor210(tmp_path):
     np.testing.assert_array_equal(T, load_txt("Monitor210", "triangles.txt", dtype=np.int32))
 
 
+def _be_rows(out):
+    rows = [ln for ln in out.strip().splitlines() if ln[:1].isdigit()]
+    return [float(ln.split(",")[1]) for ln in rows], rows
+
+
+@pytest.mark.gpu
+def test_lasolver_mirror_backward_euler_monitor220():
+    """Method 2 of Monitor220 (SquareGrid 20, MEx3, dt 0.025 tau 0.5 rho 100, DtTol 1e-4) with the
+    backward Euler step driven from the host in the reference's call sequence over the LASolver
+    classes of include/mmadmm/MatrixIter.h (Mesh<D>::buildMatrix, src/Mesh.cpp:262-382;
+    Mesh<D>::backwardsEulerStep, 1263-1341): the pattern MatrixStruc builds equals the engine's,
+    the trace reproduces the reference's Experiments/Results/Monitor220/Ih2.txt to its 6 printed
+    digits with the same step count, and every energy and the final node positions equal the
+    engine's own mmadmm_backward_euler_step run bit for bit."""
+    if not os.path.exists(DRIVER):
+        pytest.skip("dropin_driver not built in-tree")
+    args = [DRIVER, "be", "2", "20", "3", "0.025", "0.5", "100", "1000", "1e-4"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "pattern equal" in r.stdout, r.stdout[:400]
+    ours, rows = _be_rows(r.stdout)
+    ref = load_txt("Monitor220", "Ih2.txt")[:, 1]
+    assert len(ours) == len(ref) and rel_err(np.array(ours), ref) < SIX_DIGITS
+    e = subprocess.run(args + ["engine"], capture_output=True, text=True, timeout=300)
+    assert e.returncode == 0, e.stderr
+    _, rows_e = _be_rows(e.stdout)
+    assert rows == rows_e  # %.17g: bit-identical energies
+    tail = [ln for ln in r.stdout.splitlines() if ln.startswith("newton")][0].split()
+    tail_e = [ln for ln in e.stdout.splitlines() if ln.startswith("newton")][0].split()
+    assert tail[1] == tail_e[1] and tail[-1] == tail_e[-1], (tail, tail_e)  # Newton count, position hash
+
+
+def test_lasolver_mirror_without_gpu_reports():
+    """CPU: the mirror compiles with the driver (MatrixStruc, MatrixIter, ParamIter, General_Exception in
+    namespace SparseItObj) and, with no GPU, fails with the engine's status, not a crash."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the GPU test")
+    d = driver()
+    r = subprocess.run([d, "be", "2", "4", "3", "0.025", "0.5", "100", "2", "1e-4"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 3 and "mmadmm error 2" in r.stderr, (r.returncode, r.stderr)
+
+
 @pytest.mark.gpu
 def test_python_monitor_subclass_equals_builtin():
     """MEx1 (Experiments/TestMonitors/MEx1.h:10-18) written as a Python MonitorFunction: the same

@@ -148,6 +148,44 @@ def test_c3_disc_reference_semantics():
     assert np.abs(xo - xg).max() / np.abs(xo).max() <= POS_TOL
 
 
+def _ref_semantics_protocol(m, mon, dt, tau, rho, steps, iters):
+    """The bench's protocol (early exit off: exactly `iters` ADMM iterations per step, the timed
+    trajectory of bench.py) against the reference-semantics oracle (glibc pow, Jacobi-CG on the
+    block-diagonal t with tol = eps; src/MeshIntegrator.cpp:144-172).  After every step: the same
+    BFGS iteration total (every L1 < 1e-5 exit of src/Mesh.cpp:850 decided alike) and the maximum
+    relative node-position error, which is returned per step."""
+    O, G = _pair(m, mon, dt, tau, rho, pow_mode=0, cg_mode=0)
+    errs = []
+    for s in range(steps):
+        ih_o, it_o = O.step(iters, -1.0)[:2]
+        ih_g, it_g = G.step(iters, -1.0)
+        assert it_o == it_g == iters
+        xo, xg = O.get("x"), G.get("x")
+        errs.append(float(np.abs(xo - xg).max() / np.abs(xo).max()))
+        bo, bg = O.bfgs_iters(), G.stats()["bfgs_iters"]
+        print(f"step {s}: max relative position error {errs[-1]:.3e}, BFGS total {bo} / {bg}", flush=True)
+        assert bg == bo, f"BFGS iteration total differs after step {s}"
+        assert abs(ih_o - ih_g) <= 1e-11 * abs(ih_o), f"step {s}"
+    print("max relative node-position error per step:", ", ".join(f"{e:.3e}" for e in errs))
+    assert errs[-1] <= POS_TOL, errs
+    G.close()
+    return errs
+
+
+def test_c3_disc_reference_semantics_bench_protocol():
+    """C3 (1,000,519 nodes) over the bench's timed protocol: 5 steps x 10 ADMM iterations, early
+    exit off, glibc pow + Jacobi-CG in the oracle; <= 1e-10 relative positions after the last step."""
+    m = mx.MeshData.hexdisc(577, 0.5, 0.5, 0.5)
+    _ref_semantics_protocol(m, 1, 0.055, 0.5, 50.0, 5, 10)
+
+
+def test_c4_cube_reference_semantics_bench_protocol():
+    """C4 (512,191 nodes, 3,000,564 tetrahedra) over the bench's protocol: 2 steps x 10 ADMM
+    iterations, early exit off, reference arithmetic in the oracle."""
+    m = mx.MeshData.rect(3, 63)
+    _ref_semantics_protocol(m, 6, 0.025, 0.5, 2000.0, 2, 10)
+
+
 def test_c4_cube_reference_semantics():
     """C4 (512,191 nodes, 3,000,564 tetrahedra) at reference semantics: one step with the early exit
     on, the same ADMM and BFGS iteration counts and node positions within 1e-10 relative."""

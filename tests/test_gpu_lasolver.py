@@ -262,15 +262,20 @@ def test_chain_sweeps_equal_level_sweeps(la, mesh, pair, monkeypatch):
         assert _bit(yc, L.ilu_solve(ia, ja, L.ilu0(ia, ja, a), b))
 
 
-@pytest.mark.parametrize("shift", [0.5, 0.3])
-def test_full_size_factor_sweeps_and_solve_bitwise(la, shift):
+@pytest.mark.parametrize("shift,factor", [(0.5, "auto"), (0.3, "auto"), (0.5, "level")])
+def test_full_size_factor_sweeps_and_solve_bitwise(la, shift, factor, monkeypatch):
     """The bench's ILU(0)-CG-STAB solve at its size (SquareGrid n=707 Jacobian pattern, 2,002,226
     rows, 28,008,516 nonzeros; shift 0.5 = the bench's diagonal, 0.3 = a harder system with more
-    iterations): the numeric factor (k_ilu_factor_lds on the level schedule), the chain/band
-    sweeps (2,048-slot import ring, ticket order, the one-iteration bands) and the whole CG-STAB
-    solve are bit-identical to the restatement (dotMode 1: the GPU's reduction order), with the
-    same iteration count; the sequential-dot restatement agrees within resid_reduc."""
+    iterations): the numeric factor (the 2D default k_chain_factor on the chain/band schedule, and
+    with MMX_FACTOR=level k_ilu_factor_lds on the level schedule), the chain/band sweeps (2,048-slot
+    import ring, ticket order, the one-iteration bands) and the whole CG-STAB solve are
+    bit-identical to the restatement (dotMode 1: the GPU's reduction order), with the same
+    iteration count; the sequential-dot restatement agrees within resid_reduc."""
     import mmadmm_amd as mx
+    if factor == "level":
+        monkeypatch.setenv("MMX_FACTOR", "level")
+    else:
+        monkeypatch.delenv("MMX_FACTOR", raising=False)
     mesh = mx.MeshData.rect(2, 707)
     s = la.MatrixStruc(2 * mesh.nP)
     s.mesh_pattern(2, mesh.F)
@@ -293,6 +298,7 @@ def test_full_size_factor_sweeps_and_solve_bitwise(la, shift):
     A.factor()
     st = A.stats()
     assert st["sweep_mode"] == 1  # the chain/band sweeps
+    assert st["factor_mode"] == (0 if factor == "level" else 1)  # no silent fallback at this size
     af = L.ilu0(ia, ja, a)
     assert _bit(A.get_factor()[2], af)
     assert _bit(A.ilu_solve(b), L.ilu_solve(ia, ja, af, b))

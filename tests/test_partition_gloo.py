@@ -172,3 +172,81 @@ def test_rcb_gives_every_rank_a_simplex(dim, n, world):
     sizes = [len(p["localSimplices"]) for p in plans]
     assert min(sizes) >= 1 and sum(sizes) == len(mesh.F), sizes
     assert all(len(p["localNodes"]) >= dim + 1 for p in plans)
+
+
+def _transport_main(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import mmadmm_amd as mx
+        tr = mx.TorchDistTransport()
+        ok = True
+        # all-gather of a block per rank into one buffer (the engine's per-step scalar partials, and
+        # the partitioned regrid's owned-vertex positions)
+        send = np.arange(5, dtype=np.float64) + 10 * rank
+        recv = np.zeros(5 * world)
+        tr.allgather(send, recv)
+        ok &= bool(np.array_equal(recv, np.concatenate([np.arange(5) + 10 * q for q in range(world)])))
+        # halo exchange on a ring: rank r sends (r + 1) * 3 values to both neighbours, in views of one
+        # host buffer at different offsets (as the engine's staging buffers), twice (tags by call order)
+        for rep in range(2):
+            peers = sorted({(rank + 1) % world, (rank - 1) % world} - {rank})
+            buf = np.zeros(64)
+            sends, recvs = [], []
+            off = 0
+            for q in peers:
+                n = (rank + 1) * 3
+                buf[off:off + n] = 1000 * rank + 100 * q + rep + np.arange(n)
+                sends.append(buf[off:off + n])
+                off += n
+            rbuf = np.zeros(64)
+            off = 0
+            for q in peers:
+                n = (q + 1) * 3
+                recvs.append(rbuf[off:off + n])
+                off += n
+            tr.exchange(peers, sends, recvs)
+            for q, r in zip(peers, recvs):
+                ok &= bool(np.array_equal(r, 1000 * q + 100 * rank + rep + np.arange(len(r))))
+            tr.exchange([], [], [])  # a rank with no peers still takes part in the call sequence
+        ok &= tr.calls == 4
+        out[rank] = ok
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_torch_dist_host_transport(world):
+    """mmadmm_amd.TorchDistTransport, the host transport of mmadmm_comm_create_host, on gloo CPU ranks:
+    the all-gather and the tagged neighbour exchange deliver every block where the engine's staging
+    buffers expect it (the GPU-side staging is tests/test_gpu_multiprocess.py)."""
+    pytest.importorskip("mmadmm_amd")
+    port = 31800 + world
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    procs = [ctx.Process(target=_transport_main, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    assert all(out[r] for r in range(world))
+
+
+def test_host_comm_create_without_gpu():
+    """mmadmm_comm_create_host validates its arguments and needs no device to be created."""
+    import mmadmm_amd as mx
+
+    class Null:
+        def allgather(self, s, r):
+            r[:] = 0
+
+        def exchange(self, peers, sends, recvs):
+            pass
+
+    c = mx.Comm.host(2, 1, Null())
+    c.close()
+    with pytest.raises(mx.MMADMMError):
+        mx.Comm.host(2, 2, Null())
