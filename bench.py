@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-be", action="store_true", help="skip the backward-Euler (method 2) section")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 (2D unit square, 99,905 nodes) section")
     ap.add_argument("--no-3d", action="store_true", help="skip the 3D (BASELINE config 4) section")
+    ap.add_argument("--no-bfgs", action="store_true", help="skip the BFGS-heavy (rho = 1) 2D section")
     ap.add_argument("--c5", action="store_true",
                     help="add BASELINE config 5 on one GPU: 3D 5.09M-node mesh, time-varying monitor")
     ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
@@ -289,6 +290,71 @@ def c4_bench(mx, with_cpu, threads, admm_iter):
     return out
 
 
+def bfgs_bench(mx, with_cpu, threads, admm_iter, steps=3):
+    """The compute-heavy prox regime: every other section runs at ~1.0 BFGS
+    iteration per simplex per prox, where the prox is one blockGrad plus a Bkinv stream.  Here the
+    1M-node SquareGrid n = 707 (1,001,113 nodes, 2,000,000 triangles) with MEx1 at rho = 1 (a weak
+    ADMM penalty: the prox minimises the functional almost freely), dt 0.055 tau 0.5, where the
+    BFGS loop (src/Mesh.cpp:827-856) takes ~3-4 iterations per simplex once the mesh moves.  Two
+    untimed steps, then `steps` timed steps of admm_iter iterations; the CPU leg runs the oracle on
+    the same mesh and trajectory (16 threads, 1 step after the same two)."""
+    mesh = mx.MeshData.rect(2, 707)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 1), rho=1.0, tau=0.5)
+    E = mx.Engine(M, 0.055)
+    for _ in range(2):
+        E.step(admm_iter, -1.0)
+    E.set_timing(True)
+    E.reset_stats()
+    E.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        E.step(admm_iter, -1.0)
+    E.sync()
+    el = time.perf_counter() - t0
+    st = E.stats()
+    prox_ms = st["t_prox_ms"] / max(st["n_prox"], 1)
+    xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
+    bpp = st["bfgs_iters"] / max(st["admm_iters"], 1) / mesh.nF
+    # algorithmic bytes grow with the BFGS iterations only through Bkinv's LDS image (read once,
+    # written once per prox): the same per-launch bytes as one iteration
+    prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
+    out = {"workload": "SquareGrid n=707, %d nodes, %d triangles, MEx1, rho 1, dt 0.055 tau 0.5, %d ADMM iterations "
+                       "per step, steps 3-5 of the run" % (mesh.nP, mesh.nF, admm_iter),
+           "value": round(steps * admm_iter / el, 3), "unit": "ADMM it/s", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 3),
+           "kernels": {"k_prox_ms": round(prox_ms, 4), "k_xupdate_ms": round(xup_ms, 4),
+                       "bfgs_iters_per_prox": round(bpp, 4), "max_bfgs": st["max_bfgs"]},
+           "prox_GBs_algorithmic": round(prox_gbs, 1),
+           "prox_us_per_bfgs_iteration": round(prox_ms * 1e3 / max(bpp, 1e-9), 2)}
+    fl = pmc_entry("k_prox_lds<2, 128>@bfgs_heavy").get("fp64_flops_per_launch")
+    if fl:
+        out["prox_fp64"] = {"executed_flops_per_launch": fl, "achieved_TFLOPs": round(fl / (prox_ms * 1e-3) / 1e12, 2),
+                            "peak_TFLOPs": 78.6, "frac": round(fl / (prox_ms * 1e-3) / 1e12 / 78.6, 4),
+                            "source": "builder-measured rocprofv3 SQ_INSTS_VALU_*_F64 pass of this section "
+                                      "(profiles/pmc_summary.json)"}
+    E.close()
+
+    def _cpu():
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_py
+        om = oracle_py.Mesh(2, mesh.Xp, mesh.F, mesh.mask)
+        O = oracle_py.Integrator(om, 1, 0.055, 0.5, 1.0, nthreads=threads)
+        for _ in range(2):
+            O.step(admm_iter, -1.0)
+        b0 = O.bfgs_iters()
+        t0 = time.perf_counter()
+        O.step(admm_iter, -1.0)
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(admm_iter / cdt, 3), "unit": "ADMM it/s", "cores": threads,
+                               "kind": "port", "bfgs_iters_per_prox": round((O.bfgs_iters() - b0) / admm_iter / mesh.nF, 4),
+                               "gpu_speedup": round(out["value"] * cdt / admm_iter, 1),
+                               "sample": "the same mesh and trajectory: 2 untimed steps, then 1 timed step of %d ADMM "
+                                         "iterations (oracle/oracle.cpp, %d threads)" % (admm_iter, threads)}
+    if with_cpu:
+        DEFERRED.append(_cpu)
+    return out
+
+
 def tv_bench(mx, n, admm_iter, steps=3):
     """Time-varying monitor (BASELINE config 5's "time-varying monitor") on one GPU:
     3D SquareGrid n (63: the C4 mesh; 136: C5, 5.09 M nodes), MonType 7 (a bump moving on a circle),
@@ -355,7 +421,10 @@ def pmc_traffic(kernel):
 def host_info(threads):
     """The GPU box's host as the CPU baseline saw it: nproc, the CPUs this job may run
     on, the lscpu model and physical core count, and the threads the baseline used."""
-    info = {"threads_used": threads, "nproc": os.cpu_count(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+    info = {"threads_used": threads, "nproc": os.cpu_count(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "threads_note": "the all-core leg uses the CPU share this job is granted (the harness sets OMP_NUM_THREADS "
+                            "on the GPU box; the box's other cores serve other jobs), not every physical core "
+                            "nproc reports"}
     try:
         info["affinity_cpus"] = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -586,7 +655,8 @@ def main():
                      "achieved": round(prox_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_fetch_uncorrected": traffic_raw,
-                     "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE, WRITE_SIZE passes)",
+                     "traffic_source": "builder-measured, not this run: profiles/pmc_summary.json (rocprofv3 "
+                                       "FETCH_SIZE, WRITE_SIZE passes of the committed tree)",
                      "bytes_per_launch": st["prox_bytes"],
                      "avg_launch_ms": round(prox_ms, 4)},
         "prox_fp64": None,
@@ -604,6 +674,14 @@ def main():
                                "peak_TFLOPs": 78.6, "frac": round(fl / (prox_ms * 1e-3) / 1e12 / 78.6, 4),
                                "source": "rocprofv3 SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes "
                                          "(profiles/pmc_summary.json); peak: AMD MI355X fp64 vector spec"}
+    if not c4:
+        # SURVEY §8(d)'s compulsory bytes exclude the entry-gradient cache (16 (K+1) B per simplex,
+        # read and written every launch): an implementation choice that saves a blockGrad
+        comp = st["prox_bytes"] - 16 * 7 * eng.nF
+        result["roofline"]["compulsory_bytes_per_launch"] = comp
+        result["roofline"]["frac_compulsory"] = round(comp / (prox_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        result["roofline"]["compulsory_note"] = ("bytes_per_launch minus the prox-entry gradient cache "
+                                                 "(16 (K+1) B per simplex, K = 6)")
     if rank == 0 and world == 1:
         cc, tc = stream_copy_ceiling(torch, la)
         result["roofline"]["measured_copy_ceiling_GBs"] = cc
@@ -619,6 +697,12 @@ def main():
     if not args.no_c2 and world == 1 and not c4:
         log("C2 square grid")
         result["c2"] = c2_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
+    if not args.no_bfgs and world == 1 and not c4:
+        log("BFGS-heavy 2D (rho 1)")
+        try:
+            result["bfgs_heavy"] = bfgs_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
+        except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
+            result["bfgs_heavy"] = {"error": str(e)}
     if not args.no_3d and world == 1 and not c4:
         log("3D C4")
         result["c4_3d"] = c4_bench(mx, not args.no_cpu_baseline, threads, args.admm_iter)
@@ -635,7 +719,7 @@ def main():
         result["c5_time_varying"] = tv_bench(mx, 136, args.admm_iter, steps=2)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c4:
         log("cpu baseline")
-        result["cpu_baseline"] = cpu_baseline(mesh, args.admm_iter, threads)
+        result["cpu_baseline"] = cpu_baseline(mesh, args.admm_iter, threads, steps1=CPU_STEPS)
     for f in DEFERRED:  # the sections' CPU baselines, after every GPU measurement
         log("cpu baseline:", f.__qualname__.split(".")[0])
         f()

@@ -149,13 +149,11 @@ def test_lasolver_mirror_backward_euler_monitor220():
 def test_lasolver_mirror_without_gpu_reports():
     """CPU: the mirror compiles with the driver (MatrixStruc, MatrixIter, ParamIter, General_Exception in
     namespace SparseItObj) and, with no GPU, fails with the engine's status, not a crash."""
-    import torch
-
-    if torch.cuda.is_available():
-        pytest.skip("GPU present: covered by the GPU test")
     d = driver()
     r = subprocess.run([d, "be", "2", "4", "3", "0.025", "0.5", "100", "2", "1e-4"], capture_output=True, text=True,
                        timeout=120)
+    if r.returncode == 0 and "pattern equal" in r.stdout:
+        pytest.skip("a GPU is present: the run went through (the GPU test checks its numbers)")
     assert r.returncode == 3 and "mmadmm error 2" in r.stderr, (r.returncode, r.stderr)
 
 
