@@ -675,13 +675,13 @@ def main():
                                "source": "rocprofv3 SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes "
                                          "(profiles/pmc_summary.json); peak: AMD MI355X fp64 vector spec"}
     if not c4:
-        # SURVEY §8(d)'s compulsory bytes exclude the entry-gradient cache (16 (K+1) B per simplex,
+        # SURVEY §8(d)'s compulsory bytes exclude the entry-gradient cache (16 K B per simplex,
         # read and written every launch): an implementation choice that saves a blockGrad
-        comp = st["prox_bytes"] - 16 * 7 * eng.nF
+        comp = st["prox_bytes"] - 16 * 6 * eng.nF
         result["roofline"]["compulsory_bytes_per_launch"] = comp
         result["roofline"]["frac_compulsory"] = round(comp / (prox_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         result["roofline"]["compulsory_note"] = ("bytes_per_launch minus the prox-entry gradient cache "
-                                                 "(16 (K+1) B per simplex, K = 6)")
+                                                 "(16 K B per simplex, K = 6)")
     if rank == 0 and world == 1:
         cc, tc = stream_copy_ceiling(torch, la)
         result["roofline"]["measured_copy_ceiling_GBs"] = cc

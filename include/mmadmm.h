@@ -97,7 +97,10 @@ typedef struct mmadmm_stats {
   double t_be_ms;         /* backward Euler: wall time of whole steps */
   long long regrids;      /* monitor-grid rebuilds on the device (mmadmm_regrid / set_regrid) */
   long long regrid_rows;  /* grid rows the last rebuild filled (an element partition: this rank's box) */
-  double regrid_gather_bytes; /* vertex positions this rank received for the last rebuild */
+  double regrid_gather_bytes; /* bytes this rank received for the last rebuild (element partition) */
+  long long regrid_cand;       /* element partition: candidate vertices of the last rebuild's nearest-
+                                  vertex fill (this rank's + those received from its neighbours) */
+  long long regrid_fallbacks;  /* element partition: rebuilds that fell back to all-gathering every vertex */
 } mmadmm_stats;
 
 /* Time-varying monitors (the reference's Mesh<D>::setUp hook, commented out at

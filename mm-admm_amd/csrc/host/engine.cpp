@@ -147,6 +147,7 @@ class Engine final : public EngineBase {
         mine.push_back((int)(std::lower_bound(plan_.localNodes.begin(), plan_.localNodes.end(), v) - plan_.localNodes.begin()));
       nOwned_ = (int)mine.size();
       ownAllGid_.upload(all.data(), all.size(), st_);
+      ownAllGidH_ = all;
       ownLocal_.upload(mine.data(), std::max<size_t>(mine.size(), 1), st_);
       MMX_HIP(hipStreamSynchronize(st_));
     }
@@ -238,7 +239,7 @@ class Engine final : public EngineBase {
       remote_.alloc((size_t)std::max(plan_.recvRows, 1) * D);
     }
     z_.alloc((size_t)nF_ * K);
-    gcache_.alloc((size_t)nF_ * (K + 1));
+    gcache_.alloc((size_t)nF_ * K);
     tieList_.alloc((size_t)nF_ / 16 + 1);  // prox blocks queued for the exact recomputation
     // [0..1]: queued blocks, double-buffered over the steady proxes (k_prox_fix); [2]: the
     // inverted-element flag (GridView::invFlag), cleared when a failed step reads it
@@ -273,6 +274,7 @@ class Engine final : public EngineBase {
 
   ~Engine() override {
     if (rgHost_) (void)hipHostFree(rgHost_);
+    if (rgnHost_) (void)hipHostFree(rgnHost_);
     if (jac_) (void)mmx_matrix_destroy(jac_);
     for (auto& e : evPool_) (void)hipEventDestroy(e);
     if (st_) (void)hipStreamDestroy(st_);
@@ -637,11 +639,11 @@ class Engine final : public EngineBase {
     // writes z, u, Bkinv; x is gathered once per node.  x-update reads the incidence CSR,
     // z and u once each, xBar and invdiag, writes x.
     const double nF = nF_, nP = nP_;
-    // + the gradient cache: K+1 doubles read at entry and written by the last BFGS iteration
+    // + the gradient cache: K doubles read at entry and written by the last BFGS iteration
     // with the slot terms (tslot, 3D) the prox also writes K doubles per simplex and the x-update
     // reads those instead of z and u
     const double ts = tslotOn_ ? 1.0 : 0.0;
-    s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2 + 8.0 * (K + 1) * 2 + ts * 8.0 * K) +
+    s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2 + 8.0 * K * 2 + ts * 8.0 * K) +
                     nP * 8.0 * D;
     s->xupdate_bytes = 4.0 * (nP + 1) + 4.0 * (D + 1) * nF + (16.0 - 8.0 * ts) * K * nF + 8.0 * D * nP * 2 + 8.0 * nP;
   }
@@ -771,13 +773,273 @@ class Engine final : public EngineBase {
   // box, monitor at the vertices (MonType 7 on the device at time t; any other monitor through its
   // host callback), nearest vertex of every grid point, smoothing -- bit-identical to the host
   // set-up (regrid_kernels.hip).  One 2D-double readback (the bounding box) per call.
-  // On an element partition every rank needs every vertex: each rank sends the positions of the
-  // vertices it owns (lowest incident simplex), one all-gather, and every rank places all of them
-  // at their global ids and builds the same grid (the replicated interface positions are
-  // bit-identical across ranks, so the owner choice does not matter).
+  // On an element partition (regridNear) a rank rebuilds only the box of grid rows its monitor
+  // evaluations can reach, and receives only the vertices that can be nearest to a point of that
+  // box: the ranks all-gather their bounding boxes (the global box sets the grid geometry, the same
+  // on every rank) and their search boxes S (the row box widened by a margin), each rank sends
+  // the vertices it owns (lowest incident simplex) that lie in another rank's S to that rank, and
+  // the nearest-vertex fill over these candidates checks, point by point, that its answer is
+  // strictly nearer than S's boundary -- so no vertex it does not hold can be as near, and the
+  // rows equal the single-GPU grid's.  If any point of any rank fails the check (all ranks agree
+  // on it), the rebuild falls back to regridAll: every owned vertex all-gathered to every rank.
   void setRegrid(bool on) override { regridEachStep_ = on; }
 
   void regrid(double t) override {
+    if (nranks_ > 1) {
+      const char* mode = getenv("MMX_REGRID_GATHER");  // "all": the full all-gather (round 3)
+      if (!(mode && std::string(mode) == "all") && regridNear(t)) return;
+      st_stats_.regrid_fallbacks += (mode && std::string(mode) == "all") ? 0 : 1;
+    }
+    regridAll(t);
+  }
+
+  // the partitioned rebuild from the candidates near this rank's box; false: fall back (collective)
+  bool regridNear(double t) {
+    constexpr int DD = D * D;
+    const int nG = plan_.nP;
+    const int nbl = std::max(1, std::min(256, (nP_ + 255) / 256));
+    const int nbe = std::max(1, std::min(256, (nF_ + 255) / 256));
+    const size_t smallN = (size_t)std::max(2 * D, nranks_);
+    if (!rgnPart_.p) {
+      rgnPart_.alloc((size_t)256 * 2 * D + 256 * D);
+      rgnSmallS_.alloc(smallN);
+      rgnSmallR_.alloc(smallN * nranks_);
+      rgnSbox_.alloc((size_t)nranks_ * 2 * D);
+      rgnCnt_.alloc(nranks_ + 1);  // + the fail flag
+      rgnSend_.alloc((size_t)nranks_ * maxOwned_ * (D + 1));
+      rgnGid_.upload(plan_.localNodes.data(), plan_.localNodes.size(), st_);
+      ownGidH_.assign(ownAllGidH_.begin() + (size_t)rank_ * maxOwned_,
+                      ownAllGidH_.begin() + (size_t)rank_ * maxOwned_ + std::max(nOwned_, 1));
+      rgnOwnGid_.upload(ownGidH_.data(), ownGidH_.size(), st_);
+      rgTmp_.alloc(gvals_.n);
+      rgTmp2_.alloc(gvals_.n);
+      MMX_HIP(hipHostMalloc((void**)&rgnHost_, sizeof(double) * ((size_t)256 * 3 * D + 2 * smallN * nranks_ + 64),
+                            hipHostMallocDefault));
+    }
+    double* H0 = rgnHost_;
+    // this rank's bounding box and widest simplex per axis
+    launch_bbox<D>(Vp_.p, nP_, rgnPart_.p, nbl, st_);
+    launch_extent<D>(Vp_.p, F_.p, nF_, rgnPart_.p + (size_t)256 * 2 * D, nbe, st_);
+    MMX_HIP(hipMemcpyAsync(H0, rgnPart_.p, sizeof(double) * nbl * 2 * D, hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipMemcpyAsync(H0 + (size_t)256 * 2 * D, rgnPart_.p + (size_t)256 * 2 * D, sizeof(double) * nbe * D,
+                           hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int b = 0; b < nbl; ++b)
+      for (int d = 0; d < D; ++d) {
+        llo[d] = std::min(llo[d], H0[(size_t)b * 2 * D + d]);
+        lhi[d] = std::max(lhi[d], H0[(size_t)b * 2 * D + D + d]);
+      }
+    for (int d = 0; d < D; ++d) extMax_[d] = 0.0;
+    for (int b = 0; b < nbe; ++b)
+      for (int d = 0; d < D; ++d) extMax_[d] = std::max(extMax_[d], H0[(size_t)256 * 2 * D + (size_t)b * D + d]);
+    // the global box: every vertex is some rank's, so the union of the ranks' boxes (min / max exact)
+    double* hs = H0 + (size_t)256 * 3 * D;  // small host staging
+    double* hr = hs + smallN;
+    auto smallGather = [&](const double* in, int n) {  // n doubles per rank -> hr[q * n + i]
+      MMX_HIP(hipMemcpyAsync(rgnSmallS_.p, in, sizeof(double) * n, hipMemcpyHostToDevice, st_));
+      comm_->allgather(rank_, rgnSmallS_.p, rgnSmallR_.p, (size_t)n, st_);
+      MMX_HIP(hipMemcpyAsync(hr, rgnSmallR_.p, sizeof(double) * n * nranks_, hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+    };
+    for (int d = 0; d < D; ++d) {
+      hs[d] = llo[d];
+      hs[D + d] = lhi[d];
+    }
+    smallGather(hs, 2 * D);
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int q = 0; q < nranks_; ++q)
+      for (int d = 0; d < D; ++d) {
+        lo[d] = std::min(lo[d], hr[(size_t)q * 2 * D + d]);
+        hi[d] = std::max(hi[d], hr[(size_t)q * 2 * D + D + d]);
+      }
+    setGridGeometry(nG, lo, hi);
+    const CellGrid cg = cellGrid(lo, hi);
+    int marg[3] = {0, 0, 0};
+    const GridBox R = rowBox(llo, lhi, marg);
+    const int passes = smoothPasses();
+    const GridBox H = widenBox(R, passes);
+    // the search box S: the grid points of H's rows widened by a simplex diameter and two cells (a
+    // point inside the mesh lies in some simplex, within its diameter of each of its vertices; the
+    // fill checks the margin point by point).  The fill gives storage row (sx, sy, k) the point
+    // (gx[sx], gy[sy], gz[k]) in 2D but (gx[sy], gy[sx], gz[k]) in 3D (the host layout's x/y swap,
+    // src/MeshInterpolator.cpp:234)
+    double slo[3] = {0, 0, 0}, shi[3] = {0, 0, 0};
+    double diam = 0.0;
+    for (int d = 0; d < D; ++d) diam += extMax_[d] * extMax_[d];
+    diam = std::sqrt(diam);
+    for (int d = 0; d < D; ++d) {
+      const std::vector<double>& g = d == 0 ? grid_.gx : d == 1 ? grid_.gy : grid_.gz;
+      const int sd = (D == 3 && d < 2) ? 1 - d : d;  // the storage axis holding coordinate axis d
+      const double mu = diam + 2.0 * (g[1] - g[0]);
+      slo[d] = g[H.lo[sd]] - mu;
+      shi[d] = g[H.hi[sd]] + mu;
+    }
+    for (int d = 0; d < D; ++d) {
+      hs[d] = slo[d];
+      hs[D + d] = shi[d];
+    }
+    smallGather(hs, 2 * D);
+    MMX_HIP(hipMemcpyAsync(rgnSbox_.p, hr, sizeof(double) * nranks_ * 2 * D, hipMemcpyHostToDevice, st_));
+    // my owned vertices in the other ranks' boxes, per destination
+    MMX_HIP(hipMemsetAsync(rgnCnt_.p, 0, sizeof(int) * (nranks_ + 1), st_));
+    launch_select_owned<D>(Vp_.p, ownLocal_.p, rgnOwnGid_.p, nOwned_, nranks_, rank_, rgnSbox_.p, rgnCnt_.p,
+                           rgnSend_.p, maxOwned_, st_);
+    std::vector<int> cnt(nranks_ + 1);
+    MMX_HIP(hipMemcpyAsync(cnt.data(), rgnCnt_.p, sizeof(int) * nranks_, hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    for (int q = 0; q < nranks_; ++q) hs[q] = (double)cnt[q];
+    smallGather(hs, nranks_);
+    std::vector<HaloPeer> peers;
+    int nRecv = 0;
+    for (int q = 0; q < nranks_; ++q) {
+      if (q == rank_) continue;
+      const int sc = cnt[q], rc = (int)hr[(size_t)q * nranks_ + rank_];
+      if (sc == 0 && rc == 0) continue;
+      HaloPeer p;
+      p.rank = q;
+      p.sendOff = q * maxOwned_;
+      p.sendCount = sc;
+      p.recvOff = nRecv;
+      p.recvCount = rc;
+      nRecv += rc;
+      peers.push_back(p);
+    }
+    const int nCand = nP_ + nRecv;
+    if ((int)rgnRecv_.n < std::max(nRecv, 1) * (D + 1)) rgnRecv_.alloc((size_t)std::max(nRecv, 1) * (D + 1) * 2);
+    if ((int)rgnCandX_.n < nCand * D) {
+      rgnCandX_.alloc((size_t)nCand * D * 2);
+      rgnCandGid_.alloc((size_t)nCand * 2);
+      rgnCellOf_.alloc((size_t)nCand * 2);
+      rgnNodes_.alloc((size_t)nCand * 2);
+      rgnMon_.alloc((size_t)nCand * DD * 2);
+    }
+    comm_->exchange(rank_, rgnSend_.p, rgnRecv_.p, peers, D + 1, st_);
+    launch_build_cand<D>(Vp_.p, rgnGid_.p, nP_, rgnRecv_.p, nRecv, rgnCandX_.p, rgnCandGid_.p, st_);
+    evalMonitorAt(rgnCandX_.p, nCand, t, rgnMon_.p);
+    ensureCells(cg);
+    launch_bin<D>(rgnCandX_.p, nCand, cg, rgnCellOf_.p, rgCounts_.p, rgStarts_.p, rgFill_.p, rgnNodes_.p, rgScan_.p,
+                  rgScanBytes_, st_);
+    NnCand nc{rgnCandGid_.p, {slo[0], slo[1], slo[2]}, {shi[0], shi[1], shi[2]}, rgnCnt_.p + nranks_};
+    launch_nn_fill<D>(rgnCandX_.p, cg, rgStarts_.p, rgnNodes_.p, gx_.p, gy_.p, D == 3 ? gz_.p : gy_.p, grid_.nx,
+                      grid_.ny, grid_.nz, rgnMon_.p, rgTmp_.p, H, st_, nc);
+    int fail = 0;
+    MMX_HIP(hipMemcpyAsync(&fail, rgnCnt_.p + nranks_, sizeof(int), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    hs[0] = (double)fail;
+    smallGather(hs, 1);
+    for (int q = 0; q < nranks_; ++q)
+      if (hr[q] != 0.0) return false;  // some point of some rank: rebuild from every vertex
+    smoothCommit(R, passes, true);
+    st_stats_.regrid_rows = (long long)(H.hi[0] - H.lo[0] + 1) * (H.hi[1] - H.lo[1] + 1) * (H.hi[2] - H.lo[2] + 1);
+    st_stats_.regrid_gather_bytes = (double)sizeof(double) * ((size_t)nranks_ * (4 * D + nranks_ + 1) +
+                                                              (size_t)nRecv * (D + 1));
+    st_stats_.regrid_cand = nCand;
+    MMX_HIP(hipGetLastError());
+    gridOnDevice_ = true;
+    m_ = makeView();
+    st_stats_.regrids += 1;
+    return true;
+  }
+
+  void setGridGeometry(int nG, const double* lo, const double* hi) {
+    grid_geometry(D, nG, lo, hi, grid_);
+    gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
+    gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
+    if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
+  }
+  // vertex cells over the global box: about two vertices per cell
+  CellGrid cellGrid(const double* lo, const double* hi) const {
+    CellGrid cg{};
+    const int gn[3] = {grid_.nx, grid_.ny, grid_.nz};
+    cg.hmin = INFINITY;
+    for (int d = 0; d < 3; ++d) {
+      const double ext = d < D ? hi[d] - lo[d] : 0.0;
+      cg.lo[d] = d < D ? lo[d] : 0.0;
+      cg.n[d] = (d < D && ext > 0) ? std::max(1, gn[d] / 2) : 1;
+      cg.inv[d] = (d < D && ext > 0) ? cg.n[d] / ext : 0.0;
+      if (d < D && ext > 0) cg.hmin = std::min(cg.hmin, ext / cg.n[d]);
+    }
+    if (!(cg.hmin < INFINITY)) cg.hmin = 0.0;
+    return cg;
+  }
+  void ensureCells(const CellGrid& cg) {
+    const int ncell = cg.n[0] * cg.n[1] * cg.n[2];
+    if ((int)rgStarts_.n < ncell + 1) {
+      rgCounts_.alloc(ncell + 1);
+      rgStarts_.alloc(ncell + 1);
+      rgFill_.alloc(ncell);
+      rgScanBytes_ = bin_scan_bytes(ncell);
+      rgScan_.alloc(std::max<size_t>(rgScanBytes_, 1));
+    }
+  }
+  static int smoothPasses() { return (D == 2) ? 5 : 2; }  // smoothMonitorGrid
+  // the grid rows this rank's monitor evaluations can reach: its vertices' bounding box widened by
+  // two local simplex extents and two cells (marg[d] rows) for the motion within a step
+  GridBox rowBox(const double* llo, const double* lhi, int* marg) const {
+    const int gn3[3] = {grid_.nx, grid_.ny, D == 3 ? grid_.nz : 0};
+    GridBox R{{0, 0, 0}, {gn3[0], gn3[1], gn3[2]}};
+    for (int d = 0; d < D; ++d) {  // evalMonitor reads rows zInd P + yInd (nx+1) + xInd: storage axis d = axis d
+      const std::vector<double>& g = d == 0 ? grid_.gx : d == 1 ? grid_.gy : grid_.gz;
+      const double h = g[1] - g[0];
+      const int M = (int)std::ceil(2.0 * extMax_[d] / h) + 2;
+      marg[d] = M;
+      R.lo[d] = std::max(0, std::min(gn3[d], (int)std::floor((llo[d] - g[0]) / h) - M));
+      R.hi[d] = std::max(0, std::min(gn3[d], (int)std::floor((lhi[d] - g[0]) / h) + 1 + M));
+    }
+    return R;
+  }
+  GridBox widenBox(const GridBox& b, int w) const {
+    const int gn3[3] = {grid_.nx, grid_.ny, D == 3 ? grid_.nz : 0};
+    GridBox o = b;
+    for (int d = 0; d < D; ++d) {
+      o.lo[d] = std::max(0, b.lo[d] - w);
+      o.hi[d] = std::min(gn3[d], b.hi[d] + w);
+    }
+    return o;
+  }
+  // the monitor at n vertices (MonitorFunction::evaluateAtVertices, src/MonitorFunction.cpp:16-32)
+  void evalMonitorAt(const double* X, int n, double t, double* mon) {
+    constexpr int DD = D * D;
+    if (builtin_monitor_kind(monFn_, monUser_) == 7) {
+      double c[3];
+      moving_bump_centre(t, c);
+      launch_monitor_tv<D>(X, n, c, mon, st_);
+    } else {  // a host plugin: evaluated on the host at the current vertices, as the reference does
+      std::vector<double> Xh((size_t)n * D), mv((size_t)n * DD);
+      MMX_HIP(hipMemcpyAsync(Xh.data(), X, Xh.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+      for (int v = 0; v < n; ++v) {
+        double M[9];
+        for (int i = 0; i < DD; ++i) M[i] = 0.0;
+        monFn_(D, &Xh[(size_t)v * D], M, monUser_);
+        std::memcpy(&mv[(size_t)v * DD], M, DD * sizeof(double));
+      }
+      MMX_HIP(hipMemcpyAsync(mon, mv.data(), mv.size() * sizeof(double), hipMemcpyHostToDevice, st_));
+      MMX_HIP(hipStreamSynchronize(st_));
+    }
+  }
+  // smoothing passes over the box (shrinking halo) and the commit: the rows of R (NaN elsewhere)
+  // on a partition, the whole grid on one rank
+  void smoothCommit(const GridBox& R, int passes, bool part) {
+    double* cur = rgTmp_.p;
+    double* oth = part ? rgTmp2_.p : gvals_.p;
+    for (int it = 0; it < passes; ++it) {
+      launch_smooth<D>(cur, oth, grid_.nx, grid_.ny, grid_.nz, widenBox(R, part ? passes - 1 - it : 0), st_);
+      std::swap(cur, oth);
+    }
+    if (part) {
+      launch_box_commit<D>(cur, gvals_.p, D == 3 ? gpad_.p : nullptr, grid_.nx, grid_.ny, grid_.nz, R, st_);
+    } else {
+      if (cur != gvals_.p)
+        MMX_HIP(hipMemcpyAsync(gvals_.p, cur, gvals_.n * sizeof(double), hipMemcpyDeviceToDevice, st_));
+      if (D == 3) launch_pad_rows(gvals_.p, (long long)(gvals_.n / 9), gpad_.p, st_);
+    }
+  }
+
+  // every vertex: on one rank its own; on a partition each rank's owned vertices all-gathered to
+  // every rank (the fallback of regridNear, and MMX_REGRID_GATHER=all)
+  void regridAll(double t) {
     constexpr int DD = D * D;
     const int nG = (nranks_ > 1) ? plan_.nP : nP_;  // vertices the grid is built from
     const int nb = std::max(1, std::min(256, (nG + 255) / 256));
@@ -921,6 +1183,7 @@ class Engine final : public EngineBase {
     }
     st_stats_.regrid_rows = (long long)(H.hi[0] - H.lo[0] + 1) * (H.hi[1] - H.lo[1] + 1) * (H.hi[2] - H.lo[2] + 1);
     st_stats_.regrid_gather_bytes = part ? (double)nranks_ * maxOwned_ * D * sizeof(double) : 0.0;
+    st_stats_.regrid_cand = part ? nG : 0;
     MMX_HIP(hipGetLastError());
     gridOnDevice_ = true;
     m_ = makeView();
@@ -1040,6 +1303,12 @@ class Engine final : public EngineBase {
   DevBuf<double> rgPart_, rgMon_, rgTmp_, rgTmp2_, rgXg_, rgSend_, rgRecv_;
   double extMax_[3] = {0.0, 0.0, 0.0};  // widest local simplex per axis (partitioned regrid box), per rebuild
   DevBuf<int> ownLocal_, ownAllGid_;  // partitioned regrid: my owned vertices (local ids), all ranks' (global ids)
+  std::vector<int> ownAllGidH_, ownGidH_;
+  // regridNear: partials, small all-gathers, search boxes, per-destination counts (+ the fail
+  // flag), send / receive rows {x, gid}, candidates (positions, global ids, cells, monitor)
+  DevBuf<double> rgnPart_, rgnSmallS_, rgnSmallR_, rgnSbox_, rgnSend_, rgnRecv_, rgnCandX_, rgnMon_;
+  DevBuf<int> rgnCnt_, rgnGid_, rgnOwnGid_, rgnCandGid_, rgnCellOf_, rgnNodes_;
+  double* rgnHost_ = nullptr;
   int nOwned_ = 0, maxOwned_ = 1;
   DevBuf<int> rgCellOf_, rgNodes_, rgCounts_, rgStarts_, rgFill_;
   DevBuf<unsigned char> rgScan_;

@@ -293,8 +293,9 @@ __device__ __forceinline__ double pow_dp2m1(double x, bool& tie) {
 // AdaptationFunctional<D>::blockGrad (src/AdaptationFunctional.cpp:102-287).
 // Returns the (regularised if REG) energy, sets Igt = |K| G, grad (if GRAD).
 // An inverted element (assert(Edet > 0), line 174) returns NaN and a NaN gradient.
-// ghuang (optional): receives the unregularised gradient |K| dG (K values) and Igt (entry K) --
-// the part of the result that depends on z alone, reused by the next prox at the same z.
+// ghuang (optional): receives the unregularised gradient |K| dG (K values) -- the part of the
+// result that depends on z alone, reused by the next prox at the same z.  (Igt is not kept: the
+// energy a prox reports is only read for the first prox of a step, which never uses the cache.)
 // EXACT = false (prox fast path): a power too close to a rounding midpoint, or outside the
 // double-double ranges, raises *tie instead of being resolved; the results are then void.
 template <int D, bool GRAD, bool REG, bool EXACT = true>
@@ -357,7 +358,7 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
       for (int i = 0; i < K; ++i) grad[i] = nan;
       if (ghuang)
 #pragma unroll
-        for (int i = 0; i <= K; ++i) ghuang[i] = nan;
+        for (int i = 0; i < K; ++i) ghuang[i] = nan;
     }
     Igt = nan;
     return nan;
@@ -459,7 +460,6 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
     if (ghuang) {
 #pragma unroll
       for (int i = 0; i < K; ++i) ghuang[i] = grad[i];
-      ghuang[K] = Igt;
     }
     if constexpr (REG) {
       Ih += 0.5 * fc.w * fc.w * sq;

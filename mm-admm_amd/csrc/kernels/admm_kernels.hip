@@ -798,10 +798,10 @@ __device__ __forceinline__ void entry_grad(const GridView<D>& g, const Functiona
   if (useCache) {
 #pragma unroll
     for (int i = 0; i < K; ++i) G[i] = cache[i];
-    Igt = cache[K];
+    Igt = 0.0;  // unused: a step reports the energy of its first prox, which never takes the cache
 #pragma unroll
     for (int i = 0; i < K; ++i) G[i] += fc.w * fc.w * (-dx[i] + z[i]);
-    bad |= (Igt != Igt);
+    bad |= (cache[0] != cache[0]);  // an inverted element's cached gradient is all NaN
   } else {
     const double e = blockGrad<D, true, true, EXACT>(g, fc, z, xi, dx, G, Igt, nullptr, tie);
     bad |= (e != e);
@@ -842,7 +842,7 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
   double G[K], G1[K], Igt;
   bool bad = false;
   (void)G1;
-  double* gc = m.gcache + (size_t)s * (K + 1);
+  double* gc = m.gcache + (size_t)s * K;
   entry_grad<D>(g, fc, z, xi, dx, gc, !FIRST && useCache, G, Igt, bad);
   zeroFixed<D>(G, fixedBits);
   const double Ihsave = Igt;
@@ -964,8 +964,8 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   const unsigned fixedBits = m.sbits[s] & 0xF;
   double* zs = zg + (size_t)s * K;
   double* us = ug + (size_t)s * K;
-  double* gc = m.gcache + (size_t)s * (K + 1);
-  double z[K], z0[K], dx[K], gcv[K + 1];
+  double* gc = m.gcache + (size_t)s * K;
+  double z[K], z0[K], dx[K], gcv[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     z[i] = zs[i];
@@ -974,7 +974,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   }
   if (useCache) {
 #pragma unroll
-    for (int i = 0; i <= K; ++i) gcv[i] = gc[i];
+    for (int i = 0; i < K; ++i) gcv[i] = gc[i];
   }
   // the chunk: BS/64 whole wave blocks (the buffer is padded to whole chunks of 256 simplices, so a
   // short last chunk copies -- and writes back unchanged -- its padding)
@@ -1089,8 +1089,8 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
   const unsigned fixedBits = m.sbits[s] & 0xF;
   double* zs = zg + (size_t)s * K;
   double* us = ug + (size_t)s * K;
-  double* gc = m.gcache + (size_t)s * (K + 1);
-  double z[K], dx[K], gcv[K + 1];
+  double* gc = m.gcache + (size_t)s * K;
+  double z[K], dx[K], gcv[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     z[i] = zs[i];
@@ -1098,7 +1098,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
   }
   if (!EXACT && useCache) {
 #pragma unroll
-    for (int i = 0; i <= K; ++i) gcv[i] = gc[i];
+    for (int i = 0; i < K; ++i) gcv[i] = gc[i];
   }
   double xi[K];
   if constexpr (COMP) gatherX<D>(m.Vc, f, xi);
@@ -1332,7 +1332,6 @@ __device__ __forceinline__ double blockGradQuad(const GridView<3>& g, const Func
     if (ghuang) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) ghuang[3 * k + c] = nan;
-      if (k == 0) ghuang[12] = nan;
     }
     Igt = nan;
     return nan;
@@ -1418,7 +1417,6 @@ __device__ __forceinline__ double blockGradQuad(const GridView<3>& g, const Func
   if (ghuang) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) ghuang[3 * k + c] = go[c];
-    if (k == 0) ghuang[12] = Igt;
   }
   Ih += 0.5 * fc.w * fc.w * sq;
 #pragma unroll
@@ -1458,7 +1456,7 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
     const bool ownFixed = (fixedBits >> k) & 1u;
     double* zs = zg + (size_t)s * K + 3 * k;
     double* us = ug + (size_t)s * K + 3 * k;
-    double* gc = m.gcache + (size_t)s * (K + 1);
+    double* gc = m.gcache + (size_t)s * K;
     double zo[3], z0[3], dxo[3], go[3], Igt = 0.0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -1470,7 +1468,6 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
     if (cached) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) go[c] = gc[3 * k + c];
-      Igt = gc[K];
     }
     double xi[K];
     if constexpr (COMP) {
@@ -1503,7 +1500,7 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
       if (cached) {  // entry_grad with the cache: the unregularised part plus the regulariser
 #pragma unroll
         for (int c = 0; c < 3; ++c) go[c] += fc.w * fc.w * (-dxo[c] + zo[c]);
-        bad |= (Igt != Igt);
+        bad |= (go[0] != go[0]);  // an inverted element's cached gradient is all NaN
       } else {
         double zf[K];
         qfull(zo, zf);

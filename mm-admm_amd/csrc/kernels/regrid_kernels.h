@@ -37,12 +37,29 @@ size_t bin_scan_bytes(int ncell);
 // MonType 7 at the vertices, centre c[3] of the moving bump at the current time
 template <int D>
 void launch_monitor_tv(const double* X, int n, const double* c, double* monVals, hipStream_t st);
+// candidates of a partitioned regrid: global ids (the tie rule) and the search box S they were
+// gathered from; every grid point checks its nearest candidate is strictly nearer than S's
+// boundary, else *fail is set (gid == nullptr: every vertex, indexed by global id)
+struct NnCand {
+  const int* gid;
+  double slo[3], shi[3];
+  int* fail;
+};
 // nearest vertex of the grid point of every row in `box` -> its monitor value (host layout: 3D
 // rows swap x and y, src/MeshInterpolator.cpp:234); rows enumerated in storage order
 template <int D>
 void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, const int* cellNodes, const double* gx,
                     const double* gy, const double* gz, int nx, int ny, int nz, const double* monVals, double* vals,
-                    const GridBox& box, hipStream_t st);
+                    const GridBox& box, hipStream_t st, const NnCand& cand = NnCand{nullptr, {0, 0, 0}, {0, 0, 0}, nullptr});
+// partitioned regrid: owned vertices inside other ranks' search boxes (sboxes: nranks x {lo[D],
+// hi[D]}) appended as rows {x[D], gid} to send block q (rows q*cap ..); counts[q] must start at 0
+template <int D>
+void launch_select_owned(const double* X, const int* ownLocal, const int* ownGid, int nOwned, int nranks, int rank,
+                         const double* sboxes, int* counts, double* send, int cap, hipStream_t st);
+// candidates = this rank's vertices (X, gidLocal) then the received rows {x[D], gid}
+template <int D>
+void launch_build_cand(const double* X, const int* gidLocal, int nLocal, const double* recv, int nRecv, double* cx,
+                       int* cgid, hipStream_t st);
 // one Jacobi smoothing pass in -> out over the rows of `box` (the others are not written)
 template <int D>
 void launch_smooth(const double* in, double* out, int nx, int ny, int nz, const GridBox& box, hipStream_t st);

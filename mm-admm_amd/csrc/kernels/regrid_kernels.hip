@@ -166,13 +166,18 @@ __device__ __forceinline__ long long box_rows(const GridBox& b) {
 // the host set-up's layout: 2D row j(nx+1) + i holds point (i, j); 3D row (nx+1)(ny+1)k + i(nx+1) + j
 // holds point (i, j, k) (src/MeshInterpolator.cpp:234: x and y swapped), i.e. storage (sx, sy) is
 // point (sy, sx).
+// Candidates restricted to a search box S (partitioned regrid, cand != nullptr): vertices are
+// compared by their global ids cand->gid (the host's lowest-id tie rule), and every grid point
+// checks that its nearest candidate is strictly nearer than the boundary of S -- no vertex outside
+// S (which this rank does not hold) can then be as near; otherwise *cand->fail is set and the
+// caller rebuilds from every vertex.
 template <int D>
 __global__ void __launch_bounds__(kRB) k_nn_fill(const double* __restrict__ X, CellGrid cg,
                                                  const int* __restrict__ starts, const int* __restrict__ cellNodes,
                                                  const double* __restrict__ gx, const double* __restrict__ gy,
                                                  const double* __restrict__ gz, int nx, int ny, int nz,
                                                  const double* __restrict__ monVals, double* __restrict__ vals,
-                                                 GridBox box) {
+                                                 GridBox box, NnCand cand) {
   constexpr int DD = D * D;
   const long long p = (long long)blockIdx.x * kRB + threadIdx.x;
   if (p >= box_rows(box)) return;
@@ -183,7 +188,7 @@ __global__ void __launch_bounds__(kRB) k_nn_fill(const double* __restrict__ X, C
   int c[3] = {0, 0, 0};
   cellOf<D>(q, cg, c);
   double best = INFINITY;
-  int bi = -1;
+  int bi = -1, bg = -1;  // nearest candidate: index, global id (tie rule)
   int rmax = 0;
 #pragma unroll
   for (int d = 0; d < D; ++d) rmax = max(rmax, max(c[d], cg.n[d] - 1 - c[d]));
@@ -199,15 +204,17 @@ __global__ void __launch_bounds__(kRB) k_nn_fill(const double* __restrict__ X, C
           const int cell = (cz * cg.n[1] + cy) * cg.n[0] + cx;
           for (int t = starts[cell]; t < starts[cell + 1]; ++t) {
             const int v = cellNodes[t];
+            const int gv = cand.gid ? cand.gid[v] : v;
             double dd = 0.0;
 #pragma unroll
             for (int d = 0; d < D; ++d) {
               const double df = q[d] - X[(size_t)v * D + d];
               dd += df * df;
             }
-            if (dd < best || (dd == best && v < bi)) {
+            if (dd < best || (dd == best && gv < bg)) {
               best = dd;
               bi = v;
+              bg = gv;
             }
           }
         }
@@ -216,8 +223,65 @@ __global__ void __launch_bounds__(kRB) k_nn_fill(const double* __restrict__ X, C
     const double lb = ((double)r - 1e-6) * cg.hmin;
     if (bi >= 0 && r > 0 && best < lb * lb) break;
   }
+  if (cand.gid) {
+    double gap = INFINITY;  // distance from q to the outside of the search box
+#pragma unroll
+    for (int d = 0; d < D; ++d) gap = fmin(gap, fmin(q[d] - cand.slo[d], cand.shi[d] - q[d]));
+    if (!(bi >= 0 && gap > 0.0 && best < gap * gap * (1.0 - 1e-9))) {
+      atomicOr(cand.fail, 1);
+      if (bi < 0) return;
+    }
+  }
 #pragma unroll
   for (int e = 0; e < DD; ++e) vals[row * DD + e] = monVals[(size_t)bi * DD + e];
+}
+
+// partitioned regrid: this rank's owned vertices inside another rank's search box S_q are appended
+// (position, global id) to the send block of rank q (rows of D + 1 doubles at q * cap)
+template <int D>
+__global__ void __launch_bounds__(kRB) k_select_owned(const double* __restrict__ X, const int* __restrict__ ownLocal,
+                                                      const int* __restrict__ ownGid, int nOwned, int nranks, int rank,
+                                                      const double* __restrict__ sboxes, int* __restrict__ counts,
+                                                      double* __restrict__ send, int cap) {
+  const int i = blockIdx.x * kRB + threadIdx.x;
+  if (i >= nOwned) return;
+  const int v = ownLocal[i];
+  double x[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) x[d] = X[(size_t)v * D + d];
+  for (int q = 0; q < nranks; ++q) {
+    if (q == rank) continue;
+    const double* s = sboxes + (size_t)q * 2 * D;
+    bool in = true;
+#pragma unroll
+    for (int d = 0; d < D; ++d) in = in && x[d] >= s[d] && x[d] <= s[D + d];
+    if (in) {
+      const int k = atomicAdd(&counts[q], 1);
+      double* r = send + ((size_t)q * cap + k) * (D + 1);
+#pragma unroll
+      for (int d = 0; d < D; ++d) r[d] = x[d];
+      r[D] = (double)ownGid[i];
+    }
+  }
+}
+
+// the candidates: this rank's vertices (positions, global ids) then the received rows
+template <int D>
+__global__ void __launch_bounds__(kRB) k_build_cand(const double* __restrict__ X, const int* __restrict__ gidLocal,
+                                                    int nLocal, const double* __restrict__ recv, int nRecv,
+                                                    double* __restrict__ cx, int* __restrict__ cgid) {
+  const int i = blockIdx.x * kRB + threadIdx.x;
+  if (i >= nLocal + nRecv) return;
+  if (i < nLocal) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) cx[(size_t)i * D + d] = X[(size_t)i * D + d];
+    cgid[i] = gidLocal[i];
+  } else {
+    const double* r = recv + (size_t)(i - nLocal) * (D + 1);
+#pragma unroll
+    for (int d = 0; d < D; ++d) cx[(size_t)i * D + d] = r[d];
+    cgid[i] = (int)r[D];
+  }
 }
 
 // smoothMonitorGrid (src/MeshInterpolator.cpp:366-404): one Jacobi pass, interior points
@@ -327,11 +391,27 @@ static long long host_box_rows(const GridBox& b) {
 template <int D>
 void launch_nn_fill(const double* X, const CellGrid& cg, const int* starts, const int* cellNodes, const double* gx,
                     const double* gy, const double* gz, int nx, int ny, int nz, const double* monVals, double* vals,
-                    const GridBox& box, hipStream_t st) {
+                    const GridBox& box, hipStream_t st, const NnCand& cand) {
   const long long n = host_box_rows(box);
   if (n > 0)
     hipLaunchKernelGGL(k_nn_fill<D>, dim3(blocks(n)), dim3(kRB), 0, st, X, cg, starts, cellNodes, gx, gy, gz, nx, ny,
-                       nz, monVals, vals, box);
+                       nz, monVals, vals, box, cand);
+}
+
+template <int D>
+void launch_select_owned(const double* X, const int* ownLocal, const int* ownGid, int nOwned, int nranks, int rank,
+                         const double* sboxes, int* counts, double* send, int cap, hipStream_t st) {
+  if (nOwned > 0)
+    hipLaunchKernelGGL(k_select_owned<D>, dim3(blocks(nOwned)), dim3(kRB), 0, st, X, ownLocal, ownGid, nOwned, nranks,
+                       rank, sboxes, counts, send, cap);
+}
+
+template <int D>
+void launch_build_cand(const double* X, const int* gidLocal, int nLocal, const double* recv, int nRecv, double* cx,
+                       int* cgid, hipStream_t st) {
+  if (nLocal + nRecv > 0)
+    hipLaunchKernelGGL(k_build_cand<D>, dim3(blocks(nLocal + nRecv)), dim3(kRB), 0, st, X, gidLocal, nLocal, recv,
+                       nRecv, cx, cgid);
 }
 
 template <int D>
@@ -362,7 +442,11 @@ void launch_rows_scatter(int D, const int* idx, int n, const double* in, double*
   template void launch_monitor_tv<D>(const double*, int, const double*, double*, hipStream_t);                  \
   template void launch_nn_fill<D>(const double*, const CellGrid&, const int*, const int*, const double*,        \
                                   const double*, const double*, int, int, int, const double*, double*,          \
-                                  const GridBox&, hipStream_t);                                                \
+                                  const GridBox&, hipStream_t, const NnCand&);                                 \
+  template void launch_select_owned<D>(const double*, const int*, const int*, int, int, int, const double*, int*, \
+                                       double*, int, hipStream_t);                                               \
+  template void launch_build_cand<D>(const double*, const int*, int, const double*, int, double*, int*,          \
+                                     hipStream_t);                                                               \
   template void launch_smooth<D>(const double*, double*, int, int, int, const GridBox&, hipStream_t);           \
   template void launch_box_commit<D>(const double*, double*, double*, int, int, int, const GridBox&, hipStream_t);
 MMX_REGRID_INST(2)

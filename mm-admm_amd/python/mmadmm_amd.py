@@ -50,7 +50,8 @@ class mmadmm_stats(ctypes.Structure):
                 ("newton_iters", ctypes.c_longlong), ("jacobians", ctypes.c_longlong),
                 ("cg_iters", ctypes.c_longlong), ("t_jac_ms", ctypes.c_double), ("t_solve_ms", ctypes.c_double),
                 ("t_be_ms", ctypes.c_double), ("regrids", ctypes.c_longlong), ("regrid_rows", ctypes.c_longlong),
-                ("regrid_gather_bytes", ctypes.c_double)]
+                ("regrid_gather_bytes", ctypes.c_double), ("regrid_cand", ctypes.c_longlong),
+                ("regrid_fallbacks", ctypes.c_longlong)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

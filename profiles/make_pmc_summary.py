@@ -55,7 +55,8 @@ def load_f64(path):
     return out
 
 
-def main(fetch, write, f64=None):
+def main(fetch, write, f64=None, *tagged):
+    """tagged: "name=path" f64 passes of single workloads, summarised as "<kernel>@name" (largest grid)"""
     f, w = load(fetch), load(write)
     fl = load_f64(f64) if f64 else {}
     out = {"source": [os.path.relpath(p) for p in (fetch, write, f64) if p], "units": "bytes per launch",
@@ -80,10 +81,19 @@ def main(fetch, write, f64=None):
         if len(grids) > 1:
             e["by_grid"] = {str(g): entry(k, g) for g in grids[1:]}
         out[short(k)] = e
+    for t in tagged:
+        name, path = t.split("=", 1)
+        out["source"].append(os.path.relpath(path))
+        best = {}
+        for (k, g), v in load_f64(path).items():
+            if k.startswith(("void mmx::", "mmx::")) and g >= best.get(k, (0, 0))[0]:
+                best[k] = (g, v)
+        for k, (g, v) in best.items():
+            out[short(k) + "@" + name] = {"grid_size": g, "fp64_flops_per_launch": v}
     here = os.path.dirname(os.path.abspath(__file__))
     with open(os.path.join(here, "pmc_summary.json"), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:])

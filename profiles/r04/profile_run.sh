@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-4 rocprofv3 evidence, each pass its own run (MI355X_MICROARCH.md: no --pmc together with
+# tracing domains; one counter block per pass): kernel trace + stats of the bench, then FETCH_SIZE,
+# WRITE_SIZE and the fp64-instruction pass of the bench without the BFGS-heavy section, then the
+# fp64 pass of the BFGS-heavy section alone.  Output under gpurun_out/r4prof/.
+set -o pipefail
+cd "$(dirname "$0")/../.."
+export TMPDIR=/tmp
+O=gpurun_out/r4prof
+mkdir -p $O
+B="bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $O/kt -o run -- python3 $B > $O/bench_under_rocprof.json 2> $O/kt.err || exit $?
+timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o run -- python3 $B --no-bfgs > /dev/null 2> $O/fetch.err || exit $?
+timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write -o run -- python3 $B --no-bfgs > /dev/null 2> $O/write.err || exit $?
+timeout -s KILL 400 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 -f csv -d $O/f64 -o run -- python3 $B --no-bfgs > /dev/null 2> $O/f64.err || exit $?
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 -f csv -d $O/f64b -o run -- python3 profiles/r04/bfgs_only.py > $O/bfgs_only.json 2> $O/f64b.err

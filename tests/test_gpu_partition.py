@@ -108,11 +108,17 @@ def _check_rank_grid(e, gr, r):
     assert 0 < st["regrid_rows"] <= len(g) // (e.dim * e.dim)
 
 
+@pytest.mark.parametrize("gather", ["near", "all"])
 @pytest.mark.parametrize("mon,dim,nranks,n", [(7, 2, 2, 12), (1, 2, 3, 12), (7, 3, 2, 4), (7, 2, 4, 40), (7, 3, 4, 10)])
-def test_partitioned_regrid_equals_single(mx, mon, dim, nranks, n):
-    """Time-varying monitor on a partition: every rank all-gathers the vertex positions and
-    rebuilds the grid rows its simplices can reach (NaN elsewhere); node positions stay
-    bit-identical to the single-GPU run."""
+def test_partitioned_regrid_equals_single(mx, mon, dim, nranks, n, gather, monkeypatch):
+    """Time-varying monitor on a partition: every rank rebuilds the grid rows its simplices can
+    reach (NaN elsewhere) from the vertices near them (gather "near": the ranks exchange only the
+    owned vertices inside each other's search boxes; "all": every owned vertex all-gathered, the
+    fallback); node positions stay bit-identical to the single-GPU run."""
+    if gather == "all":
+        monkeypatch.setenv("MMX_REGRID_GATHER", "all")
+    else:
+        monkeypatch.delenv("MMX_REGRID_GATHER", raising=False)
     mesh = mx.MeshData.rect(dim, n)
     M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, mon), rho=200.0, tau=0.5, device=0)
     ref = mx.Engine(M, 0.05)
@@ -137,7 +143,10 @@ def test_partitioned_regrid_equals_single(mx, mon, dim, nranks, n):
     for r, e in enumerate(parts):
         _check_rank_grid(e, gr, r)
         assert np.array_equal(e.get("x").reshape(-1, dim), xr[e.local_nodes()]), f"rank {r}: positions differ"
-        assert e.stats()["regrids"] == steps
+        st = e.stats()
+        assert st["regrids"] == steps
+        if gather == "near":  # the candidate exchange sufficed at every rebuild
+            assert st["regrid_fallbacks"] == 0 and 0 < st["regrid_cand"] <= mesh.nP + e.nP, st
     for e in parts:
         e.close()
     comm.close()
@@ -179,7 +188,7 @@ def test_partitioned_regrid_long_run_equals_single(mx, dim, n, nranks):
         ids = e.local_nodes()
         for k in range(steps):
             assert np.array_equal(got[r][k], xs[k][ids]), f"rank {r} step {k}: positions differ"
-        assert e.stats()["regrids"] == steps
+        assert e.stats()["regrids"] == steps and e.stats()["regrid_fallbacks"] == 0
         e.close()
     comm.close()
     ref.close()
@@ -208,7 +217,11 @@ def test_c4_eight_ranks_regrid_equals_single(mx):
     for r, e in enumerate(parts):
         assert np.array_equal(e.get("x").reshape(-1, 3), xr[e.local_nodes()]), f"rank {r}: positions differ"
         _check_rank_grid(e, gr, r)
-        assert e.stats()["regrid_rows"] < 0.5 * total, (r, e.stats()["regrid_rows"], total)
+        st = e.stats()
+        assert st["regrid_rows"] < 0.5 * total, (r, st["regrid_rows"], total)
+        # only the vertices near the rank's box travel: a fraction of the all-gather's bytes
+        assert st["regrid_fallbacks"] == 0 and st["regrid_cand"] < 0.5 * mesh.nP, st
+        assert st["regrid_gather_bytes"] < 0.5 * 8 * 3 * mesh.nP, st
         e.close()
     comm.close()
 
