@@ -203,3 +203,21 @@ def test_meshutils_header():
     assert r.returncode == 0, r.stderr
     lines = r.stdout.strip().splitlines()
     assert len(lines) == 7 and all(" ok" in ln for ln in lines), r.stdout
+
+
+def test_matrixiter_header():
+    """include/mmadmm/MatrixIter.h (SparseItObj::MatrixStruc / ParamIter / MatrixIter / General_Exception,
+    lib/LASolver/MatrixIter.h:66-383) compiles with the reference's names and behaves as the reference on
+    the host: the pattern MatrixStruc packs, the General_Exception cases, ParamIter's defaults; a
+    MatrixIter needs the device (on a GPU box its host accessors are checked too)."""
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, "matrixiter_check")
+    cmd = ["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wall", "-Wno-unused-variable",
+           "-I", os.path.join(INC, "mmadmm"), os.path.join(ROOT, "tests", "cpp", "matrixiter_check.cpp"), "-o", exe,
+           "-L", os.path.join(ROOT, "mm-admm_amd", "lib"), "-lmmadmm", "-Wl,-rpath,$ORIGIN/../../mm-admm_amd/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) >= 7 and all(" ok" in ln for ln in lines), r.stdout
