@@ -189,7 +189,7 @@ class Engine final : public EngineBase {
        // 0.36 -> 0.18 ms; 2D C3: prox +0.027 ms, x-update -0.024 ms); MMX_TSLOT=0/1 overrides
       const char* ts = getenv("MMX_TSLOT");
       tslotOn_ = ts ? atoi(ts) != 0 : (D == 3);
-      if (tslotOn_) tslot_.alloc(std::max<size_t>((size_t)nF_ * (D + 1) * 4, 1));  // room for the padded layout
+      if (tslotOn_) tslot_.alloc(std::max<size_t>((size_t)nF_ * K, 1));
     }
     {  // x-update order: nodes by their first incident (local) simplex, then id -- locality of the
        // slot gathers when the node numbering is not simplex-ordered (e.g. cell centres numbered last)

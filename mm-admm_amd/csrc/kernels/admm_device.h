@@ -44,22 +44,6 @@ __device__ __forceinline__ double gridCoord(double a, double span, double ns, do
 template <int D>
 constexpr double kRecipD1 = 1.0 / ((double)D + 1.0);  // RN(1/(D+1))
 
-// x / (D + 1).  3D: a division by 4, exact as a multiplication (the compiler does so).  2D, fast
-// path (EXACT = false, MMX_DIV3_MK): Markstein's correction from RN(1/3) (div_mk, correctly rounded
-// for x = +-0 or |x| in [2^-900, 2^900]); outside that range the block takes the exact path (tie)
-#ifndef MMX_DIV3_MK
-#define MMX_DIV3_MK 0
-#endif
-template <int D, bool EXACT>
-__device__ __forceinline__ double divD1(double x, bool& tie) {
-  if constexpr (D == 2 && !EXACT && MMX_DIV3_MK) {
-    tie = tie || mk_exp(x, 900) > 1799u;
-    return div_mk(x, 3.0, kRecip3);
-  } else {
-    return x / ((double)D + 1.0);
-  }
-}
-
 template <int D>
 struct FunctionalConsts {
   double Ehat[D * D];  // row-major, !CompMesh reference simplex (host computed, std::pow)
@@ -355,7 +339,7 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
 #pragma unroll
   for (int r = 0; r < D; ++r)
 #pragma unroll
-    for (int c = 0; c < D; ++c) Minv.m[r][c] = divD1<D, EXACT>(Minv.m[r][c], tie);
+    for (int c = 0; c < D; ++c) Minv.m[r][c] = Minv.m[r][c] / ((double)D + 1);
   M<D> E, Ehat;
 #pragma unroll
   for (int j = 0; j < D; ++j) {
@@ -456,7 +440,7 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
 #pragma unroll
     for (int n = 0; n < D; n++)
 #pragma unroll
-      for (int c = 0; c < D; ++c) vLoc.m[n][c] -= divD1<D, EXACT>(basisComb[c], tie);
+      for (int c = 0; c < D; ++c) vLoc.m[n][c] -= (basisComb[c]) / ((double)D + 1.0);
 #pragma unroll
     for (int c = 0; c < D; ++c) {
       double s = 0.0;

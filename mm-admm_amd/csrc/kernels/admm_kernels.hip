@@ -138,43 +138,15 @@ __device__ __forceinline__ void loadXi(const DeviceMesh<D>& m, const int (&f)[D 
   if (m.compMesh) gatherX<D>(m.Vc, f, xi);
 }
 
-// the x-update's term of the simplex's slots (DeviceMesh::tslot): the same expression the
-// x-update forms from z and u (bit-identical).  Layout: the slots of simplex s at s * kTsStride,
-// slot n at n * kTsSlot; 3D with MMX_TSLOT_PAD: four doubles per slot (the fourth 0), so a
-// tetrahedron's four slots are one 128-byte line and a slot is two 16-byte loads
-#ifndef MMX_TSLOT_PAD
-#define MMX_TSLOT_PAD 0
-#endif
-template <int D>
-constexpr int kTsSlot = (D == 3 && MMX_TSLOT_PAD) ? 4 : D;
-template <int D>
-constexpr int kTsStride = (D + 1) * kTsSlot<D>;
-// slot offset s K + n D in z's layout (the incidence's) -> its offset in the tslot layout
-template <int D>
-__device__ __forceinline__ int tslot_off(int off) {
-  if constexpr (kTsSlot<D> == D) return off;
-  else return (off / D) * kTsSlot<D>;
-}
+// the x-update's term of the simplex's slots (DeviceMesh::tslot, the layout of z): the same
+// expression the x-update forms from z and u (bit-identical)
 template <int D>
 __device__ __forceinline__ void write_tslot(const DeviceMesh<D>& m, int s, const double* z, const double* u) {
   if (!m.tslot) return;
   constexpr int K = D * (D + 1);
-  double* ts = m.tslot + (size_t)s * kTsStride<D>;
-  if constexpr (kTsSlot<D> == D) {
+  double* ts = m.tslot + (size_t)s * K;
 #pragma unroll
-    for (int i = 0; i < K; ++i) ts[i] = m.w * (m.w * (z[i] - u[i]));
-  } else {
-    typedef double v2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int n = 0; n < D + 1; ++n) {
-      double t[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int c = 0; c < D; ++c) t[c] = m.w * (m.w * (z[n * D + c] - u[n * D + c]));
-      v2* p = reinterpret_cast<v2*>(ts + n * kTsSlot<D>);
-      p[0] = v2{t[0], t[1]};
-      p[1] = v2{t[2], t[3]};
-    }
-  }
+  for (int i = 0; i < K; ++i) ts[i] = m.w * (m.w * (z[i] - u[i]));
 }
 
 // z = D x (Dmat * x, src/MeshIntegrator.cpp:121,126): exact gather into simplex copies
@@ -281,22 +253,9 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
       for (int j = 0; j < CH; ++j) {
         const bool loc = off[j] >= 0;
         if constexpr (TS) {  // the prox's terms; another rank's slot from `remote`
-          const double* pt = loc ? m.tslot + tslot_off<D>(off[j]) : m.remote + (size_t)(-1 - off[j]) * D;
-          if constexpr (kTsSlot<D> == 4) {  // padded: two 16-byte loads per slot
-            typedef double v2 __attribute__((ext_vector_type(2)));
-            if (loc) {
-              const v2 a = reinterpret_cast<const v2*>(pt)[0], b = reinterpret_cast<const v2*>(pt)[1];
-              zv[j][0] = a.x;
-              zv[j][1] = a.y;
-              zv[j][2] = b.x;
-            } else {
+          const double* pt = loc ? m.tslot + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
 #pragma unroll
-              for (int c = 0; c < D; ++c) zv[j][c] = pt[c];
-            }
-          } else {
-#pragma unroll
-            for (int c = 0; c < D; ++c) zv[j][c] = pt[c];
-          }
+          for (int c = 0; c < D; ++c) zv[j][c] = pt[c];
         } else {
           const double* pz = loc ? z + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
           const double* pu = loc ? u + off[j] : pz;
@@ -1719,7 +1678,7 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
         const double un = dxo[c] - zo[c];  // uBar = DXpU - z
         zs[c] = zo[c];
         us[c] = un;
-        if (m.tslot) m.tslot[(size_t)s * kTsStride<3> + kTsSlot<3> * k + c] = m.w * (m.w * (zo[c] - un));
+        if (m.tslot) m.tslot[(size_t)s * K + 3 * k + c] = m.w * (m.w * (zo[c] - un));
       }
     }
     if constexpr (EXACT) __syncthreads();  // (the fast path's __syncthreads_or orders the image)
