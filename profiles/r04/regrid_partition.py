@@ -30,7 +30,10 @@ for wl, n in (("c4", 63), ("c5", 136)):
                 os.environ.pop("MMX_REGRID_GATHER", None)
             t0 = time.perf_counter()
             comm = mx.Comm.loopback(N)
-            eng = [mx.Engine(M, 0.025, rank=r, nranks=N, comm=comm) for r in range(N)]
+            eng = []
+            for r in range(N):
+                eng.append(mx.Engine(M, 0.025, rank=r, nranks=N, comm=comm))
+                print(f"{wl} N={N} {mode}: rank {r} set up", file=sys.stderr, flush=True)
             setup = time.perf_counter() - t0
             for e in eng:
                 e.set_regrid(True)
