@@ -14,8 +14,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "admm_device.h"
 #include "admm_kernels.h"
@@ -503,6 +505,26 @@ __device__ __forceinline__ size_t bidx(int s, int ij) {
 #define MMX_ROW_FENCE(BA) \
   if constexpr (BA::kRowFence) __builtin_amdgcn_sched_barrier(0)
 
+// Timing probe (build option -DMMX_WAVE_PROF, never in the product build): per-block shader-clock
+// stamps of the phases of the 3D steady prox's first BFGS iteration, written by lane 0 with a
+// vector store; the host side is mmx_wprof_dump (below).  `dep` is a value the phase produces, so
+// the stamp is taken once it is available.
+#ifdef MMX_WAVE_PROF
+__device__ unsigned long long* g_wprof;
+#define WPROF(slot, dep)                                                                     \
+  do {                                                                                       \
+    asm volatile("" ::"v"(dep));                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    const unsigned long long t_ = __builtin_readcyclecounter();                              \
+    if (threadIdx.x == 0 && g_wprof) g_wprof[(size_t)blockIdx.x * 8 + (slot)] = t_;          \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+  } while (0)
+#else
+#define WPROF(slot, dep) \
+  do {                   \
+  } while (0)
+#endif
+
 template <int K, class BA>
 __device__ __forceinline__ void load_row(const BA& B, int i, double (&r)[K]) {
 #pragma unroll
@@ -655,12 +677,18 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
       pk[i] = sacc;
     }
     MMX_ROW_FENCE(BA);
+    if constexpr (BA::kPipe > 0 && !EXACT) {
+      if (iter == 0) WPROF(2, pk[K - 1]);
+    }
 #pragma unroll
     for (int i = 0; i < K; ++i) z[i] += pk[i];
     double G1[K], Igt;
     {
       const double e = blockGrad<D, true, true, EXACT>(g, fc, z, xi, dx, G1, Igt, gcache, tie);
       bad |= (e != e);
+    }
+    if constexpr (BA::kPipe > 0 && !EXACT) {
+      if (iter == 0) WPROF(3, G1[K - 1]);
     }
     if constexpr (!EXACT) {
       if (*tie) break;
@@ -710,6 +738,9 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
     }
     MMX_ROW_FENCE(BA);
     const double c1 = (c2 + yBy) / cr_pow_2(c2);
+    if constexpr (BA::kPipe > 0 && !EXACT) {
+      if (iter == 0) WPROF(4, c1);
+    }
     // fast path (EXACT = false): the 2 K^2 divisions by c2 below by Markstein's correction from
     // one reciprocal (div_mk, bit-identical inside the ranges checked after the pass; outside
     // them the block is recomputed exactly, as for a near-midpoint power)
@@ -770,6 +801,9 @@ __device__ __forceinline__ int bfgs_iterations(BA B, const GridView<D>& g, const
       }
     }
     MMX_ROW_FENCE(BA);
+    if constexpr (BA::kPipe > 0 && !EXACT) {
+      if (iter == 0) WPROF(5, fin);
+    }
     B.advance();
     if constexpr (!EXACT) {
       // div_mk's ranges: c2 in [2^-100, 2^100]; by = 0 or in [2^-900, 2^900]; p_i yB_j likewise,
@@ -1084,6 +1118,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
   const int s0 = lb * 64;
   const bool act = s0 + tid < m.nF;
   const int s = act ? s0 + tid : s0;
+  if constexpr (!EXACT) WPROF(0, s);
   int f[D + 1];
   loadVerts<D>(m, s, f);
   const unsigned fixedBits = m.sbits[s] & 0xF;
@@ -1133,6 +1168,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     entry_grad<D, EXACT>(g, fc, z, xi, dx, gcv, !EXACT && useCache != 0, G, Igt, bad, &tie);
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
+    if constexpr (!EXACT) WPROF(1, G[K - 1]);
     const size_t gb = (size_t)lb * KK * 64 + tid;
     int its;
     {
@@ -1171,6 +1207,10 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     write_tslot<D>(m, s, z, un);
   }
   block_partials<6, 64>(pv, partials, lb);
+  if constexpr (!EXACT) {
+    __builtin_amdgcn_s_waitcnt(0);
+    WPROF(6, pv[0]);
+  }
 }
 
 template <int D, bool COMP>
@@ -2122,9 +2162,24 @@ constexpr int kFixGrid = 256;  // workgroups of the exact (tie) recomputation: a
 #endif
 constexpr int kQuadTets = MMX_QUAD_TETS;  // tets per k_prox_quad workgroup (64: 4.03 ms at C4, 16: 4.37 ms)
 
+#ifdef MMX_WAVE_PROF
+static unsigned long long* g_wprofHost = nullptr;
+static size_t g_wprofN = 0;
+static void wprof_arm(int nblocks) {
+  if (g_wprofN >= (size_t)nblocks * 8) return;
+  if (g_wprofHost) (void)hipFree(g_wprofHost);
+  g_wprofN = (size_t)nblocks * 8;
+  (void)hipMalloc((void**)&g_wprofHost, g_wprofN * sizeof(unsigned long long));
+  (void)hipMemset(g_wprofHost, 0, g_wprofN * sizeof(unsigned long long));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), &g_wprofHost, sizeof(g_wprofHost));
+}
+#endif
 template <int D>
 void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, const double* x, double* z, double* u,
                  const double* Bin, double* Bout, double* partials, int* nblocks, hipStream_t st) {
+#ifdef MMX_WAVE_PROF
+  if (D == 3 && !first) wprof_arm((m.nF + 63) / 64);
+#endif
   const int uc = (useCache && cache_enabled()) ? 1 : 0;
   *nblocks = nblk(m.nF);
   if (m.nF == 0) return;
@@ -2280,3 +2335,18 @@ MMX_INST(2)
 MMX_INST(3)
 
 }  // namespace mmx
+
+#ifdef MMX_WAVE_PROF
+// the probe's stamps of the last 3D steady prox launch: 8 per block, written to `path` (binary)
+extern "C" int mmx_wprof_dump(const char* path) {
+  if (!mmx::g_wprofHost) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  std::vector<unsigned long long> h(mmx::g_wprofN);
+  if (hipMemcpy(h.data(), mmx::g_wprofHost, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+  FILE* f = fopen(path, "wb");
+  if (!f) return -4;
+  fwrite(h.data(), 8, h.size(), f);
+  fclose(f);
+  return (int)(h.size() / 8);
+}
+#endif
