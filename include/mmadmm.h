@@ -263,7 +263,9 @@ int mmadmm_plan_get(mmadmm_plan h, int32_t* localNodes, int32_t* localSimplices,
 int mmadmm_plan_destroy(mmadmm_plan h);
 
 /* device math self-test (correctly rounded powers): op 0 sqrt, 1 x^1.5, 2 x^-0.5, 3 x^2.25,
- * 4 x^1.25; op 5: in = pairs (x, c), out[i] = x_i / c_i by reciprocal + FMA correction */
+ * 4 x^1.25; op 5: in = pairs (x, c), out[i] = x_i / c_i by reciprocal + FMA correction;
+ * ops 6-9: the prox fast path of ops 1-4 (NaN where it defers to the exact path); op 10: the
+ * double-double sqrt of in[i] as out[2i] + out[2i+1], i < n/2 */
 int mmadmm_devmath(int op, int n, const double* in, double* out);
 
 #ifdef __cplusplus

@@ -134,7 +134,11 @@ int mmx_factor_schedule_info(int n, const int32_t* ia, const int32_t* ja, int le
 /* Measurement utility (no reference counterpart): the achievable HBM ceiling.  Copies n doubles
  * (n even, device pointers, 16-byte aligned) reps times with a 16-B-per-lane streaming kernel
  * (variant 0: grid-stride, nontemporal; 1: one element per lane; 2: four per lane) on a private
- * stream; *ms = average milliseconds per copy (bytes moved per copy: 16 n). */
+ * stream; *ms = average milliseconds per copy (bytes moved per copy: 16 n).  Variants 3-8 calibrate
+ * the rocprofv3 byte counters on the ADMM kernels' access widths (profiles/r04/calib_counters.py):
+ * 3 reads 8 B per lane, 4 a 24-B record per lane (three 8-B loads), 5 16 B per lane, 6 / 7 store
+ * 8 B per lane (plain / nontemporal), 8 reads a random 24-B record per lane; each touches 8 n bytes
+ * (8: n/3 records). */
 int mmx_stream_copy(int device, const double* d_src, double* d_dst, long long n, int reps, int variant, double* ms);
 
 #ifdef __cplusplus

@@ -221,9 +221,7 @@ class Engine final : public EngineBase {
     }
     invdiag_.upload(invdiag.data(), invdiag.size(), st_);
     if (compMesh_) Vc_.upload(Vcl.data(), Vcl.size(), st_);
-    gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
-    gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
-    if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
+    uploadGridCoords();
     gvals_.upload(grid_.vals.data(), grid_.vals.size(), st_);
     if (D == 3) {
       gpad_.alloc(gvals_.n / 9 * 10);
@@ -942,11 +940,32 @@ class Engine final : public EngineBase {
     return true;
   }
 
-  void setGridGeometry(int nG, const double* lo, const double* hi) {
-    grid_geometry(D, nG, lo, hi, grid_);
+  // the grid coordinates and, in 3D, each axis's cell table {g_i, h_i = g_{i+1} - g_i, RN(1/h_i), 0}
+  // (blockGrad's monitor interpolation, MMX_MON_RECIP)
+  void uploadGridCoords() {
     gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
     gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
-    if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
+    if (D == 3) {
+      gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
+      const std::vector<double>* ax[3] = {&grid_.gx, &grid_.gy, &grid_.gz};
+      for (int a = 0; a < 3; ++a) {
+        const std::vector<double>& g = *ax[a];
+        const size_t nc = g.size() > 1 ? g.size() - 1 : 1;
+        std::vector<double>& t = gcellH_[a];
+        t.assign(4 * nc, 0.0);
+        for (size_t i = 0; i + 1 < g.size(); ++i) {
+          const double h = g[i + 1] - g[i];
+          t[4 * i] = g[i];
+          t[4 * i + 1] = h;
+          t[4 * i + 2] = 1.0 / h;
+        }
+        gcell_[a].upload(t.data(), t.size(), st_);
+      }
+    }
+  }
+  void setGridGeometry(int nG, const double* lo, const double* hi) {
+    grid_geometry(D, nG, lo, hi, grid_);
+    uploadGridCoords();
   }
   // vertex cells over the global box: about two vertices per cell
   CellGrid cellGrid(const double* lo, const double* hi) const {
@@ -1097,9 +1116,7 @@ class Engine final : public EngineBase {
         for (int d = 0; d < D; ++d) extMax_[d] = std::max(extMax_[d], rgHost_[(size_t)512 * 2 * D + (size_t)b * D + d]);
     }
     grid_geometry(D, nG, lo, hi, grid_);
-    gx_.upload(grid_.gx.data(), grid_.gx.size(), st_);
-    gy_.upload(grid_.gy.data(), grid_.gy.size(), st_);
-    if (D == 3) gz_.upload(grid_.gz.data(), grid_.gz.size(), st_);
+    uploadGridCoords();
     // vertex cells: about two vertices per cell
     CellGrid cg{};
     const int gn[3] = {grid_.nx, grid_.ny, grid_.nz};
@@ -1225,6 +1242,7 @@ class Engine final : public EngineBase {
     m.gz = (D == 3) ? gz_.p : gy_.p;
     m.gvals = gvals_.p;
     m.gpad = (D == 3) ? gpad_.p : nullptr;
+    for (int a = 0; a < 3; ++a) m.gcell[a] = (D == 3) ? gcell_[a].p : nullptr;
     m.gnx = grid_.nx;
     m.gny = grid_.ny;
     m.gnz = grid_.nz;
@@ -1319,6 +1337,8 @@ class Engine final : public EngineBase {
   DevBuf<double> tslot_;
   bool tslotOn_ = false;
   DevBuf<uint8_t> sbits_, interior_;
+  DevBuf<double> gcell_[3];
+  std::vector<double> gcellH_[3];  // the cell tables' host images (kept until the async uploads finish)
   DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_, gpad_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
   DevBuf<int32_t> expOff_, tieList_, nodeOrder_;

@@ -24,6 +24,7 @@ struct GridView {  // the smoothed monitor grid, rows of D*D doubles
   const double* gz;
   const double* vals;
   const double* pad;  // 3D: the grid rows padded to 10 doubles (16-byte aligned rows)
+  const double* cell[3];  // 3D: per axis and cell i {g_i, h_i = g_{i+1} - g_i, RN(1/h_i), 0}
   int nx, ny, nz;
   double hx, hy, hz;     // gx[1]-gx[0] etc., the divisors of findLimInfMeshPoint
   double rhx, rhy, rhz;  // RN(1/h)
@@ -149,8 +150,17 @@ __device__ __forceinline__ int findLimInf(double w, double m0, int size, double 
 // and its eight corner rows) and the trilinear interpolation (monEval3), so blockGrad can request
 // the next vertex's cell while it interpolates the current one: the same operations as the 3D
 // branch of evalMonitor below
+// MMX_MON_RECIP: the cell's coordinate, width and RN(1/width) from the per-axis cell tables, and
+// the fraction (p - g_i) / (g_{i+1} - g_i) as div_nr (exact: both operands normal or zero, as for
+// findLimInf) instead of an IEEE division
+#ifndef MMX_MON_RECIP
+#define MMX_MON_RECIP 0
+#endif
 struct MonIn3 {
-  double x0, x1, y0, y1, z0, z1;
+  double x0, x1, y0, y1, z0, z1;  // MMX_MON_RECIP: x1 etc. hold the cell widths
+#if MMX_MON_RECIP
+  double rx, ry, rz;
+#endif
   double r[8][9];
 };
 __device__ __forceinline__ void monLoad3(const GridView<3>& g, const double* pnt, MonIn3& in) {
@@ -158,12 +168,30 @@ __device__ __forceinline__ void monLoad3(const GridView<3>& g, const double* pnt
   const int yInd = findLimInf(pnt[1], g.ay, g.ny + 1, g.hy, g.rhy);
   const int zInd = findLimInf(pnt[2], g.az, g.nz + 1, g.hz, g.rhz);
   const int nx = g.nx;
+#if MMX_MON_RECIP
+  {
+    const double2* cx = reinterpret_cast<const double2*>(g.cell[0]) + 2 * xInd;
+    const double2* cy = reinterpret_cast<const double2*>(g.cell[1]) + 2 * yInd;
+    const double2* cz = reinterpret_cast<const double2*>(g.cell[2]) + 2 * zInd;
+    const double2 ax = cx[0], bx = cx[1], ay = cy[0], by = cy[1], az = cz[0], bz = cz[1];
+    in.x0 = ax.x;
+    in.x1 = ax.y;
+    in.rx = bx.x;
+    in.y0 = ay.x;
+    in.y1 = ay.y;
+    in.ry = by.x;
+    in.z0 = az.x;
+    in.z1 = az.y;
+    in.rz = bz.x;
+  }
+#else
   in.x0 = g.gx[xInd];
   in.x1 = g.gx[xInd + 1];
   in.y0 = g.gy[yInd];
   in.y1 = g.gy[yInd + 1];
   in.z0 = g.gz[zInd];
   in.z1 = g.gz[zInd + 1];
+#endif
   const size_t P = (size_t)(nx + 1) * (g.ny + 1);
   const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
   const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
@@ -181,9 +209,15 @@ __device__ __forceinline__ void monLoad3(const GridView<3>& g, const double* pnt
   }
 }
 __device__ __forceinline__ void monEval3(const MonIn3& in, const double* pnt, M<3>& mv) {
+#if MMX_MON_RECIP
+  const double xd = div_nr(pnt[0] - in.x0, in.x1, in.rx);
+  const double yd = div_nr(pnt[1] - in.y0, in.y1, in.ry);
+  const double zd = div_nr(pnt[2] - in.z0, in.z1, in.rz);
+#else
   const double xd = (pnt[0] - in.x0) / (in.x1 - in.x0);
   const double yd = (pnt[1] - in.y0) / (in.y1 - in.y0);
   const double zd = (pnt[2] - in.z0) / (in.z1 - in.z0);
+#endif
   const double c[8] = {(1 - xd) * (1 - yd) * (1 - zd), xd * (1 - yd) * (1 - zd),
                        (1 - xd) * yd * (1 - zd),       xd * yd * (1 - zd),
                        (1 - xd) * (1 - yd) * zd,       xd * (1 - yd) * zd,

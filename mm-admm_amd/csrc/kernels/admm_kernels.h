@@ -40,6 +40,7 @@ struct DeviceMesh {
   const double* gz;
   const double* gvals;
   const double* gpad;    // 3D: the grid rows padded to 10 doubles (launch_pad_rows)
+  const double* gcell[3];  // 3D: per axis and cell i {g_i, h_i = g_{i+1} - g_i, RN(1/h_i), 0}
   int gnx, gny, gnz;
   double ghx, ghy, ghz, grhx, grhy, grhz;  // grid spacings of findLimInf and RN(1/h)
   double gax, gay, gaz, gspx, gspy, gspz, gnsx, gnsy, gnsz, grnsx, grnsy, grnsz;  // linspace params

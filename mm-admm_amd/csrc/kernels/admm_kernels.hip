@@ -78,6 +78,9 @@ __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   g.gz = m.gz;
   g.vals = m.gvals;
   g.pad = m.gpad;
+  g.cell[0] = m.gcell[0];
+  g.cell[1] = m.gcell[1];
+  g.cell[2] = m.gcell[2];
   g.nx = m.gnx;
   g.ny = m.gny;
   g.nz = m.gnz;
@@ -2016,16 +2019,31 @@ __global__ void k_devmath(int op, int n, const double* __restrict__ in, double* 
     }
     return;
   }
+  if (op == 10) {  // the double-double sqrt the powers use: pairs (s, e) for in[0 .. n/2)
+    if (2 * i + 1 < n) {
+      double sv, ev, hv;
+      dd_sqrt_h(in[i], sv, ev, hv);
+      out[2 * i] = sv;
+      out[2 * i + 1] = ev;
+    }
+    return;
+  }
   const double x = in[i];
   double r;
+  bool tie = false;
   switch (op) {
     case 0: r = cr_sqrt(x); break;
     case 1: r = cr_pow_p15(x); break;
     case 2: r = cr_pow_m05(x); break;
     case 3: r = cr_pow_p225(x); break;
-    default: r = cr_pow_p125(x); break;
+    case 4: r = cr_pow_p125(x); break;
+    // the prox kernels' fast path (no tie resolution): NaN where it would defer to the exact path
+    case 6: r = cr_pow_p15<false>(x, tie); break;
+    case 7: r = cr_pow_m05<false>(x, tie); break;
+    case 8: r = cr_pow_p225<false>(x, tie); break;
+    default: r = cr_pow_p125<false>(x, tie); break;
   }
-  out[i] = r;
+  out[i] = tie ? __builtin_nan("") : r;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -338,6 +338,39 @@ MMX_HD void cr_sqrt_dd(double x, double& s, double& e) {
 // x^0.5 -- correctly rounded sqrt
 MMX_HD double cr_pow_p05(double x) { return cr_sqrt(x); }
 
+// MMX_DD_FAST (device only): the double-double square roots of the powers below from the
+// hardware reciprocal square root, refined by two coupled Newton (Goldschmidt) steps -- no IEEE
+// sqrt and no division.  g -> sqrt(x) and hh -> 1/(2 sqrt(x)) converge quadratically from any
+// start within 2^-10, so after two steps both are within a few ulps; the residual x - s^2 is then
+// formed by FMA with relative error <= 2^-53, and e = (x - s^2) hh (= r / (2s) to ~2^-50) leaves
+// s + e within ~2^-101 |s| of sqrt(x) (the neglected term e^2 / (2s) is ~2^-103 |s|).  Only the
+// double-double changes: every power is still rounded by cr_round_t, whose 2^-95 margin covers
+// it, so the results are the same correctly rounded values (tests/test_gpu_parity.py).
+#ifndef MMX_DD_FAST
+#define MMX_DD_FAST 0
+#endif
+// sqrt(x) = s + e and hh ~ 1 / (2 sqrt(x)) (to a few ulps)
+MMX_HD void dd_sqrt_h(double x, double& s, double& e, double& hh) {
+#if defined(__HIP_DEVICE_COMPILE__) && MMX_DD_FAST
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  double r = cr_fma(-g, h, 0.5);
+  g = cr_fma(g, r, g);
+  h = cr_fma(h, r, h);
+  r = cr_fma(-g, h, 0.5);
+  g = cr_fma(g, r, g);
+  h = cr_fma(h, r, h);
+  s = g;
+  e = cr_fma(-g, g, x) * h;
+  hh = h;
+#else
+  s = cr_sqrt(x);
+  const double r = cr_fma(-s, s, x);
+  e = r / (2.0 * s);
+  hh = 0.5 / s;
+#endif
+}
+
 // Outside the ranges below the powers defer to the library pow (EXACT) or raise `tie` (fast
 // path: the exact recomputation takes the library call).
 #define MMX_CR_RANGE(lo, hi, e)         \
@@ -355,7 +388,12 @@ template <bool EXACT>
 MMX_HD double cr_pow_p15(double x, bool& tie) {
   MMX_CR_RANGE(1e-90, 1e90, 1.5)
   double s, e;
+#if MMX_DD_FAST
+  double hh;
+  dd_sqrt_h(x, s, e, hh);
+#else
   cr_sqrt_dd(x, s, e);
+#endif
   const double p = x * s;
   const double lo = cr_fma(x, s, -p) + x * e;
   return cr_round_t<EXACT>(x, 3, 2, p, lo, tie);
@@ -366,21 +404,40 @@ template <bool EXACT>
 MMX_HD double cr_pow_m05(double x, bool& tie) {
   MMX_CR_RANGE(1e-100, 1e100, -0.5)
   double s, e;
+#if MMX_DD_FAST && defined(__HIP_DEVICE_COMPILE__)
+  // q = 2 hh is within a few ulps of 1/s: 1/(s + e) = q / (1 - u) = q (1 + u + u^2 + ...)
+  double hh;
+  dd_sqrt_h(x, s, e, hh);
+  const double q = 2.0 * hh;
+  const double d = cr_fma(-q, s, 1.0);  // 1 - q*s (error <= 2^-53 of it)
+  const double u = d - q * e;           // 1 - q*(s + e)
+  return cr_round_t<EXACT>(x, -1, 2, q, q * cr_fma(u, u, u), tie);
+#else
   cr_sqrt_dd(x, s, e);
   const double q = 1.0 / s;
   const double d = cr_fma(-q, s, 1.0);  // 1 - q*s, exact
   const double u = d - q * e;           // 1 - q*(s + e)
   return cr_round_t<EXACT>(x, -1, 2, q, q * u, tie);
+#endif
 }
 
 // x^0.25 as hi + lo, |error| < 2^-103 |hi|
 MMX_HD void cr_qrt_dd(double x, double& hi, double& lo) {
+#if MMX_DD_FAST && defined(__HIP_DEVICE_COMPILE__)
+  double s, e, hs;
+  dd_sqrt_h(x, s, e, hs);  // sqrt(x) = s + e, hs ~ 1/(2s)
+  double b, eb, hb;
+  dd_sqrt_h(s, b, eb, hb);  // sqrt(s) = b + eb
+  hi = b;
+  lo = eb + b * (e * hs);  // sqrt(s + e) = sqrt(s) (1 + e/(2s) - ...)
+#else
   double s, e;
   cr_sqrt_dd(x, s, e);  // sqrt(x) = s + e
   double b, eb;
   cr_sqrt_dd(s, b, eb);  // sqrt(s) = b + eb
   hi = b;
   lo = eb + b * (e / (2.0 * s));  // sqrt(s + e) = sqrt(s) (1 + e/(2s) - ...)
+#endif
 }
 
 // x^2.25 = x^2 * x^0.25

@@ -814,6 +814,35 @@ __global__ void __launch_bounds__(256) k_stream_copy(long long n2, const v2d_t* 
   } else if constexpr (VAR == 1) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i < n2) dst[i] = src[i];
+  } else if constexpr (VAR >= 3) {
+    // counter calibration (MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are calibrated only for
+    // 16-B streaming reads and stores): the access widths of the ADMM kernels over n = 2 n2 doubles,
+    // one access group per lane; reads keep their value live through a store that never happens
+    const double* sd = reinterpret_cast<const double*>(src);
+    double* dd = reinterpret_cast<double*>(dst);
+    const long long n = 2 * n2, i = (long long)blockIdx.x * 256 + threadIdx.x;
+    double a = 0.0;
+    if constexpr (VAR == 3) {  // 8 B per lane, coalesced (the 3D prox's Bkinv rows)
+      if (i < n) a = sd[i];
+    } else if constexpr (VAR == 4) {  // a 24-B record per lane as three 8-B loads (slot terms)
+      if (i < n / 3) a = sd[3 * i] + sd[3 * i + 1] + sd[3 * i + 2];
+    } else if constexpr (VAR == 5) {  // 16 B per lane, coalesced (the calibrated case)
+      if (i < n2) {
+        const v2d_t v = src[i];
+        a = v.x + v.y;
+      }
+    } else if constexpr (VAR == 6) {  // 8-B stores per lane, coalesced
+      if (i < n) dd[i] = (double)i;
+    } else if constexpr (VAR == 7) {  // 8-B nontemporal stores per lane (the 3D prox's new Bkinv)
+      if (i < n) __builtin_nontemporal_store((double)i, dd + i);
+    } else {  // a random 24-B record per lane (the x-update's gathers at their worst)
+      const long long nrec = n / 3;
+      if (i < nrec) {
+        const long long r = (long long)(((unsigned long long)i * 2654435761ull) % (unsigned long long)nrec);
+        a = sd[3 * r] + sd[3 * r + 1] + sd[3 * r + 2];
+      }
+    }
+    if (a == -7.25e300) dd[i] = a;
   } else {
     const long long base = (long long)blockIdx.x * 1024 + threadIdx.x;
     v2d_t v[4];
@@ -832,7 +861,13 @@ void launch_stream_copy(int variant, long long n2, const double* src, double* ds
   switch (variant) {
     case 0: hipLaunchKernelGGL(k_stream_copy<0>, dim3(256 * 8), dim3(256), 0, st, n2, s2, d2); break;
     case 1: hipLaunchKernelGGL(k_stream_copy<1>, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
-    default: hipLaunchKernelGGL(k_stream_copy<2>, dim3((unsigned)((n2 + 1023) / 1024)), dim3(256), 0, st, n2, s2, d2); break;
+    case 2: hipLaunchKernelGGL(k_stream_copy<2>, dim3((unsigned)((n2 + 1023) / 1024)), dim3(256), 0, st, n2, s2, d2); break;
+    case 3: hipLaunchKernelGGL(k_stream_copy<3>, dim3((unsigned)((2 * n2 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
+    case 4: hipLaunchKernelGGL(k_stream_copy<4>, dim3((unsigned)((2 * n2 / 3 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
+    case 5: hipLaunchKernelGGL(k_stream_copy<5>, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
+    case 6: hipLaunchKernelGGL(k_stream_copy<6>, dim3((unsigned)((2 * n2 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
+    case 7: hipLaunchKernelGGL(k_stream_copy<7>, dim3((unsigned)((2 * n2 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
+    default: hipLaunchKernelGGL(k_stream_copy<8>, dim3((unsigned)((2 * n2 / 3 + 255) / 256)), dim3(256), 0, st, n2, s2, d2); break;
   }
 }
 

@@ -64,6 +64,48 @@ def test_devmath_correctly_rounded():
         np.testing.assert_array_equal(mx.devmath(op, sub), ref)
 
 
+def _near_midpoint_args(rng):
+    """arguments whose powers sit close to rounding midpoints: a few ulps from 1 and from perfect
+    powers (x = k^4, k^2), plus random ones"""
+    one = 1.0 + np.arange(-64, 65) * 2.0 ** -52
+    k = np.arange(1.0, 3000.0)
+    pp = np.concatenate([k ** 2, k ** 4, (k + 0.5) ** 2])
+    pp = np.concatenate([np.nextafter(pp, 0), pp, np.nextafter(pp, np.inf)])
+    return np.concatenate([one, pp, np.exp(rng.uniform(-20, 20, 6000))])
+
+
+def test_devmath_fast_path_correct_or_deferred():
+    """The prox kernels' fast powers (EXACT = false, with the library's double-double, MMX_DD_FAST
+    or not) either return the correctly rounded power or defer (NaN here) to the exact path --
+    never a wrong rounding -- and defer rarely on random arguments."""
+    rng = np.random.default_rng(7)
+    x = _near_midpoint_args(rng)
+    for op, y in ((6, 1.5), (7, -0.5), (8, 2.25), (9, 1.25)):
+        got = mx.devmath(op, x)
+        ref = np.array([oracle_py.crpow(v, y) for v in x])
+        ok = ~np.isnan(got)
+        np.testing.assert_array_equal(got[ok], ref[ok])
+        assert np.isnan(got[-6000:]).mean() < 1e-3, (op, np.isnan(got[-6000:]).mean())
+
+
+def test_devmath_dd_sqrt_error_bound():
+    """The double-double sqrt behind the powers: |s + e - sqrt(x)| < 2^-98 |sqrt(x)| (crmath.h;
+    the rounding decision needs 2^-95), checked in 60-digit decimal arithmetic."""
+    from decimal import Decimal, getcontext
+
+    getcontext().prec = 60
+    rng = np.random.default_rng(11)
+    x = np.concatenate([np.exp(rng.uniform(-60, 60, 1500)), 1.0 + np.arange(-200, 200) * 2.0 ** -52])
+    out = mx.devmath(10, np.concatenate([x, np.zeros_like(x)]))
+    worst = 0.0
+    for i, v in enumerate(x):
+        s, e = out[2 * i], out[2 * i + 1]
+        t = Decimal(float(v)).sqrt()
+        err = abs((Decimal(float(s)) + Decimal(float(e)) - t) / t)
+        worst = max(worst, float(err))
+    assert worst < 2.0 ** -98, worst
+
+
 @pytest.mark.parametrize("name", list(cases()))
 def test_setup_identical(name):
     mk, mon, dt, tau, rho, comp = cases()[name]
