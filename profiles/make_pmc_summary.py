@@ -2,15 +2,19 @@
 share a pass on gfx950) -> profiles/pmc_summary.json, read by bench.py for roofline.traffic.
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports half the bytes of 16-byte-per-lane
-coalesced streaming reads (MI355X_MICROARCH.md §HBM); `hbm_bytes_per_launch` applies that x2 to the
-fetch side (the prox kernel's bulk read, Bkinv, is such a stream), `hbm_bytes_raw_per_launch` does
-not.  Other access widths are uncalibrated, so the truth lies between the two for mixed kernels.
+coalesced streaming reads (MI355X_MICROARCH.md §HBM); round 4 calibrated the kernels' other read
+widths the same way (8 B per lane, 24-B records, random records: also half, 128-B lines tallied at
+64 B; WRITE_SIZE exact for 8-B plain and nontemporal stores; profiles/r04/calib/), so
+`hbm_bytes_per_launch` applies the x2 to every kernel's fetch side; `hbm_bytes_raw_per_launch` is
+the uncorrected figure.
 
-  python profiles/make_pmc_summary.py profiles/r03/pmc/fetch_counter_collection.csv.gz \
-         profiles/r03/pmc/write_counter_collection.csv.gz [profiles/r03/pmc/f64_counter_collection.csv.gz]
+  python profiles/make_pmc_summary.py profiles/r04/pmc/fetch_counter_collection.csv.gz \
+         profiles/r04/pmc/write_counter_collection.csv.gz profiles/r04/pmc/f64_counter_collection.csv.gz \
+         bfgs_heavy=profiles/r04/pmc/f64b_counter_collection.csv.gz
 
-(round 3: each pass is its own rocprofv3 run of `bench.py --steps 5 --warmup 1 --no-cpu-baseline`,
-dev/gpu_final_b.sh; the summary holds only the kernels those runs launched)
+(round 4: each pass is its own rocprofv3 run of `bench.py --steps 10 --warmup 2 --no-cpu-baseline
+--no-bfgs`, dev/final_pmc.sh; the f64 pass of the BFGS-heavy section alone is profiles/r04/bfgs_only.py;
+the summary holds only the kernels those runs launched)
 
 The optional third pass (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, wave instructions) gives
 `fp64_flops_per_launch` = 64 lanes x (ADD + MUL + 2 FMA + TRANS): executed fp64 work, including
