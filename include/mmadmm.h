@@ -101,6 +101,8 @@ typedef struct mmadmm_stats {
   long long regrid_cand;       /* element partition: candidate vertices of the last rebuild's nearest-
                                   vertex fill (this rank's + those received from its neighbours) */
   long long regrid_fallbacks;  /* element partition: rebuilds that fell back to all-gathering every vertex */
+  int monitor_iso;             /* 1: the monitor grid is isotropic (every point a multiple of the identity,
+                                  bit for bit) and kept as one value per point; MMX_ISO=0 disables it */
 } mmadmm_stats;
 
 /* Time-varying monitors (the reference's Mesh<D>::setUp hook, commented out at

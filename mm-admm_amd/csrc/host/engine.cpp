@@ -227,6 +227,7 @@ class Engine final : public EngineBase {
       gpad_.alloc(gvals_.n / 9 * 10);
       launch_pad_rows(gvals_.p, (long long)(gvals_.n / 9), gpad_.p, st_);
     }
+    updateIso();
     Vp_.upload(Vl.data(), Vl.size(), st_);  // Mesh::Vp
     x_.upload(Vl.data(), Vl.size(), st_);   // MeshIntegrator ctor: x = xPrev = xBar = copyX(Vp)
     xPrev_.upload(Vl.data(), Vl.size(), st_);
@@ -644,6 +645,7 @@ class Engine final : public EngineBase {
     s->prox_bytes = nF * (4.0 * (D + 1) + 1 + 8.0 * (2 * K + K * K) * 2 + 8.0 * K * 2 + ts * 8.0 * K) +
                     nP * 8.0 * D;
     s->xupdate_bytes = 4.0 * (nP + 1) + 4.0 * (D + 1) * nF + (16.0 - 8.0 * ts) * K * nF + 8.0 * D * nP * 2 + 8.0 * nP;
+    s->monitor_iso = iso_ ? 1 : 0;
   }
 
   void resetStats() override {
@@ -935,11 +937,32 @@ class Engine final : public EngineBase {
     st_stats_.regrid_cand = nCand;
     MMX_HIP(hipGetLastError());
     gridOnDevice_ = true;
+    updateIso();
     m_ = makeView();
     st_stats_.regrids += 1;
     return true;
   }
 
+  // An isotropic monitor grid (every point a multiple of the identity, bit for bit: the built-in
+  // MEx1/3/4/5 and moving-bump monitors; NaN rows of a partitioned rebuild count as isotropic) is
+  // also kept as one value per point, and evalMonitor then gathers 8 bytes per cell corner instead
+  // of 8 D^2 (2D: C3 prox -4.6%).  Checked on the device after every
+  // (re)build; MMX_ISO=0 keeps the full rows.
+  void updateIso() {
+    iso_ = false;
+    const char* e = getenv("MMX_ISO");
+    if (e && atoi(e) == 0) return;
+    const long long np = (long long)(gvals_.n / (D * D));
+    if (np <= 0) return;
+    if ((long long)giso_.n != np) giso_.alloc(np);
+    if (!isoFlag_.p) isoFlag_.alloc(1);
+    MMX_HIP(hipMemsetAsync(isoFlag_.p, 0, sizeof(int), st_));
+    launch_iso_compact<D>(gvals_.p, np, giso_.p, isoFlag_.p, st_);
+    int notIso = 1;
+    MMX_HIP(hipMemcpyAsync(&notIso, isoFlag_.p, sizeof(int), hipMemcpyDeviceToHost, st_));
+    MMX_HIP(hipStreamSynchronize(st_));
+    iso_ = (notIso == 0);
+  }
   // the grid coordinates and, in 3D, each axis's cell table {g_i, h_i = g_{i+1} - g_i, RN(1/h_i), 0}
   // (blockGrad's monitor interpolation, MMX_MON_RECIP)
   void uploadGridCoords() {
@@ -1203,6 +1226,7 @@ class Engine final : public EngineBase {
     st_stats_.regrid_cand = part ? nG : 0;
     MMX_HIP(hipGetLastError());
     gridOnDevice_ = true;
+    updateIso();
     m_ = makeView();
     st_stats_.regrids += 1;
   }
@@ -1243,6 +1267,7 @@ class Engine final : public EngineBase {
     m.gvals = gvals_.p;
     m.gpad = (D == 3) ? gpad_.p : nullptr;
     for (int a = 0; a < 3; ++a) m.gcell[a] = (D == 3) ? gcell_[a].p : nullptr;
+    m.giso = iso_ ? giso_.p : nullptr;
     m.gnx = grid_.nx;
     m.gny = grid_.ny;
     m.gnz = grid_.nz;
@@ -1338,6 +1363,9 @@ class Engine final : public EngineBase {
   bool tslotOn_ = false;
   DevBuf<uint8_t> sbits_, interior_;
   DevBuf<double> gcell_[3];
+  DevBuf<double> giso_;  // isotropic grid: one value per point (updateIso)
+  DevBuf<int> isoFlag_;
+  bool iso_ = false;
   std::vector<double> gcellH_[3];  // the cell tables' host images (kept until the async uploads finish)
   DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_, gpad_;
   DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;

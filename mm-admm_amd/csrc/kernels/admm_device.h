@@ -25,6 +25,7 @@ struct GridView {  // the smoothed monitor grid, rows of D*D doubles
   const double* vals;
   const double* pad;  // 3D: the grid rows padded to 10 doubles (16-byte aligned rows)
   const double* cell[3];  // 3D: per axis and cell i {g_i, h_i = g_{i+1} - g_i, RN(1/h_i), 0}
+  const double* iso;      // isotropic grid: one value per point (the diagonal), else nullptr
   int nx, ny, nz;
   double hx, hy, hz;     // gx[1]-gx[0] etc., the divisors of findLimInfMeshPoint
   double rhx, rhy, rhz;  // RN(1/h)
@@ -232,6 +233,47 @@ __device__ __forceinline__ void monEval3(const MonIn3& in, const double* pnt, M<
 #pragma unroll
   for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = f[n];
 }
+// the same two halves on an isotropic grid (one value per point, GridView::iso): the corner values
+// and the sums of monEval3 on the diagonal value and on the off-diagonal +0 (bit-identical)
+struct MonIso3 {
+  double x0, x1, y0, y1, z0, z1;
+  double r[8];
+};
+__device__ __forceinline__ void monLoad3Iso(const GridView<3>& g, const double* pnt, MonIso3& in) {
+  const int xInd = findLimInf(pnt[0], g.ax, g.nx + 1, g.hx, g.rhx);
+  const int yInd = findLimInf(pnt[1], g.ay, g.ny + 1, g.hy, g.rhy);
+  const int zInd = findLimInf(pnt[2], g.az, g.nz + 1, g.hz, g.rhz);
+  const int nx = g.nx;
+  in.x0 = g.gx[xInd];
+  in.x1 = g.gx[xInd + 1];
+  in.y0 = g.gy[yInd];
+  in.y1 = g.gy[yInd + 1];
+  in.z0 = g.gz[zInd];
+  in.z1 = g.gz[zInd + 1];
+  const size_t P = (size_t)(nx + 1) * (g.ny + 1);
+  const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
+  const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
+                          base + P, base + P + 1, base + P + nx + 1, base + P + nx + 2};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) in.r[q] = g.iso[rows[q]];
+}
+__device__ __forceinline__ void monEval3Iso(const MonIso3& in, const double* pnt, M<3>& mv) {
+  const double xd = (pnt[0] - in.x0) / (in.x1 - in.x0);
+  const double yd = (pnt[1] - in.y0) / (in.y1 - in.y0);
+  const double zd = (pnt[2] - in.z0) / (in.z1 - in.z0);
+  const double c[8] = {(1 - xd) * (1 - yd) * (1 - zd), xd * (1 - yd) * (1 - zd),
+                       (1 - xd) * yd * (1 - zd),       xd * yd * (1 - zd),
+                       (1 - xd) * (1 - yd) * zd,       xd * (1 - yd) * zd,
+                       (1 - xd) * yd * zd,             xd * yd * zd};
+  double d = 0.0, o = 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    d += c[q] * in.r[q];
+    o += c[q] * 0.0;
+  }
+#pragma unroll
+  for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = (n / 3 == n % 3) ? d : o;
+}
 // MeshInterpolator<D>::evalMonitorOnGrid (src/MeshInterpolator.cpp:287-342)
 template <int D>
 __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* pnt, M<D>& mv) {
@@ -245,6 +287,21 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     const double norm = (1 / ((xm1 - xm0) * (ym1 - ym0)));
     const double c0 = norm * (xm1 - x) * (ym1 - y), c1 = norm * (x - xm0) * (ym1 - y);
     const double c2 = norm * (xm1 - x) * (y - ym0), c3 = norm * (x - xm0) * (y - ym0);
+    if (g.iso) {
+      // an isotropic grid (every point s I, off-diagonals +0): the same sums as below on one value
+      // per corner -- 8 bytes gathered per corner instead of 32; the off-diagonal sums of +0 are
+      // formed as below, so they are bit-identical too (NaN positions included)
+      const double* r0 = g.iso + (size_t)yInd * (nx + 1) + xInd;
+      const double* r1 = r0 + (nx + 1);
+      const double a = r0[0], b = r0[1], e = r1[0], f = r1[1];
+      const double d = c0 * a + c1 * b + c2 * e + c3 * f;
+      const double o = c0 * 0.0 + c1 * 0.0 + c2 * 0.0 + c3 * 0.0;
+      mv.m[0][0] = d;
+      mv.m[0][1] = o;
+      mv.m[1][0] = o;
+      mv.m[1][1] = d;
+      return;
+    }
     const double2* r0 = reinterpret_cast<const double2*>(g.vals + ((size_t)yInd * (nx + 1) + xInd) * 4);
     const double2* r1 = reinterpret_cast<const double2*>(g.vals + ((size_t)(yInd + 1) * (nx + 1) + xInd) * 4);
     const double2 a0 = r0[0], a1 = r0[1], b0 = r0[2], b1 = r0[3];  // g00, g10
@@ -269,6 +326,17 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
     const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
     const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
                             base + P, base + P + 1, base + P + nx + 1, base + P + nx + 2};
+    if (g.iso) {  // an isotropic grid (monEval3)
+      double d = 0.0, o = 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        d += c[q] * g.iso[rows[q]];
+        o += c[q] * 0.0;
+      }
+#pragma unroll
+      for (int n = 0; n < 9; ++n) mv.m[n / 3][n % 3] = (n / 3 == n % 3) ? d : o;
+      return;
+    }
     // rows read from the 10-double padded copy: 5 16-byte loads per row instead of 9 8-byte ones
     // (the same values; the sums below are unchanged).  All eight rows are requested before the
     // first is used: loaded row by row, the compiler waited for each corner before requesting the
@@ -342,15 +410,27 @@ __device__ __forceinline__ double blockGrad(const GridView<D>& g, const Function
   const double dFact = (D == 2) ? 2.0 : 6.0;
   M<D> mPre[D + 1], Msum;
   if constexpr (D == 3 && MMX_MON_PIPE) {  // vertex i + 1's cell requested while vertex i interpolates
-    MonIn3 ia, ib;
-    monLoad3(g, &z[0], ia);
-    monLoad3(g, &z[3], ib);
-    monEval3(ia, &z[0], mPre[0]);
-    monLoad3(g, &z[6], ia);
-    monEval3(ib, &z[3], mPre[1]);
-    monLoad3(g, &z[9], ib);
-    monEval3(ia, &z[6], mPre[2]);
-    monEval3(ib, &z[9], mPre[3]);
+    if (g.iso) {
+      MonIso3 ja, jb;
+      monLoad3Iso(g, &z[0], ja);
+      monLoad3Iso(g, &z[3], jb);
+      monEval3Iso(ja, &z[0], mPre[0]);
+      monLoad3Iso(g, &z[6], ja);
+      monEval3Iso(jb, &z[3], mPre[1]);
+      monLoad3Iso(g, &z[9], jb);
+      monEval3Iso(ja, &z[6], mPre[2]);
+      monEval3Iso(jb, &z[9], mPre[3]);
+    } else {
+      MonIn3 ia, ib;
+      monLoad3(g, &z[0], ia);
+      monLoad3(g, &z[3], ib);
+      monEval3(ia, &z[0], mPre[0]);
+      monLoad3(g, &z[6], ia);
+      monEval3(ib, &z[3], mPre[1]);
+      monLoad3(g, &z[9], ib);
+      monEval3(ia, &z[6], mPre[2]);
+      monEval3(ib, &z[9], mPre[3]);
+    }
   }
 #pragma unroll
   for (int i = 0; i < D + 1; i++) {

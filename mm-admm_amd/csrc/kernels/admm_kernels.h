@@ -41,6 +41,7 @@ struct DeviceMesh {
   const double* gvals;
   const double* gpad;    // 3D: the grid rows padded to 10 doubles (launch_pad_rows)
   const double* gcell[3];  // 3D: per axis and cell i {g_i, h_i = g_{i+1} - g_i, RN(1/h_i), 0}
+  const double* giso;      // an isotropic grid's one value per point (launch_iso_compact), else nullptr
   int gnx, gny, gnz;
   double ghx, ghy, ghz, grhx, grhy, grhz;  // grid spacings of findLimInf and RN(1/h)
   double gax, gay, gaz, gspx, gspy, gspz, gnsx, gnsy, gnsz, grnsx, grnsy, grnsz;  // linspace params
@@ -71,6 +72,10 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
 // gradient in m.gcache; the entry blockGrad then reduces to adding the regulariser.
 // 3D: pad[r 10 + n] = vals[r 9 + n], pad[r 10 + 9] = 0 (rebuilt whenever vals changes)
 void launch_pad_rows(const double* vals, long long rows, double* pad, hipStream_t st);
+// iso[i] = vals[i D^2] for every grid point; *notIso (zeroed by the caller) is set unless every point
+// is a multiple of the identity bit for bit (off-diagonals +0, equal diagonals) or all NaN
+template <int D>
+void launch_iso_compact(const double* vals, long long points, double* iso, int* notIso, hipStream_t st);
 // diagonal entries of the identity Bkinv of nF simplices in the bidx<D> layout (buffer zeroed before)
 template <int D>
 void launch_bkinv_identity(int nF, double* B, hipStream_t st);

@@ -70,7 +70,10 @@ __device__ __forceinline__ int logical_block_any() {
   return x * q + min(x, r) + (int)(blockIdx.x / 8);
 }
 
-template <int D>
+// ISO: -1 the monitor path chosen at run time from m.giso; 0 the full-row path only; 1 the
+// isotropic path only (m.giso set).  3D kernels are instantiated per path and launched by m.giso
+// (launch_iso3), so neither path's registers count against the other's.
+template <int D, int ISO = -1>
 __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   GridView<D> g;
   g.gx = m.gx;
@@ -81,6 +84,7 @@ __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   g.cell[0] = m.gcell[0];
   g.cell[1] = m.gcell[1];
   g.cell[2] = m.gcell[2];
+  g.iso = m.giso;
   g.nx = m.gnx;
   g.ny = m.gny;
   g.nz = m.gnz;
@@ -103,6 +107,10 @@ __device__ __forceinline__ GridView<D> gridOf(const DeviceMesh<D>& m) {
   g.rnsy = m.grnsy;
   g.rnsz = m.grnsz;
   g.invFlag = m.invFlag;
+  if constexpr (ISO == 0)
+    g.iso = nullptr;
+  else if constexpr (ISO == 1)
+    __builtin_assume(g.iso != nullptr);
   return g;
 }
 
@@ -170,7 +178,7 @@ __global__ void __launch_bounds__(kBlock) k_gather_z(DeviceMesh<D> m, const doub
 }
 
 // per-simplex gradient of the unregularised functional (Mesh::eulerGrad / eulerStepMod)
-template <int D>
+template <int D, int ISO = -1>
 __global__ void __launch_bounds__(kBlock) k_grad_simplex(DeviceMesh<D> m, const double* __restrict__ x,
                                                           double* __restrict__ gs, int zeroFixedRows,
                                                           double* __restrict__ partials) {
@@ -183,7 +191,7 @@ __global__ void __launch_bounds__(kBlock) k_grad_simplex(DeviceMesh<D> m, const 
     double z[K], xi[K], g[K], Igt;
     gatherX<D>(x, f, z);
     loadXi<D>(m, f, xi);
-    const double e = blockGrad<D, true, false>(gridOf<D>(m), constsOf<D>(m), z, xi, nullptr, g, Igt);
+    const double e = blockGrad<D, true, false>(gridOf<D, ISO>(m), constsOf<D>(m), z, xi, nullptr, g, Igt);
     if (zeroFixedRows) zeroFixed<D>(g, m.sbits[s] & 0xF);
 #pragma unroll
     for (int i = 0; i < K; ++i) gs[(size_t)s * K + i] = g[i];
@@ -847,13 +855,13 @@ __device__ __forceinline__ void entry_grad(const GridView<D>& g, const Functiona
 
 // The prox (src/Mesh.cpp:930-994 / 777-872), one lane per simplex.  FIRST = the first prox of
 // the run, which builds the finite-difference Hessian and inverts it.
-template <int D, bool FIRST>
+template <int D, bool FIRST, int ISO = -1>
 __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol, const double* __restrict__ x,
                                              double* __restrict__ zg, double* __restrict__ ug,
                                              const double* Bin, double* Bout, bool useCache, int s,
                                              double (&pv)[6]) {
   constexpr int K = D * (D + 1);
-  const GridView<D> g = gridOf<D>(m);
+  const GridView<D> g = gridOf<D, ISO>(m);
   const FunctionalConsts<D> fc = constsOf<D>(m);
   int f[D + 1];
   loadVerts<D>(m, s, f);
@@ -926,14 +934,14 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
   pv[5] = (double)its;
 }
 
-template <int D, bool FIRST>
+template <int D, bool FIRST, int ISO = -1>
 __global__ void __launch_bounds__(kBlock) k_prox(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                   double* __restrict__ zg, double* __restrict__ ug,
                                                   const double* Bin, double* Bout, double* __restrict__ partials,
                                                   int useCache) {
   const int s = blockIdx.x * kBlock + threadIdx.x;
   double pv[6] = {0, 0, 0, 0, 0, 0};
-  if (s < m.nF) prox_simplex<D, FIRST>(m, tol, x, zg, ug, Bin, Bout, useCache != 0, s, pv);
+  if (s < m.nF) prox_simplex<D, FIRST, ISO>(m, tol, x, zg, ug, Bin, Bout, useCache != 0, s, pv);
   block_partials<6>(pv, partials);
 }
 
@@ -1111,7 +1119,7 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 // returns false, having written nothing, when a power met a near-midpoint (the block is queued).
 // EXACT = true (k_prox_wave_fix): the exact recomputation of a queued block, entry gradient
 // included (the fast pass may have left the cache at a point it then abandoned).
-template <int D, bool COMP, bool EXACT>
+template <int D, bool COMP, bool EXACT, bool ISO = false>
 __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double tol, const double* __restrict__ x,
                                                 double* __restrict__ zg, double* __restrict__ ug, const double* Bin,
                                                 double* Bout, double* __restrict__ partials, int useCache, int lb,
@@ -1163,7 +1171,13 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
   double pv[6] = {0, 0, 0, 0, 0, 0};
   bool tie = false;
   if (act) {
-    const GridView<D> g = gridOf<D>(m);
+    // ISO: the isotropic-grid instance (GridView::iso set); otherwise the full-row instance, whose
+    // monitor code is then exactly the general one (no second path competing for registers)
+    GridView<D> g = gridOf<D>(m);
+    if constexpr (ISO)
+      __builtin_assume(g.iso != nullptr);
+    else
+      g.iso = nullptr;
     FunctionalConsts<D> fc = constsOf<D>(m);
     fc.compMesh = COMP ? 1 : 0;
     double G[K], Igt;
@@ -1216,7 +1230,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
   }
 }
 
-template <int D, bool COMP>
+template <int D, bool COMP, bool ISO = false>
 __global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_prox_wave(DeviceMesh<D> m, double tol, const double* __restrict__ x,
                                                      double* __restrict__ zg, double* __restrict__ ug,
                                                      const double* Bin, double* Bout, double* __restrict__ partials,
@@ -1224,13 +1238,13 @@ __global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_p
   constexpr int K = D * (D + 1);
   __shared__ __attribute__((aligned(16))) double ldsHeld[WaveB<K>::kHeld > 0 ? WaveB<K>::kHeld * K * 64 : 2];
   const int lb = MMX_WAVE_XCD ? logical_block_any() : (int)blockIdx.x;  // XCD-contiguous tet ranges
-  prox_wave_block<D, COMP, false>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
+  prox_wave_block<D, COMP, false, ISO>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
 }
 
 // The exact recomputation of the blocks k_prox_wave queued, with the same Bkinv streaming (the
 // generic one-lane k_prox_fix holds a tet's 144 Bkinv entries in registers and spills: ~0.3 ms
 // for one block).  A fixed grid strides over the queue, as k_prox_fix.
-template <int D, bool COMP>
+template <int D, bool COMP, bool ISO = false>
 __global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_prox_wave_fix(DeviceMesh<D> m, double tol,
                                                          const double* __restrict__ x, double* __restrict__ zg,
                                                          double* __restrict__ ug, const double* Bin, double* Bout,
@@ -1239,7 +1253,7 @@ __global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_p
   __shared__ __attribute__((aligned(16))) double ldsHeld[WaveB<K>::kHeld > 0 ? WaveB<K>::kHeld * K * 64 : 2];
   const unsigned n = *m.tieCount;
   for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
-    prox_wave_block<D, COMP, true>(m, tol, x, zg, ug, Bin, Bout, partials, 0, m.tieList[i], ldsHeld);
+    prox_wave_block<D, COMP, true, ISO>(m, tol, x, zg, ug, Bin, Bout, partials, 0, m.tieList[i], ldsHeld);
     __syncthreads();
   }
   rearm_tie_queue(m.tieStale);
@@ -1739,7 +1753,7 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
 }
 
 // Mesh::computeEnergy (src/Mesh.cpp:496-530) on positions x
-template <int D>
+template <int D, int ISO = -1>
 __global__ void __launch_bounds__(kBlock) k_energy(DeviceMesh<D> m, const double* __restrict__ x,
                                                     double* __restrict__ partials) {
   constexpr int K = D * (D + 1);
@@ -1751,7 +1765,7 @@ __global__ void __launch_bounds__(kBlock) k_energy(DeviceMesh<D> m, const double
     double z[K], xi[K], Igt;
     gatherX<D>(x, f, z);
     loadXi<D>(m, f, xi);
-    const double e = blockGrad<D, false, false>(gridOf<D>(m), constsOf<D>(m), z, xi, nullptr, nullptr, Igt);
+    const double e = blockGrad<D, false, false>(gridOf<D, ISO>(m), constsOf<D>(m), z, xi, nullptr, nullptr, Igt);
     pv[0] = e;
     pv[4] = (e == e) ? 0.0 : 1.0;
   }
@@ -1786,7 +1800,7 @@ __global__ void __launch_bounds__(kBlock) k_euler_apply(DeviceMesh<D> m, const d
 // moved by h (pass i), and writes derivs(i, :) = (Gkp1 - Gk) / h.  A BOUNDARY_FIXED vertex gets
 // the reference's identity pattern, which is nonzero only for n == 0 (r == c in D*n..D*n+D-1).
 // The node-centric reference evaluates Gk once per (node, simplex); the values are the same.
-template <int D>
+template <int D, int ISO = -1>
 __global__ void __launch_bounds__(kBlock) k_fd_jac(DeviceMesh<D> m, const double* __restrict__ Vp, double h,
                                                     double* __restrict__ dv) {
   constexpr int K = D * (D + 1);
@@ -1805,7 +1819,7 @@ __global__ void __launch_bounds__(kBlock) k_fd_jac(DeviceMesh<D> m, const double
   double xl[K], xi[K], gk[K], g1[K], xp[K], Igt;
   gatherX<D>(Vp, f, xl);
   loadXi<D>(m, f, xi);
-  const GridView<D> g = gridOf<D>(m);
+  const GridView<D> g = gridOf<D, ISO>(m);
   const FunctionalConsts<D> fc = constsOf<D>(m);
 #pragma unroll 1
   for (int it = -1; it < D; ++it) {
@@ -2070,7 +2084,14 @@ void launch_grad_simplex(const DeviceMesh<D>& m, const double* x, double* gs, bo
                          double* partials, int* nblocks, hipStream_t st) {
   *nblocks = nblk(m.nF);
   if (m.nF == 0) return;
-  hipLaunchKernelGGL(k_grad_simplex<D>, dim3(*nblocks), dim3(kBlock), 0, st, m, x, gs,
+  if (D == 3 && m.giso)
+    hipLaunchKernelGGL((k_grad_simplex<D, 1>), dim3(*nblocks), dim3(kBlock), 0, st, m, x, gs,
+                     zeroFixedRows ? 1 : 0, partials);
+  else if (D == 3)
+    hipLaunchKernelGGL((k_grad_simplex<D, 0>), dim3(*nblocks), dim3(kBlock), 0, st, m, x, gs,
+                     zeroFixedRows ? 1 : 0, partials);
+  else
+    hipLaunchKernelGGL((k_grad_simplex<D, -1>), dim3(*nblocks), dim3(kBlock), 0, st, m, x, gs,
                      zeroFixedRows ? 1 : 0, partials);
 }
 template <int D>
@@ -2120,6 +2141,32 @@ __global__ void __launch_bounds__(kBlock) k_pad_rows(const double* __restrict__ 
   for (int n = 0; n < 9; ++n) pad[r * 10 + n] = vals[r * 9 + n];
   pad[r * 10 + 9] = 0.0;
 }
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_iso_compact(const double* __restrict__ vals, long long n,
+                                                        double* __restrict__ iso, int* __restrict__ notIso) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double* v = vals + i * D * D;
+  const unsigned long long d0 = __double_as_longlong(v[0]);
+  bool ok = true, nan = true;
+#pragma unroll
+  for (int k = 0; k < D * D; ++k) {
+    const unsigned long long b = __double_as_longlong(v[k]);
+    ok = ok && (b == ((k / D == k % D) ? d0 : 0ull));
+    nan = nan && (v[k] != v[k]);
+  }
+  if (!(ok || nan)) *notIso = 1;  // (every writer stores the same value)
+  iso[i] = v[0];
+}
+template <int D>
+void launch_iso_compact(const double* vals, long long points, double* iso, int* notIso, hipStream_t st) {
+  if (points > 0)
+    hipLaunchKernelGGL(k_iso_compact<D>, dim3((unsigned)((points + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vals,
+                       points, iso, notIso);
+}
+template void launch_iso_compact<2>(const double*, long long, double*, int*, hipStream_t);
+template void launch_iso_compact<3>(const double*, long long, double*, int*, hipStream_t);
+
 void launch_pad_rows(const double* vals, long long rows, double* pad, hipStream_t st) {
   if (rows > 0) hipLaunchKernelGGL(k_pad_rows, dim3((unsigned)((rows + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vals, rows, pad);
 }
@@ -2202,7 +2249,12 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
   *nblocks = nblk(m.nF);
   if (m.nF == 0) return;
   if (first) {
-    hipLaunchKernelGGL((k_prox<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+    if (D == 3 && m.giso)
+      hipLaunchKernelGGL((k_prox<D, true, 1>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+    else if (D == 3)
+      hipLaunchKernelGGL((k_prox<D, true, 0>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
+    else
+      hipLaunchKernelGGL((k_prox<D, true, -1>), dim3(*nblocks), dim3(kBlock), 0, st, m, tol, x, z, u, Bin, Bout, partials, 0);
   } else if (D == 2 && m.prox2dWave) {
     *nblocks = (m.nF + 63) / 64;
     const dim3 fg(std::min(*nblocks, kFixGrid));
@@ -2247,20 +2299,29 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
       }
       return;
     }
+#define MMX_WAVE3(C, I)                                                                                            \
+  do {                                                                                                           \
+    hipLaunchKernelGGL((k_prox_wave<D, C, I>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc); \
+    hipLaunchKernelGGL((k_prox_wave_fix<D, C, I>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);          \
+  } while (0)
     if (m.compMesh) {
-      hipLaunchKernelGGL((k_prox_wave<D, true>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
-      hipLaunchKernelGGL((k_prox_wave_fix<D, true>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+      if (m.giso) MMX_WAVE3(true, true); else MMX_WAVE3(true, false);
     } else {
-      hipLaunchKernelGGL((k_prox_wave<D, false>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc);
-      hipLaunchKernelGGL((k_prox_wave_fix<D, false>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);
+      if (m.giso) MMX_WAVE3(false, true); else MMX_WAVE3(false, false);
     }
+#undef MMX_WAVE3
   }
 }
 template <int D>
 void launch_energy(const DeviceMesh<D>& m, const double* x, double* partials, int* nblocks, hipStream_t st) {
   *nblocks = nblk(m.nF);
   if (m.nF == 0) return;
-  hipLaunchKernelGGL(k_energy<D>, dim3(*nblocks), dim3(kBlock), 0, st, m, x, partials);
+  if (D == 3 && m.giso)
+    hipLaunchKernelGGL((k_energy<D, 1>), dim3(*nblocks), dim3(kBlock), 0, st, m, x, partials);
+  else if (D == 3)
+    hipLaunchKernelGGL((k_energy<D, 0>), dim3(*nblocks), dim3(kBlock), 0, st, m, x, partials);
+  else
+    hipLaunchKernelGGL((k_energy<D, -1>), dim3(*nblocks), dim3(kBlock), 0, st, m, x, partials);
 }
 template <int D>
 void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
@@ -2309,7 +2370,13 @@ template <int D>
 void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st) {
   const long long nt = (long long)m.nF * (D + 1);
   if (nt == 0) return;
-  hipLaunchKernelGGL(k_fd_jac<D>, dim3((unsigned)((nt + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, m, Vp, h, dv);
+  const dim3 gj((unsigned)((nt + kBlock - 1) / kBlock));
+  if (D == 3 && m.giso)
+    hipLaunchKernelGGL((k_fd_jac<D, 1>), gj, dim3(kBlock), 0, st, m, Vp, h, dv);
+  else if (D == 3)
+    hipLaunchKernelGGL((k_fd_jac<D, 0>), gj, dim3(kBlock), 0, st, m, Vp, h, dv);
+  else
+    hipLaunchKernelGGL((k_fd_jac<D, -1>), gj, dim3(kBlock), 0, st, m, Vp, h, dv);
 }
 template <int D>
 void launch_jac_assemble(const DeviceMesh<D>& m, const int* ia, const int* ja, const double* dv, double dt_over_tau,

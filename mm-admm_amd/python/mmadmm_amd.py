@@ -51,7 +51,7 @@ class mmadmm_stats(ctypes.Structure):
                 ("cg_iters", ctypes.c_longlong), ("t_jac_ms", ctypes.c_double), ("t_solve_ms", ctypes.c_double),
                 ("t_be_ms", ctypes.c_double), ("regrids", ctypes.c_longlong), ("regrid_rows", ctypes.c_longlong),
                 ("regrid_gather_bytes", ctypes.c_double), ("regrid_cand", ctypes.c_longlong),
-                ("regrid_fallbacks", ctypes.c_longlong)]
+                ("regrid_fallbacks", ctypes.c_longlong), ("monitor_iso", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1,7 +1,7 @@
 """Same-box comparison of build variants of libmmadmm (profiles/r04/variants.sh builds them with
 extra -D flags into dev/lib_<name>/): for each library (MMADMM_LIB) in a fresh process, the
 workload's prox / x-update times from HIP events and a hash of the node positions (variants must be
-bit-identical).  Usage: python variant_bench.py <c3|c4|c2> <steps> <lib> [<lib> ...]"""
+bit-identical).  Usage: python variant_bench.py <c3|c4|c2> <steps> <lib>[+VAR=VALUE...] [...]"""
 import hashlib
 import json
 import os
@@ -54,8 +54,11 @@ if __name__ == "__main__":
         sys.exit(0)
     work, steps, libs = sys.argv[1], sys.argv[2], sys.argv[3:]
     for rep in range(2):  # two rounds, alternating, against box drift
-        for lib in libs:
+        for spec in libs:
+            # "<lib>[+VAR=VALUE...]": a library (or "default") and environment settings for it
+            lib, *sets = spec.split("+")
             env = dict(os.environ)
+            env.update(kv.split("=", 1) for kv in sets)
             if lib != "default":
                 env["MMADMM_LIB"] = os.path.abspath(lib)
             r = subprocess.run([sys.executable, __file__, "--one", work, steps], env=env, capture_output=True,
@@ -65,4 +68,5 @@ if __name__ == "__main__":
                 sys.exit(1)
             d = json.loads(r.stdout.strip().splitlines()[-1])
             d["round"] = rep
+            d["spec"] = spec
             print(json.dumps(d), flush=True)

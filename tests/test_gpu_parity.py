@@ -372,3 +372,39 @@ def test_xupdate_order_and_sweep_bitwise_2d(order, sweep, monkeypatch):
         np.testing.assert_array_equal(Q.get(f), W.get(f), err_msg=f)
     W.close()
     Q.close()
+
+
+ISO_CASES = {  # mesh, MonType, dt, tau, rho, isotropic grid
+    "hexdisc40_mex1": (lambda: mx.MeshData.hexdisc(40), 1, 0.055, 0.5, 50.0, 1),
+    "rect30_mex3": (lambda: mx.MeshData.rect(2, 30), 3, 0.025, 0.5, 1000.0, 1),
+    "rect30_mex2": (lambda: mx.MeshData.rect(2, 30), 2, 0.025, 0.5, 100.0, 0),
+    "hexdisc40_movingbump": (lambda: mx.MeshData.hexdisc(40), 7, 0.05, 0.5, 50.0, 1),
+    "rect3d_8_mex1": (lambda: mx.MeshData.rect(3, 8), 1, 0.025, 0.5, 50.0, 1),
+    "rect3d_8_aniso6": (lambda: mx.MeshData.rect(3, 8), 6, 0.025, 0.5, 50.0, 0),
+    "rect3d_8_movingbump": (lambda: mx.MeshData.rect(3, 8), 7, 0.025, 0.5, 2000.0, 1),
+}
+
+
+@pytest.mark.parametrize("name", list(ISO_CASES))
+def test_isotropic_grid_path_bitwise(name, monkeypatch):
+    """An isotropic monitor grid (every point s I bit for bit) is kept as one value per point and
+    interpolated from it (evalMonitor, engine.cpp updateIso): the state after 3 steps x 5 ADMM iterations equals the full-row path (MMX_ISO=0) bit
+    for bit, in 2D and 3D (the first prox's FD Hessian, the steady 3D prox and its exact
+    recomputation are separate isotropic instances there); MEx2 and MonType 6 are anisotropic and keep
+    the full rows; MonType 7 is rebuilt on the device every step and stays isotropic."""
+    mk, mon, dt, tau, rho, iso = ISO_CASES[name]
+    mesh = mk()
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MMX_ISO", flag)
+        M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(mesh.dim, mon), rho=rho, tau=tau)
+        G = mx.Engine(M, dt)
+        if mon == 7:
+            G.set_regrid(True)
+        for _ in range(3):
+            G.step(5, -1.0)
+        out[flag] = (G.stats()["monitor_iso"], G.get("x"), G.get("z"), G.get("u"), G.get("hess"))
+        G.close()
+    assert out["0"][0] == 0 and out["1"][0] == iso
+    for a, b in zip(out["0"][1:], out["1"][1:]):
+        np.testing.assert_array_equal(a, b)
