@@ -15,9 +15,9 @@ def one(work, steps):
     import time
     sys.path.insert(0, os.path.join(ROOT, "mm-admm_amd", "python"))
     import mmadmm_amd as mx
-    if work == "c4":
+    if work in ("c4", "c4mb"):  # c4mb: the isotropic moving-bump monitor (MonType 7) at t = 0
         m = mx.MeshData.rect(3, 63)
-        M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 6), rho=2000.0, tau=0.5)
+        M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 6 if work == "c4" else 7), rho=2000.0, tau=0.5)
         dt = 0.025
     elif work == "c2":
         m = mx.MeshData.rect(2, 223)
