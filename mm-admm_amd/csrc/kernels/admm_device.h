@@ -186,12 +186,21 @@ __device__ __forceinline__ void monLoad3(const GridView<3>& g, const double* pnt
     in.rz = bz.x;
   }
 #else
+#ifdef MMX_GRID_RECOMPUTE3
+  in.x0 = gridCoord(g.ax, g.spx, g.nsx, g.rnsx, xInd);
+  in.x1 = gridCoord(g.ax, g.spx, g.nsx, g.rnsx, xInd + 1);
+  in.y0 = gridCoord(g.ay, g.spy, g.nsy, g.rnsy, yInd);
+  in.y1 = gridCoord(g.ay, g.spy, g.nsy, g.rnsy, yInd + 1);
+  in.z0 = gridCoord(g.az, g.spz, g.nsz, g.rnsz, zInd);
+  in.z1 = gridCoord(g.az, g.spz, g.nsz, g.rnsz, zInd + 1);
+#else
   in.x0 = g.gx[xInd];
   in.x1 = g.gx[xInd + 1];
   in.y0 = g.gy[yInd];
   in.y1 = g.gy[yInd + 1];
   in.z0 = g.gz[zInd];
   in.z1 = g.gz[zInd + 1];
+#endif
 #endif
   const size_t P = (size_t)(nx + 1) * (g.ny + 1);
   const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
@@ -244,12 +253,21 @@ __device__ __forceinline__ void monLoad3Iso(const GridView<3>& g, const double* 
   const int yInd = findLimInf(pnt[1], g.ay, g.ny + 1, g.hy, g.rhy);
   const int zInd = findLimInf(pnt[2], g.az, g.nz + 1, g.hz, g.rhz);
   const int nx = g.nx;
+#ifdef MMX_GRID_RECOMPUTE3
+  in.x0 = gridCoord(g.ax, g.spx, g.nsx, g.rnsx, xInd);
+  in.x1 = gridCoord(g.ax, g.spx, g.nsx, g.rnsx, xInd + 1);
+  in.y0 = gridCoord(g.ay, g.spy, g.nsy, g.rnsy, yInd);
+  in.y1 = gridCoord(g.ay, g.spy, g.nsy, g.rnsy, yInd + 1);
+  in.z0 = gridCoord(g.az, g.spz, g.nsz, g.rnsz, zInd);
+  in.z1 = gridCoord(g.az, g.spz, g.nsz, g.rnsz, zInd + 1);
+#else
   in.x0 = g.gx[xInd];
   in.x1 = g.gx[xInd + 1];
   in.y0 = g.gy[yInd];
   in.y1 = g.gy[yInd + 1];
   in.z0 = g.gz[zInd];
   in.z1 = g.gz[zInd + 1];
+#endif
   const size_t P = (size_t)(nx + 1) * (g.ny + 1);
   const size_t base = zInd * P + (size_t)yInd * (nx + 1) + xInd;
   const size_t rows[8] = {base, base + 1, base + nx + 1, base + nx + 2,
@@ -281,8 +299,16 @@ __device__ __forceinline__ void evalMonitor(const GridView<D>& g, const double* 
   const int yInd = findLimInf(pnt[1], g.ay, g.ny + 1, g.hy, g.rhy);
   const int nx = g.nx;
   if constexpr (D == 2) {
-    // loading the coordinates is cheaper here than recomputing them with gridCoord (measured)
+    // the cell's coordinates recomputed (gridCoord, bit-identical to the host linspace) rather than
+    // loaded: the loads were a dependent round trip after the index (round 4, C3 prox 0.365 ->
+    // 0.323 ms with the isotropic grid; round 1, with four 32-byte corner rows behind them, loading
+    // measured cheaper)
+#ifdef MMX_GRID_LOAD
     const double xm0 = g.gx[xInd], xm1 = g.gx[xInd + 1], ym0 = g.gy[yInd], ym1 = g.gy[yInd + 1];
+#else
+    const double xm0 = gridCoord(g.ax, g.spx, g.nsx, g.rnsx, xInd), xm1 = gridCoord(g.ax, g.spx, g.nsx, g.rnsx, xInd + 1);
+    const double ym0 = gridCoord(g.ay, g.spy, g.nsy, g.rnsy, yInd), ym1 = gridCoord(g.ay, g.spy, g.nsy, g.rnsy, yInd + 1);
+#endif
     const double x = pnt[0], y = pnt[1];
     const double norm = (1 / ((xm1 - xm0) * (ym1 - ym0)));
     const double c0 = norm * (xm1 - x) * (ym1 - y), c1 = norm * (x - xm0) * (ym1 - y);
