@@ -217,7 +217,7 @@ def c2_bench(mx, with_cpu, threads, admm_iter, steps=20):
            "value": round(steps * admm_iter / el, 3), "unit": "ADMM it/s", "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 3), "first_step_ms": round(first * 1e3, 1),
            "kernels": {"k_prox_ms": round(prox_ms, 4)},
-           "roofline": {"bound": "hbm", "kernel": "k_prox_lds<2, 128>", "achieved": round(prox_gbs, 1),
+           "roofline": {"bound": "hbm", "kernel": prox2d_name(), "achieved": round(prox_gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
                         "bytes_per_launch": st["prox_bytes"], "avg_launch_ms": round(prox_ms, 4)}}
     E.close()
@@ -263,10 +263,10 @@ def c4_bench(mx, with_cpu, threads, admm_iter):
            "value": round(steps * admm_iter / el, 3), "unit": "ADMM it/s", "first_step_ms": round(first * 1e3, 1),
            "kernels": {"k_prox_wave_ms": round(prox_ms, 4), "k_xupdate_ms": round(xup_ms, 4),
                        "bfgs_iters_per_prox": round(st["bfgs_iters"] / max(st["admm_iters"], 1) / mesh.nF, 4)},
-           "roofline": {"bound": "hbm", "kernel": "k_prox_wave<3, false>", "achieved": round(prox_gbs, 1),
+           "roofline": {"bound": "hbm", "kernel": PROX3D_NAME, "achieved": round(prox_gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(prox_gbs / HBM_PEAK_GBS, 4),
                         "bytes_per_launch": st["prox_bytes"], "avg_launch_ms": round(prox_ms, 4)}}
-    tr, trr = pmc_traffic("k_prox_wave<3, false>")
+    tr, trr = pmc_traffic(PROX3D_NAME)
     out["roofline"]["traffic"], out["roofline"]["traffic_fetch_uncorrected"] = tr, trr
     E.close()
     def _cpu():  # the oracle (OpenMP prox), same mesh and protocol: the FD-Hessian step untimed, then
@@ -326,7 +326,7 @@ def bfgs_bench(mx, with_cpu, threads, admm_iter, steps=3):
                        "bfgs_iters_per_prox": round(bpp, 4), "max_bfgs": st["max_bfgs"]},
            "prox_GBs_algorithmic": round(prox_gbs, 1),
            "prox_us_per_bfgs_iteration": round(prox_ms * 1e3 / max(bpp, 1e-9), 2)}
-    fl = pmc_entry("k_prox_lds<2, 128>@bfgs_heavy").get("fp64_flops_per_launch")
+    fl = pmc_entry(prox2d_name() + "@bfgs_heavy").get("fp64_flops_per_launch")
     if fl:
         out["prox_fp64"] = {"executed_flops_per_launch": fl, "achieved_TFLOPs": round(fl / (prox_ms * 1e-3) / 1e12, 2),
                             "peak_TFLOPs": 78.6, "frac": round(fl / (prox_ms * 1e-3) / 1e12 / 78.6, 4),
@@ -392,6 +392,16 @@ def tv_bench(mx, n, admm_iter, steps=3):
            "regrids": E.stats()["regrids"]}
     E.close()
     return out
+
+
+def prox2d_name():
+    """the steady 2D prox kernel the engine launches (workgroup size: MMX_PROX_BLOCK, default 64)"""
+    return "k_prox_lds<2, %d>" % int(os.environ.get("MMX_PROX_BLOCK", "64"))
+
+
+# the steady 3D prox on the full-row (anisotropic) monitor grid; isotropic grids launch the <3, false, true>
+# instance
+PROX3D_NAME = "k_prox_wave<3, false, false>"
 
 
 def pmc_entry(kernel):
@@ -620,7 +630,7 @@ def main():
     xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
     prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
     xup_gbs = st["xupdate_bytes"] / (xup_ms * 1e-3) / 1e9
-    prox_name = "k_prox_wave<3, false>" if c4 else "k_prox_lds<2, %d>" % int(os.environ.get("MMX_PROX_BLOCK", "128"))
+    prox_name = PROX3D_NAME if c4 else prox2d_name()
     # the committed PMC passes profile the default run (C3 and the C4 section): per-launch figures
     # of another mesh size do not apply to C5
     traffic, traffic_raw = pmc_traffic(prox_name) if not c5 else (None, None)

@@ -26,7 +26,8 @@ namespace mmx {
 
 constexpr int kBlock = 256;
 constexpr int kLdsStride = kBlock + 1;  // padded SoA stride of the LDS Bkinv image
-constexpr int kProxBlock = 128;         // steady-state 2D prox workgroup (measured: 128 > 256 > 64 end to end)
+constexpr int kProxBlock = 64;          // steady-state 2D prox workgroup (round 4, with the isotropic grid and recomputed
+                                        // coordinates: 64 0.322 ms, 128 0.327-0.348, 256 0.366 at C3; round 3: 128 > 256 > 64)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
