@@ -1113,6 +1113,9 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 #ifndef MMX_WAVE_OCC2
 #define MMX_WAVE_OCC2 2  // k_prox_wave<2> (MMX_PROX2D=wave): waves per SIMD
 #endif
+#ifndef MMX_WAVE_PERSIST
+#define MMX_WAVE_PERSIST 0  // 3D: a persistent grid of this many one-wave workgroups (a multiple of 8), 0: one per block
+#endif
 #ifndef MMX_WAVE_XCD
 #define MMX_WAVE_XCD 1  // measured C4: prox 3.42 -> 3.29 ms (neighbouring tets share x and monitor-grid lines in one L2)
 #endif
@@ -1238,6 +1241,21 @@ __global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_p
                                                      int useCache) {
   constexpr int K = D * (D + 1);
   __shared__ __attribute__((aligned(16))) double ldsHeld[WaveB<K>::kHeld > 0 ? WaveB<K>::kHeld * K * 64 : 2];
+#if MMX_WAVE_PERSIST
+  if constexpr (D == 3) {
+    // persistent waves (experiment): workgroup w on XCD c = w % 8 walks the XCD's contiguous range of
+    // blocks with stride gridDim / 8, so a wave starts its next block without ending (no drain of its
+    // stores before the next block's loads are issued by a new wave)
+    const int nb = (m.nF + 63) / 64, g8 = (int)gridDim.x / 8, c = (int)(blockIdx.x % 8), j = (int)(blockIdx.x / 8);
+    const int q = nb / 8, r = nb % 8, lo = c * q + min(c, r), hi = lo + q + (c < r ? 1 : 0);
+    for (int lb = lo + j; lb < hi; lb += g8) {
+      // (the next block's held-row DMA into ldsHeld is issued after this block's last reads of it
+      // have returned: the final rows' stores consume them)
+      prox_wave_block<D, COMP, false, ISO>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
+    }
+    return;
+  }
+#endif
   const int lb = MMX_WAVE_XCD ? logical_block_any() : (int)blockIdx.x;  // XCD-contiguous tet ranges
   prox_wave_block<D, COMP, false, ISO>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
 }
@@ -2302,7 +2320,7 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
     }
 #define MMX_WAVE3(C, I)                                                                                            \
   do {                                                                                                           \
-    hipLaunchKernelGGL((k_prox_wave<D, C, I>), dim3(*nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc); \
+    hipLaunchKernelGGL((k_prox_wave<D, C, I>), dim3(MMX_WAVE_PERSIST ? std::min(*nblocks, MMX_WAVE_PERSIST) : *nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc); \
     hipLaunchKernelGGL((k_prox_wave_fix<D, C, I>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);          \
   } while (0)
     if (m.compMesh) {
