@@ -630,7 +630,8 @@ def main():
     xup_ms = st["t_xupdate_ms"] / max(st["n_xupdate"], 1)
     prox_gbs = st["prox_bytes"] / (prox_ms * 1e-3) / 1e9
     xup_gbs = st["xupdate_bytes"] / (xup_ms * 1e-3) / 1e9
-    prox_name = PROX3D_NAME if c4 else prox2d_name()
+    # 3D: the isotropic-grid instance when the monitor grid is isotropic (C5's moving bump)
+    prox_name = (PROX3D_NAME.replace("false>", "true>") if st["monitor_iso"] else PROX3D_NAME) if c4 else prox2d_name()
     # the committed PMC passes profile the default run (C3 and the C4 section): per-launch figures
     # of another mesh size do not apply to C5
     traffic, traffic_raw = pmc_traffic(prox_name) if not c5 else (None, None)
