@@ -9,7 +9,9 @@ disabled, SURVEY §8d protocol); value = ADMM iterations per second over the tim
 first warm-up step (finite-difference Hessians) is reported separately.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-For N > 1 launch with torch.distributed.run: the global mesh grows with N (hexagonal disc of
+N > 1 runs N ranks, one per GPU: under a launcher (torch.distributed.run, WORLD_SIZE = N) directly,
+otherwise bench.py re-launches itself under torch.distributed.run before anything touches the GPU
+(fewer than N visible GPUs, or WORLD_SIZE != N: exit status 2, no line).  The global mesh grows with N (hexagonal disc of
 N_disc = 577*sqrt(N), ~N million nodes) and is element-partitioned across the ranks, one per GPU,
 exchanging interface-slot values with their neighbouring ranks over RCCL send/recv (recursive
 coordinate bisection of the simplex centroids; weak scaling).
@@ -38,7 +40,9 @@ DEFERRED = []
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE, else 1); without WORLD_SIZE, N > 1 re-launches "
+                         "this script under torch.distributed.run with N processes")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--admm-iter", type=int, default=10)
@@ -61,6 +65,66 @@ def parse():
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def launch_plan(gpus, env, n_visible):
+    """How a `bench.py --gpus N` invocation runs (the reference's one parallelism knob is its thread
+    count, main.cpp:788-799 -> src/Mesh.cpp:436-438; here it is N ranks, one per GPU):
+      ("run", world)  -- this process is one rank of `world` (WORLD_SIZE set by a launcher, or N = 1)
+      ("spawn", N)    -- no launcher: re-launch under torch.distributed.run with N processes
+      ("error", msg)  -- N and the launcher disagree, or fewer than N GPUs are visible
+    n_visible: a callable giving the visible GPU count (only called when it matters).  A --gpus N run
+    never falls back to fewer ranks."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if gpus is not None and gpus != world:
+            return ("error", "bench.py --gpus %d launched with WORLD_SIZE=%d" % (gpus, world))
+        if world > 1 and n_visible() < world:
+            return ("error", "bench.py: WORLD_SIZE=%d but only %d GPU(s) visible" % (world, n_visible()))
+        return ("run", world)
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        return ("error", "bench.py --gpus %d: need at least one GPU" % n)
+    if n == 1:
+        return ("run", 1)
+    have = n_visible()
+    if have < n:
+        return ("error", "bench.py --gpus %d: only %d GPU(s) visible, device %d is missing" % (n, have, have))
+    return ("spawn", n)
+
+
+def parallelism_label(world):
+    return ("single" if world == 1 else
+            "element-partition x%d (RCB, RCCL halo send/recv of interface slots)" % world)
+
+
+def visible_gpus():
+    """GPU count from a child process, so this one never touches the GPU before it re-launches."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(n):
+    """N ranks under torch.distributed.run (127.0.0.1 rendezvous); this process only waits for them
+    and exits with their status (a child process, not an exec)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    log("re-launching %d ranks:" % n, " ".join(cmd))
+    return subprocess.run(cmd).returncode
 
 
 def spmv_bench(torch, la, mx, with_cpu):
@@ -523,6 +587,19 @@ def stream_copy_ceiling(torch, la):
     return round(kern, 1), round(2 * 8 * n / (tms * 1e-3) / 1e9, 1)
 
 
+def lib_provenance(mx):
+    """the library's embedded source hash against the sources of the tree this run is in"""
+    info = mx.build_info()
+    sys.path.insert(0, os.path.join(ROOT, "mm-admm_amd", "tools"))
+    try:
+        import src_hash
+        tree = src_hash.source_hash()
+    except Exception:  # noqa: BLE001 -- reported as unknown
+        tree = None
+    return {"lib_src_hash": info.get("src_hash"), "lib_git": info.get("git"), "tree_src_hash": tree,
+            "lib_matches_tree": tree is not None and tree == info.get("src_hash")}
+
+
 def pmc_flops(kernel):
     """Executed fp64 flops per launch from the SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 pass."""
     return pmc_entry(kernel).get("fp64_flops_per_launch")
@@ -530,10 +607,17 @@ def pmc_flops(kernel):
 
 def main():
     args = parse()
+    # before anything touches the GPU: a --gpus N run is N ranks, or it fails
+    plan, val = launch_plan(args.gpus, os.environ, visible_gpus)
+    if plan == "error":
+        log(val)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(relaunch(val))
+    world = val
     import torch  # first, so libmmadmm binds to the same HIP runtime
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -571,8 +655,9 @@ def main():
 
     mesh, M = make_mesh(world)
     t_setup = time.perf_counter()
-    parallelism = "single"
+    parallelism = parallelism_label(world)
     comm = None
+    rccl_nranks = None
     if world > 1:
         # the element-partitioned engine or nothing: a failure here ends the run with a non-zero
         # exit status (no silent fallback to replicas)
@@ -580,7 +665,9 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         comm = mx.Comm.rccl(world, rank, uid[0], local)
         eng = mx.Engine(M, dt, rank=rank, nranks=world, comm=comm)
-        parallelism = f"element-partition x{world} (RCB, RCCL halo send/recv of interface slots)"
+        rccl_nranks = comm.nranks()  # ncclCommCount
+        if rccl_nranks != world:
+            raise RuntimeError("RCCL communicator has %d ranks, expected %d" % (rccl_nranks, world))
     else:
         eng = mx.Engine(M, dt)
     if c5:
@@ -617,6 +704,10 @@ def main():
         elapsed = float(t.item())
 
     st = eng.stats()
+    per_rank = [(eng.nP, eng.nF)]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, (eng.nP, eng.nF))
     # a second run with the early exit enabled reports the iterations actually executed
     eng.reset_stats()
     for _ in range(3):
@@ -660,7 +751,9 @@ def main():
                                 "monitor, dt 0.055 tau 0.5 rho 50, %d ADMM iterations per step"
                                 % (used["n"], mesh.nP, mesh.nF, args.admm_iter)),
                    "global_nodes": mesh.nP, "global_simplices": mesh.nF, "nodes_rank0": eng.nP,
-                   "simplices_rank0": eng.nF, "admm_iter": args.admm_iter, "parallelism": parallelism,
+                   "simplices_rank0": eng.nF, "nodes_per_rank": [p[0] for p in per_rank],
+                   "simplices_per_rank": [p[1] for p in per_rank], "rccl_nranks": rccl_nranks,
+                   "admm_iter": args.admm_iter, "parallelism": parallelism,
                    "value_unit_note": "ADMM it/s x global nodes / %d" % base_nodes},
         "roofline": {"bound": "hbm", "kernel": prox_name,
                      "achieved": round(prox_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -678,6 +771,7 @@ def main():
                        "admm_iters_per_step": round(st_early["admm_iters"] / 3, 2)},
         "first_step_ms": round(first_ms, 2),
         "setup_s": round(t_setup, 2),
+        "build": lib_provenance(mx),
     }
     fl = pmc_flops(prox_name) if not c5 else None
     if fl:

@@ -118,6 +118,9 @@ int mmadmm_set_regrid(mmadmm_handle h, int every_step);
 
 const char* mmadmm_last_error(void);
 int mmadmm_version(void);
+/* provenance (no reference counterpart): "src_hash=<16 hex> git=<describe> arch=gfx950", the hash of
+ * the library's sources as mm-admm_amd/tools/src_hash.py computes it at build time */
+int mmadmm_build_info(char* out, int len);
 
 /* built-in monitors MEx0..MEx5 (dim 2) and MEx0/13D/23D/33D/0/53D (dim 3) by MonType 0..5, MonType 7 a
  * time-varying bump M = (1 + 5 / (1 + 50 |x - c(t)|^2)) I, c(t) = (0.5 + 0.2 cos 2 pi t, 0.5 + 0.2 sin 2 pi t,
@@ -150,7 +153,8 @@ int mmadmm_step(mmadmm_handle h, int n_iters, double tol, double* Ih, int* admm_
 int mmadmm_euler_step(mmadmm_handle h, double* Ih);
 /* method 2: one backward Euler step (Newton + ILU(0) CG-STAB); single rank only */
 int mmadmm_backward_euler_step(mmadmm_handle h, double dt, double tol, double* Ih, int* newton_iters);
-/* the last assembled backward-Euler Jacobian (CSR over D*nP unknowns); null arrays are skipped */
+/* the last assembled backward-Euler Jacobian (CSR over D*nP unknowns; mmadmm_be_fsubjac does not
+ * replace it); null arrays are skipped */
 int mmadmm_get_jacobian(mmadmm_handle h, long long* nnz, int32_t* ia, int32_t* ja, double* a);
 /* backward Euler in pieces (single rank): xn = x, Ih = eulerStepMod(x), x -= (dt/tau) grad */
 int mmadmm_be_begin(mmadmm_handle h, double dt, double* Ih);
@@ -243,6 +247,8 @@ typedef int (*mmadmm_exchange_fn)(void* user, int npeers, const int* peer_rank, 
 int mmadmm_comm_create_host(int nranks, int rank, mmadmm_allgather_fn allgather, mmadmm_exchange_fn exchange,
                             void* user, mmadmm_comm* out);
 int mmadmm_comm_destroy(mmadmm_comm c);
+/* ranks of the communicator: for RCCL what ncclCommCount reports, else the count it was made with */
+int mmadmm_comm_nranks(mmadmm_comm c, int* nranks);
 /* like mmadmm_create, given the GLOBAL mesh on every rank; p->rank / p->nranks select the
  * share.  mmadmm_get / mmadmm_get_simplices then return this rank's nodes / simplices (in
  * global ids); mmadmm_local_nodes lists the global ids of the local nodes. */

@@ -31,6 +31,11 @@ struct RcclComm final : Comm {
   ~RcclComm() override {
     if (comm) (void)ncclCommDestroy(comm);
   }
+  int transport_ranks() override {
+    int n = 0;
+    MMX_NCCL(ncclCommCount(comm, &n));
+    return n;
+  }
   void allgather(int, const double* dsend, double* drecv, size_t count, hipStream_t st) override {
     MMX_NCCL(ncclAllGather(dsend, drecv, count, ncclDouble, comm, st));
   }
@@ -231,6 +236,13 @@ int mmadmm_comm_create_host(int nranks, int rank, mmadmm_allgather_fn allgather,
     if (!out || nranks < 1 || rank < 0 || rank >= nranks || !allgather || !exchange)
       throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_comm_create_host: bad arguments");
     *out = new mmadmm_comm_s{new mmx::HostComm(nranks, rank, allgather, exchange, user)};
+  });
+}
+
+int mmadmm_comm_nranks(mmadmm_comm c, int* nranks) {
+  return mmx::guarded([&] {
+    if (!c || !c->c || !nranks) throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_comm_nranks: bad arguments");
+    *nranks = c->c->transport_ranks();
   });
 }
 

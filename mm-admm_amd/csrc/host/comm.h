@@ -18,6 +18,8 @@ namespace mmx {
 struct Comm {
   int nranks = 1;
   virtual ~Comm() = default;
+  // the ranks the transport itself reports (RCCL: ncclCommCount)
+  virtual int transport_ranks() { return nranks; }
   // recv[q*count .. (q+1)*count) = rank q's send block (device pointers, stream-ordered)
   virtual void allgather(int rank, const double* dsend, double* drecv, size_t count, hipStream_t st) = 0;
   // for every peer p: send rows [p.sendOff, p.sendOff + p.sendCount) of dsend to p.rank, receive

@@ -285,6 +285,7 @@ class Engine final : public EngineBase {
     // Mesh<D>::setUp (src/Mesh.cpp:1006-1014, commented in the reference): time-varying monitors
     if (regridEachStep_) regrid(stepsTaken_ * prm_.dt);
     ensureResults(nIters);
+    clearInvFlag();
     const bool timing = timing_;
     hipEvent_t eStep0 = nullptr, eStep1 = nullptr;
     size_t evMark = evUsed_;
@@ -429,6 +430,7 @@ class Engine final : public EngineBase {
 
   // MeshIntegrator::eulerStep -> Mesh::eulerStepMod (src/Mesh.cpp:532-579)
   double eulerStep() override {
+    clearInvFlag();
     int nb = 0;
     launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
     launch_reduce_partials(partA_.p, nb, results_.p, st_);
@@ -454,6 +456,7 @@ class Engine final : public EngineBase {
     const double dtot = dtBE / prm_.tau;
     const double SAFETY_FAC = 1.0 / 10.0;
     const int MAX_ITERS = 1000;
+    clearInvFlag();
     MMX_HIP(hipMemcpyAsync(xn_.p, x_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st_));
     int nb = 0, nb2 = 0;
     launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);  // initial guess
@@ -511,6 +514,7 @@ class Engine final : public EngineBase {
     const int n = nP_ * D;
     std::vector<double> rv;
     int nb = 0, nb2 = 0;
+    if (op == 0 || op == 1) clearInvFlag();
     if (op == 0) {
       MMX_HIP(hipMemcpyAsync(xn_.p, x_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st_));
       launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
@@ -536,10 +540,12 @@ class Engine final : public EngineBase {
     } else if (op == 2) {
       const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
       launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
-      launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, 1.0, jval_.p, st_, false);
-      MMX_HIP(hipMemcpyAsync(out, jval_.p, jja_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
+      clearInvFlag();  // the FD blocks report no inversion (their energies are not checked)
+      // into a scratch buffer: jval_ keeps the engine's last assembled Jacobian (mmadmm_get_jacobian)
+      if (jraw_.n != jja_.n) jraw_.alloc(std::max<size_t>(jja_.n, 1));
+      launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, 1.0, jraw_.p, st_, false);
+      MMX_HIP(hipMemcpyAsync(out, jraw_.p, jja_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
       MMX_HIP(hipStreamSynchronize(st_));
-      jacVp_ = -1;  // jval_ no longer holds the engine's own Jacobian
     } else if (op == 3) {
       MMX_HIP(hipMemcpyAsync(dx_.p, in, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st_));
       launch_add_inplace(n, x_.p, dx_.p, st_);
@@ -562,6 +568,7 @@ class Engine final : public EngineBase {
   double energy() override {
     int nb = 0;
     launch_energy<D>(m_, Vp_.p, partA_.p, &nb, st_);
+    clearInvFlag();  // energy() returns NaN for an inverted element without reporting it
     launch_reduce_partials(partA_.p, nb, results_.p, st_);
     std::vector<double> rv;
     fetchResults(results_.p, 1, rv);
@@ -714,6 +721,7 @@ class Engine final : public EngineBase {
     const auto t0 = Clock::now();
     const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
     launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
+    clearInvFlag();
     launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, dtBE / prm_.tau, jval_.p, st_);
     MMX_HIP(hipStreamSynchronize(st_));
     MMX_SP(mmx_matrix_set_values_device(jac_, jval_.p));
@@ -868,10 +876,12 @@ class Engine final : public EngineBase {
     double diam = 0.0;
     for (int d = 0; d < D; ++d) diam += extMax_[d] * extMax_[d];
     diam = std::sqrt(diam);
+    const char* mg = getenv("MMX_REGRID_MARGIN");  // tests: 0 forces the fallback below
+    const double marginScale = mg ? atof(mg) : 1.0;
     for (int d = 0; d < D; ++d) {
       const std::vector<double>& g = d == 0 ? grid_.gx : d == 1 ? grid_.gy : grid_.gz;
       const int sd = (D == 3 && d < 2) ? 1 - d : d;  // the storage axis holding coordinate axis d
-      const double mu = diam + 2.0 * (g[1] - g[0]);
+      const double mu = marginScale * (diam + 2.0 * (g[1] - g[0]));
       slo[d] = g[H.lo[sd]] - mu;
       shi[d] = g[H.hi[sd]] + mu;
     }
@@ -920,7 +930,16 @@ class Engine final : public EngineBase {
     ensureCells(cg);
     launch_bin<D>(rgnCandX_.p, nCand, cg, rgnCellOf_.p, rgCounts_.p, rgStarts_.p, rgFill_.p, rgnNodes_.p, rgScan_.p,
                   rgScanBytes_, st_);
-    NnCand nc{rgnCandGid_.p, {slo[0], slo[1], slo[2]}, {shi[0], shi[1], shi[2]}, rgnCnt_.p + nranks_};
+    // the fill's exactness check: a vertex this rank lacks lies outside S, beyond one of S's sides --
+    // but not beyond a side at or past the global vertex box (every vertex x has lo <= x <= hi, and S
+    // holds x >= slo, x <= shi): such a side is infinitely far (a disc's grid corners are far from
+    // every vertex, nearer S's outer side than any vertex)
+    double clo[3], chi[3];
+    for (int d = 0; d < 3; ++d) {
+      clo[d] = (d < D && slo[d] <= lo[d]) ? -INFINITY : slo[d];
+      chi[d] = (d < D && shi[d] >= hi[d]) ? INFINITY : shi[d];
+    }
+    NnCand nc{rgnCandGid_.p, {clo[0], clo[1], clo[2]}, {chi[0], chi[1], chi[2]}, rgnCnt_.p + nranks_};
     launch_nn_fill<D>(rgnCandX_.p, cg, rgStarts_.p, rgnNodes_.p, gx_.p, gy_.p, D == 3 ? gz_.p : gy_.p, grid_.nx,
                       grid_.ny, grid_.nz, rgnMon_.p, rgTmp_.p, H, st_, nc);
     int fail = 0;
@@ -1307,6 +1326,10 @@ class Engine final : public EngineBase {
   // A NaN energy: an element met Edet <= 0 (the reference's assert(Edet > 0)) if a blockGrad set
   // the inverted flag, else a monitor value that is not finite -- on an element partition with a
   // time-varying monitor, an evaluation outside the grid box this rank rebuilt (its rows are NaN).
+  // the inverted flag is set by any blockGrad that meets Edet <= 0 (energy(), the FD Jacobian
+  // included) and read only by throwBad: every operation that can report starts from a clear flag
+  void clearInvFlag() { MMX_HIP(hipMemsetAsync(tieCount_.p + 2, 0, sizeof(unsigned), st_)); }
+
   [[noreturn]] void throwBad(const char* where) {
     unsigned flag = 0;
     MMX_HIP(hipMemcpyAsync(&flag, tieCount_.p + 2, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
@@ -1387,7 +1410,7 @@ class Engine final : public EngineBase {
   long long vpVersion_ = 0, jacVp_ = -1;  // Vp generation; the one the Jacobian was built at
   double jacDt_ = 0.0;
   DevBuf<int32_t> jia_, jja_;
-  DevBuf<double> jval_, dv_, xn_, rhs_, dx_;
+  DevBuf<double> jval_, jraw_, dv_, xn_, rhs_, dx_;
   int stepsTaken_ = 0;
   size_t maxBlocks_ = 1;                 // partial-sum rows per launch (upper bound)
   static constexpr int kDeferMax = 64;   // deferred reductions up to this many ADMM iterations

@@ -23,7 +23,7 @@ struct DeviceMesh {
   // the x-update's term w (w (z - u)) of every local slot, written by the prox in the slot layout
   // of z: the x-update then gathers D values per slot instead of 2 D (nullptr: it gathers z and u)
   double* tslot;
-  double* gcache;         // per simplex K+1: unregularised gradient and energy at the current z
+  double* gcache;         // per simplex K doubles: the unregularised gradient at the current z
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
   unsigned* tieStale;      // the previous steady prox's counter, cleared by this prox's recomputation

@@ -134,6 +134,8 @@ def lib():
     L.mmadmm_comm_create_rccl.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.mmadmm_comm_create_loopback.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.mmadmm_comm_destroy.argtypes = [vp]
+    L.mmadmm_comm_nranks.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.mmadmm_build_info.argtypes = [ctypes.c_char_p, ctypes.c_int]
     L.mmadmm_comm_create_host.argtypes = [ctypes.c_int, ctypes.c_int, ALLGATHER_FN, EXCHANGE_FN, vp, ctypes.POINTER(vp)]
     L.mmadmm_be_begin.argtypes = [vp, ctypes.c_double, c_double_p]
     L.mmadmm_be_residual.argtypes = [vp, ctypes.c_double, c_double_p, c_double_p, c_double_p]
@@ -150,6 +152,13 @@ def lib():
     L.mmadmm_plan_destroy.argtypes = [vp]
     _lib = L
     return L
+
+
+def build_info():
+    """{"src_hash": ..., "git": ..., "arch": ...} embedded in libmmadmm.so at build time"""
+    buf = ctypes.create_string_buffer(256)
+    _check(lib().mmadmm_build_info(buf, 256))
+    return dict(kv.split("=", 1) for kv in buf.value.decode().split())
 
 
 def _close_at_exit(obj):
@@ -355,7 +364,13 @@ class Comm:
         """A communicator over the caller's host transport (one process per rank; `transport` has
         allgather(send, recv) and exchange(peers, sends, recvs) on numpy arrays, e.g.
         TorchDistTransport over a gloo process group): the engine stages its blocks through pinned
-        host memory and calls the transport in the same order on every rank."""
+        host memory and calls the transport in the same order on every rank.
+
+        Failure: a transport call that raises is reported to that rank's engine as MMADMM_ERR_RCCL,
+        and the transport's abort() (if it has one) is called first, so that the other ranks, blocked
+        in the same collective, fail too instead of waiting forever.  TorchDistTransport.abort ends
+        the gloo process group; without an abort the caller must tear down every rank when any rank
+        reports MMADMM_ERR_RCCL."""
 
         def ag(_user, send, recv, count):
             try:
@@ -367,6 +382,7 @@ class Comm:
             except BaseException:  # noqa: BLE001 -- reported to the engine as a status
                 import traceback
                 traceback.print_exc()
+                _abort(transport)
                 return 1
 
         def ex(_user, npeers, peer, send, so, sc, recv, ro, rc):
@@ -384,6 +400,7 @@ class Comm:
             except BaseException:  # noqa: BLE001
                 import traceback
                 traceback.print_exc()
+                _abort(transport)
                 return 1
 
         cag, cex = ALLGATHER_FN(ag), EXCHANGE_FN(ex)
@@ -393,6 +410,12 @@ class Comm:
         c._keep = (cag, cex, transport)  # the callbacks must outlive the communicator
         return c
 
+    def nranks(self):
+        """ranks as the transport reports them (RCCL: ncclCommCount)"""
+        n = ctypes.c_int()
+        _check(lib().mmadmm_comm_nranks(self.h, ctypes.byref(n)))
+        return n.value
+
     def close(self):
         if getattr(self, "h", None):
             lib().mmadmm_comm_destroy(self.h)
@@ -400,6 +423,15 @@ class Comm:
 
     def __del__(self):
         _close_at_exit(self)
+
+
+def _abort(transport):
+    ab = getattr(transport, "abort", None)
+    if ab is not None:
+        try:
+            ab()
+        except BaseException:  # noqa: BLE001 -- best effort: the status is reported either way
+            pass
 
 
 class TorchDistTransport:
@@ -437,6 +469,11 @@ class TorchDistTransport:
                 reqs.append(d.irecv(t.from_numpy(r), q, group=self.group, tag=tag))
         for q in reqs:
             q.wait()
+
+    def abort(self):
+        """End the process group (Comm.host calls this when a transfer failed on this rank): the
+        ranks blocked in a collective or a receive with this one then fail instead of hanging."""
+        self.dist.destroy_process_group(self.group)
 
 
 def partition_plan(dim, Xp, F, nranks, rank, method="rcb"):

@@ -1,0 +1,89 @@
+"""bench.py's --gpus N contract: N ranks or a non-zero exit, decided before
+anything touches the GPU.  The reference's only parallelism knob is its thread count
+(/root/reference/main.cpp:788-799 -> src/Mesh.cpp:436-438); here it is N ranks, one per GPU."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def never():
+    raise AssertionError("device count queried when it does not matter")
+
+
+def test_single_gpu_default():
+    assert bench.launch_plan(None, {}, never) == ("run", 1)
+    assert bench.launch_plan(1, {}, never) == ("run", 1)
+
+
+def test_spawn_when_no_launcher():
+    assert bench.launch_plan(8, {}, lambda: 8) == ("spawn", 8)
+    assert bench.launch_plan(2, {}, lambda: 8) == ("spawn", 2)
+
+
+def test_too_few_gpus_is_an_error():
+    plan, msg = bench.launch_plan(2, {}, lambda: 1)
+    assert plan == "error" and "only 1 GPU" in msg and "device 1 is missing" in msg
+    plan, msg = bench.launch_plan(8, {}, lambda: 0)
+    assert plan == "error"
+
+
+def test_under_launcher():
+    env = {"WORLD_SIZE": "8", "RANK": "3", "LOCAL_RANK": "3"}
+    assert bench.launch_plan(8, env, lambda: 8) == ("run", 8)
+    assert bench.launch_plan(None, env, lambda: 8) == ("run", 8)
+    assert bench.launch_plan(4, env, lambda: 8)[0] == "error"  # --gpus disagrees with the launcher
+    assert bench.launch_plan(8, env, lambda: 4)[0] == "error"  # fewer devices than ranks
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}, never) == ("run", 1)
+
+
+def test_parallelism_label():
+    assert bench.parallelism_label(1) == "single"
+    assert bench.parallelism_label(8).startswith("element-partition x8")
+
+
+def test_relaunch_command(monkeypatch):
+    seen = {}
+
+    def fake_run(cmd, **kw):
+        seen["cmd"] = cmd
+        return subprocess.CompletedProcess(cmd, 0)
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "5"])
+    assert bench.relaunch(8) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-3:] == ["--gpus", "8", "--steps", "5"][-3:]
+
+
+def test_no_gpu_here_exits_nonzero():
+    """here (no GPU) a 2-GPU bench must exit non-zero and print no result line"""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present (the -m gpu test covers the one-GPU box)")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "only 0 GPU" in r.stderr and r.stdout.strip() == ""
+
+
+@pytest.mark.gpu
+def test_one_gpu_box_refuses_two_ranks():
+    import torch
+    n = torch.cuda.device_count()
+    if n >= 2:
+        pytest.skip("%d GPUs visible" % n)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert ("only %d GPU" % n) in r.stderr and ("device %d is missing" % n) in r.stderr
+    assert r.stdout.strip() == ""

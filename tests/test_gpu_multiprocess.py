@@ -109,3 +109,4 @@ def test_multiprocess_partition_equals_single(name):
         assert int(d["calls"]) > 0 and int(d["sent"]) > 0  # the halo really went through the transport
         covered[d["ids"]] = True
     assert covered.all()
+

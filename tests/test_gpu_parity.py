@@ -204,6 +204,26 @@ def test_inverted_element_reported():
             G.step(10, -1.0)
 
 
+class _HalfNanMonitor(mx.MonitorFunction):
+    """identity left of x = 0.6, NaN right of it: a monitor value that is not finite"""
+    dim = 2
+
+    def __call__(self, x, M):
+        M[:] = np.nan if x[0] > 0.6 else np.eye(2)
+
+
+def test_nonfinite_monitor_reported_not_as_inverted():
+    """A non-finite monitor value with no inverted element: MMADMM_ERR_NONFINITE
+    (NonFiniteEnergyError), not MMADMM_ERR_INVERTED (every reporting operation starts from a clear
+    inverted flag)."""
+    mesh = mx.MeshData.rect(2, 12)
+    G = mx.Engine(mx.Mesh(mesh.Xp, mesh.F, mesh.mask, _HalfNanMonitor(), rho=50.0, tau=0.5), 0.055)
+    assert np.isnan(G.energy())  # NaN monitor values: energy is NaN, no element inverted
+    with pytest.raises(mx.NonFiniteEnergyError):
+        G.step(5, -1.0)
+    G.close()
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_device_division_by_reciprocal_is_correctly_rounded(seed):
     """div_mk (crmath.h): RN(x/c) from RN(1/c) + one FMA correction, used for the BFGS update's

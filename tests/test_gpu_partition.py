@@ -152,6 +152,53 @@ def test_partitioned_regrid_equals_single(mx, mon, dim, nranks, n, gather, monke
     comm.close()
 
 
+def _regrid_parts(mx, mesh, dim, nranks, steps, rho=200.0, dt=0.05):
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, 7), rho=rho, tau=0.5, device=0)
+    ref = mx.Engine(M, dt)
+    ref.set_regrid(True)
+    for _ in range(steps):
+        ref.step(5, -1.0)
+    comm = mx.Comm.loopback(nranks)
+    parts = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm) for r in range(nranks)]
+    for e in parts:
+        e.set_regrid(True)
+    _run_parallel([(lambda e: (lambda: [e.step(5, -1.0) for _ in range(steps)]))(e) for e in parts])
+    xr = ref.get("x").reshape(-1, dim)
+    for r, e in enumerate(parts):
+        assert np.array_equal(e.get("x").reshape(-1, dim), xr[e.local_nodes()]), f"rank {r}: positions differ"
+    ref.close()
+    return comm, parts
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_partitioned_regrid_disc_no_fallback(mx, nranks):
+    """A non-rectangular domain (the hexagonal disc): the grid box's corners lie outside the disc, far
+    from every vertex.  The exactness check of the near exchange only counts the sides of a rank's
+    search box that lie inside the global vertex box (no vertex can lie beyond the others), so no
+    rebuild falls back to the all-gather."""
+    mesh = mx.MeshData.hexdisc(40, 0.5, 0.5, 0.5)
+    comm, parts = _regrid_parts(mx, mesh, 2, nranks, 3)
+    for r, e in enumerate(parts):
+        st = e.stats()
+        assert st["regrids"] == 3 and st["regrid_fallbacks"] == 0, (r, st)
+        e.close()
+    comm.close()
+
+
+def test_partitioned_regrid_forced_fallback(mx, monkeypatch):
+    """MMX_REGRID_MARGIN=0 shrinks the search box to the rank's own rows: the nearest-vertex check
+    fails at the cut, every rank falls back to all-gathering the vertices (regridNear ->
+    regridAll), and the result is still the single-GPU one."""
+    monkeypatch.setenv("MMX_REGRID_MARGIN", "0")
+    mesh = mx.MeshData.rect(2, 24)
+    comm, parts = _regrid_parts(mx, mesh, 2, 3, 2)
+    for r, e in enumerate(parts):
+        st = e.stats()
+        assert st["regrids"] == 2 and st["regrid_fallbacks"] == 2, (r, st)
+        e.close()
+    comm.close()
+
+
 @pytest.mark.parametrize("dim,n,nranks", [(2, 24, 3), (3, 8, 2)])
 def test_partitioned_regrid_long_run_equals_single(mx, dim, n, nranks):
     """20 steps with the moving-bump monitor (MonType 7) rebuilt at every step on a partition: the
@@ -234,6 +281,7 @@ def test_rccl_communicator_single_rank(mx):
     M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(2, 3), rho=1000.0, tau=0.5, device=0)
     ref = mx.Engine(M, 0.025)
     comm = mx.Comm.rccl(1, 0, mx.Comm.unique_id(), 0)
+    assert comm.nranks() == 1  # ncclCommCount, as bench.py's rccl_nranks
     part = mx.Engine(M, 0.025, rank=0, nranks=1, comm=comm)
     for _ in range(3):
         ref.step(5, -1.0)

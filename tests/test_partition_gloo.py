@@ -250,3 +250,71 @@ def test_host_comm_create_without_gpu():
     c.close()
     with pytest.raises(mx.MMADMMError):
         mx.Comm.host(2, 2, Null())
+
+
+def test_host_comm_failure_aborts_transport():
+    """A transport call that raises: the callback reports status 1 to the engine (MMADMM_ERR_RCCL)
+    and first calls the transport's abort(), so that the other ranks do not wait forever."""
+    import ctypes
+    import mmadmm_amd as mx
+
+    class Failing:
+        aborted = 0
+
+        def allgather(self, s, r):
+            raise RuntimeError("peer gone")
+
+        def exchange(self, peers, sends, recvs):
+            raise RuntimeError("peer gone")
+
+        def abort(self):
+            Failing.aborted += 1
+
+    tr = Failing()
+    c = mx.Comm.host(2, 0, tr)
+    ag, ex = c._keep[0], c._keep[1]
+    s = np.zeros(4)
+    r = np.zeros(8)
+    dp = ctypes.POINTER(ctypes.c_double)
+    assert ag(None, s.ctypes.data_as(dp), r.ctypes.data_as(dp), 4) == 1
+    assert Failing.aborted == 1
+    ll = (ctypes.c_longlong * 1)
+    assert ex(None, 1, (ctypes.c_int * 1)(1), s.ctypes.data_as(dp), ll(0), ll(4), r.ctypes.data_as(dp), ll(0),
+              ll(4)) == 1
+    assert Failing.aborted == 2
+    c.close()
+
+
+def _abort_main(rank, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    import time
+    import mmadmm_amd as mx
+    tr = mx.TorchDistTransport()
+    if rank == 1:
+        time.sleep(1.0)
+        tr.abort()  # what Comm.host does when this rank's transfer failed
+        out[rank] = True
+        return
+    try:
+        tr.allgather(np.ones(3), np.zeros(6))
+        out[rank] = False
+    except Exception:  # noqa: BLE001 -- the peer's abort ends the collective with an error
+        out[rank] = True
+        dist.destroy_process_group()
+
+
+def test_torch_dist_transport_abort_releases_peers():
+    """TorchDistTransport.abort ends the gloo group: a rank blocked in the all-gather with it raises
+    (within seconds) instead of hanging until gloo's 30-minute timeout."""
+    pytest.importorskip("mmadmm_amd")
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    procs = [ctx.Process(target=_abort_main, args=(r, 31811, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert out[0] and out[1]
