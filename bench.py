@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks, one per GPU (default: WORLD_SIZE, else 1); without WORLD_SIZE, N > 1 re-launches "
                          "this script under torch.distributed.run with N processes")
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="N > 1: rccl (one GPU per rank, RCCL send/recv over xGMI; the measurement) or host (the halo "
+                         "exchange through pinned host buffers over a gloo group, ranks may share a GPU: a rehearsal of "
+                         "the N-rank path on a box with fewer GPUs, not a measurement)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--admm-iter", type=int, default=10)
@@ -67,20 +71,21 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def launch_plan(gpus, env, n_visible):
+def launch_plan(gpus, env, n_visible, share=False):
     """How a `bench.py --gpus N` invocation runs (the reference's one parallelism knob is its thread
     count, main.cpp:788-799 -> src/Mesh.cpp:436-438; here it is N ranks, one per GPU):
       ("run", world)  -- this process is one rank of `world` (WORLD_SIZE set by a launcher, or N = 1)
       ("spawn", N)    -- no launcher: re-launch under torch.distributed.run with N processes
       ("error", msg)  -- N and the launcher disagree, or fewer than N GPUs are visible
-    n_visible: a callable giving the visible GPU count (only called when it matters).  A --gpus N run
-    never falls back to fewer ranks."""
+    n_visible: a callable giving the visible GPU count (only called when it matters); share: ranks may
+    share a GPU (--comm host), so the count is not checked.  A --gpus N run never falls back to fewer
+    ranks."""
     ws = env.get("WORLD_SIZE")
     if ws is not None:
         world = int(ws)
         if gpus is not None and gpus != world:
             return ("error", "bench.py --gpus %d launched with WORLD_SIZE=%d" % (gpus, world))
-        if world > 1 and n_visible() < world:
+        if world > 1 and not share and n_visible() < world:
             return ("error", "bench.py: WORLD_SIZE=%d but only %d GPU(s) visible" % (world, n_visible()))
         return ("run", world)
     n = 1 if gpus is None else gpus
@@ -88,15 +93,16 @@ def launch_plan(gpus, env, n_visible):
         return ("error", "bench.py --gpus %d: need at least one GPU" % n)
     if n == 1:
         return ("run", 1)
-    have = n_visible()
+    have = n if share else n_visible()
     if have < n:
         return ("error", "bench.py --gpus %d: only %d GPU(s) visible, device %d is missing" % (n, have, have))
     return ("spawn", n)
 
 
-def parallelism_label(world):
+def parallelism_label(world, comm="rccl"):
     return ("single" if world == 1 else
-            "element-partition x%d (RCB, RCCL halo send/recv of interface slots)" % world)
+            "element-partition x%d (RCB, RCCL halo send/recv of interface slots)" % world if comm == "rccl" else
+            "element-partition x%d (RCB, halo exchange over a gloo host transport; rehearsal)" % world)
 
 
 def visible_gpus():
@@ -608,7 +614,7 @@ def pmc_flops(kernel):
 def main():
     args = parse()
     # before anything touches the GPU: a --gpus N run is N ranks, or it fails
-    plan, val = launch_plan(args.gpus, os.environ, visible_gpus)
+    plan, val = launch_plan(args.gpus, os.environ, visible_gpus, share=args.comm == "host")
     if plan == "error":
         log(val)
         sys.exit(2)
@@ -620,9 +626,12 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    host_comm = world > 1 and args.comm == "host"
+    if host_comm:  # rehearsal: ranks may share the visible GPUs
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if host_comm else "nccl")
     import mmadmm_amd as mx
     import lasolver_amd as la
 
@@ -655,19 +664,22 @@ def main():
 
     mesh, M = make_mesh(world)
     t_setup = time.perf_counter()
-    parallelism = parallelism_label(world)
+    parallelism = parallelism_label(world, args.comm)
     comm = None
     rccl_nranks = None
     if world > 1:
         # the element-partitioned engine or nothing: a failure here ends the run with a non-zero
         # exit status (no silent fallback to replicas)
-        uid = [mx.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = mx.Comm.rccl(world, rank, uid[0], local)
+        if host_comm:
+            comm = mx.Comm.host(world, rank, mx.TorchDistTransport())
+        else:
+            uid = [mx.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = mx.Comm.rccl(world, rank, uid[0], local)
         eng = mx.Engine(M, dt, rank=rank, nranks=world, comm=comm)
-        rccl_nranks = comm.nranks()  # ncclCommCount
+        rccl_nranks = comm.nranks()  # ncclCommCount (host transport: the ranks it was made with)
         if rccl_nranks != world:
-            raise RuntimeError("RCCL communicator has %d ranks, expected %d" % (rccl_nranks, world))
+            raise RuntimeError("communicator has %d ranks, expected %d" % (rccl_nranks, world))
     else:
         eng = mx.Engine(M, dt)
     if c5:
@@ -699,7 +711,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if host_comm else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -732,7 +744,8 @@ def main():
                    "ADMM iterations/sec on 1M-node 2D mesh; achieved HBM GB/s in SpMV"),
         "value": round(iters / elapsed * scale, 3),
         "unit": "ADMM it/s",
-        "n_gpus": world,
+        "n_gpus": min(world, torch.cuda.device_count()) if host_comm else world,
+        "ranks": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -754,6 +767,7 @@ def main():
                    "simplices_rank0": eng.nF, "nodes_per_rank": [p[0] for p in per_rank],
                    "simplices_per_rank": [p[1] for p in per_rank], "rccl_nranks": rccl_nranks,
                    "admm_iter": args.admm_iter, "parallelism": parallelism,
+                   "comm": (args.comm if world > 1 else None),
                    "value_unit_note": "ADMM it/s x global nodes / %d" % base_nodes},
         "roofline": {"bound": "hbm", "kernel": prox_name,
                      "achieved": round(prox_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -2140,7 +2140,8 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
     else if (ts)
       hipLaunchKernelGGL((k_xupdate_sweep<D, true, 8>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
     else
-      hipLaunchKernelGGL((k_xupdate_sweep<D, false, 8>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+      hipLaunchKernelGGL((k_xupdate_sweep<D, false, (D == 2 ? MMX_XU_CH2D : 8)>), g, dim3(kBlock), 0, st, m, sc, xBar,
+                         z, u, x, n8);
     return;
   }
 #define MMX_XU(R, T)                                                                                               \

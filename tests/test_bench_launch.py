@@ -87,3 +87,33 @@ def test_one_gpu_box_refuses_two_ranks():
     assert r.returncode == 2, r.stderr[-2000:]
     assert ("only %d GPU" % n) in r.stderr and ("device %d is missing" % n) in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_host_comm_may_share_gpus():
+    assert bench.launch_plan(2, {}, never, share=True) == ("spawn", 2)
+    assert bench.launch_plan(4, {"WORLD_SIZE": "4"}, never, share=True) == ("run", 4)
+    assert "gloo" in bench.parallelism_label(2, "host")
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_host_transport_rehearsal():
+    """bench.py's N-rank path end to end on a one-GPU box: `--gpus 2 --comm host` re-launches itself
+    under torch.distributed.run, builds the element-partitioned engine on both ranks (sharing the
+    GPU; halo exchange over a gloo host transport), times the steps with the barrier and the max
+    over ranks, and prints one line from rank 0 with both ranks' shares.  Only the transport differs
+    from the RCCL measurement (covered at one rank in tests/test_gpu_partition.py)."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "host", "--steps", "3",
+                        "--warmup", "1", "--disc-n", "120", "--no-cpu-baseline"], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["ranks"] == 2 and d["n_gpus"] >= 1 and d["steps"] == 3
+    cfg = d["config"]
+    assert cfg["parallelism"].startswith("element-partition x2") and cfg["comm"] == "host"
+    assert cfg["rccl_nranks"] == 2 and len(cfg["nodes_per_rank"]) == 2
+    assert sum(cfg["simplices_per_rank"]) == cfg["global_simplices"]
+    assert d["value"] > 0 and d["early_exit"]["admm_iters_per_step"] > 0
