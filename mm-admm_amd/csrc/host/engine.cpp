@@ -189,6 +189,10 @@ class Engine final : public EngineBase {
        // 0.36 -> 0.18 ms; 2D C3: prox +0.027 ms, x-update -0.024 ms); MMX_TSLOT=0/1 overrides
       const char* ts = getenv("MMX_TSLOT");
       tslotOn_ = ts ? atoi(ts) != 0 : (D == 3);
+      const char* sp = getenv("MMX_SPIN");
+      spinWait_ = !(sp && atoi(sp) == 0);
+      const char* zx = getenv("MMX_ZX");  // 0: the step's z = D x by k_gather_z (DeviceMesh::zx)
+      zFromX_ = D == 2 && nranks_ == 1 && !(zx && atoi(zx) == 0);
       if (tslotOn_) tslot_.alloc(std::max<size_t>((size_t)nF_ * K, 1));
     }
     {  // x-update order: nodes by their first incident (local) simplex, then id -- locality of the
@@ -263,6 +267,8 @@ class Engine final : public EngineBase {
     maxBlocks_ = maxBlocks;
     partA_.alloc(maxBlocks * kNumPartials);
     partB_.alloc(maxBlocks * kNumPartials);
+    redScratch_.alloc((size_t)kRedSets * kRedSplit * kNumPartials);
+    red_.scratch = redScratch_.p;
     resultsCap_ = 0;
     ensureResults(64);
     m_ = makeView();
@@ -276,6 +282,8 @@ class Engine final : public EngineBase {
     if (rgnHost_) (void)hipHostFree(rgnHost_);
     if (jac_) (void)mmx_matrix_destroy(jac_);
     for (auto& e : evPool_) (void)hipEventDestroy(e);
+    if (evSync_) (void)hipEventDestroy(evSync_);
+    if (resH_) (void)hipHostFree(resH_);
     if (st_) (void)hipStreamDestroy(st_);
   }
 
@@ -285,10 +293,10 @@ class Engine final : public EngineBase {
     // Mesh<D>::setUp (src/Mesh.cpp:1006-1014, commented in the reference): time-varying monitors
     if (regridEachStep_) regrid(stepsTaken_ * prm_.dt);
     ensureResults(nIters);
-    clearInvFlag();
+    // (no clear of the inverted flag here: within a step every blockGrad that sets it is followed by
+    // a NaN energy that reports it, and energy() / the FD Jacobian clear what they leave)
     const bool timing = timing_;
     hipEvent_t eStep0 = nullptr, eStep1 = nullptr;
-    size_t evMark = evUsed_;
     if (timing) {
       eStep0 = nextEvent();
       MMX_HIP(hipEventRecord(eStep0, st_));
@@ -303,10 +311,17 @@ class Engine final : public EngineBase {
     } else {
       launch_predict<D>(m_, 1, nullptr, x_.p, xPrev_.p, xBar_.p, dtOverTau, st_);
     }
-    // x = xBar; z = D x; first step: z = D xPrev
-    launch_gather_z<D>(m_, stepsTaken_ == 0 ? xPrev_.p : xBar_.p, z_.p, st_);
+    // x = xBar; z = D x; first step: z = D xPrev.  2D on one rank: no pass over z -- the step's first
+    // x-update and first prox take z from these positions (DeviceMesh::zx; C3: -37 us per step)
+    const double* zsrc = stepsTaken_ == 0 ? xPrev_.p : xBar_.p;
+    const bool zFromX = zFromX_ && !wave2d_;
+    if (zFromX)
+      m_.zx = zsrc;
+    else
+      launch_gather_z<D>(m_, zsrc, z_.p, st_);
     gcacheValid_ = false;  // z was reset
     if (!stepTaken_) MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
+    if (!zFromX) m_.zx = nullptr;
     StepScalars sc{prm_.tau, prm_.dt * prm_.dt, w_, dtOverTau};
     int nbx = 0, nbp = 0;
     exchange(0);
@@ -334,6 +349,7 @@ class Engine final : public EngineBase {
       }
       launch_prox<D>(m_, !hessComputed_, gcacheValid_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p,
                      swapB ? B2_.p : B_.p, partA_.p + (deferRed ? slice * i : 0), &nbp, st_);
+      m_.zx = nullptr;  // z is in z_ from the first prox on
       if (swapB) std::swap(B_.p, B2_.p);
       gcacheValid_ = true;  // the prox's last blockGrad left the gradient at the final z
       if (timing) {
@@ -354,23 +370,23 @@ class Engine final : public EngineBase {
       }
       if (deferRed) {
         if (firstProx && i < nIters - 1) {  // reduced at once: the batch below assumes one partial count
-          launch_reduce_partials(partA_.p + slice * i, nbp, results_.p + (size_t)i * 2 * kNumPartials, st_);
+          launch_reduce_partials(partA_.p + slice * i, nbp, res_ + (size_t)i * 2 * kNumPartials, st_, red_);
           firstDeferred = i + 1;
         } else if (i == nIters - 1) {
           const int i0 = firstProx ? i : firstDeferred;
           launch_reduce_steps(partA_.p + slice * i0, slice, nbp, partB_.p, nbx, nIters - i0,
-                              results_.p + (size_t)i0 * 2 * kNumPartials, st_);
+                              res_ + (size_t)i0 * 2 * kNumPartials, st_, red_);
         }
       } else if (resid) {
-        launch_reduce_partials2(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, partB_.p, nbx,
-                                results_.p + (size_t)i * 2 * kNumPartials + kNumPartials, st_);
+        launch_reduce_partials2(partA_.p, nbp, res_ + (size_t)i * 2 * kNumPartials, partB_.p, nbx,
+                                res_ + (size_t)i * 2 * kNumPartials + kNumPartials, st_, red_);
       } else {
-        launch_reduce_partials(partA_.p, nbp, results_.p + (size_t)i * 2 * kNumPartials, st_);
+        launch_reduce_partials(partA_.p, nbp, res_ + (size_t)i * 2 * kNumPartials, st_, red_);
       }
       done = i + 1;
       if (early) {
         std::vector<double> rv;
-        fetchResults(results_.p + (size_t)i * 2 * kNumPartials, 1, rv);
+        fetchResults(res_ + (size_t)i * 2 * kNumPartials, 1, rv);
         const double* r = rv.data();
         primal = sqrt(r[kNumPartials + 2]);
         dual = sqrt(r[1]);
@@ -386,7 +402,7 @@ class Engine final : public EngineBase {
       eStep1 = nextEvent();
       MMX_HIP(hipEventRecord(eStep1, st_));
     }
-    fetchResults(results_.p, done, hostRes_);
+    fetchResults(res_, done, hostRes_);
     MMX_HIP(hipGetLastError());
     bool bad = false;
     long long bf = 0;
@@ -406,21 +422,9 @@ class Engine final : public EngineBase {
     st_stats_.last_primal = primal;
     st_stats_.last_dual = dual;
     st_stats_.steps += 1;
-    if (timing) {
-      float ms = 0;
-      MMX_HIP(hipEventElapsedTime(&ms, eStep0, eStep1));
-      st_stats_.t_step_ms += ms;
-      st_stats_.n_steps_timed += 1;
-      for (auto& t : timed_) {
-        MMX_HIP(hipEventElapsedTime(&ms, t.a0, t.a1));
-        st_stats_.t_prox_ms += ms;
-        st_stats_.n_prox += 1;
-        MMX_HIP(hipEventElapsedTime(&ms, t.a1, t.b1));
-        st_stats_.t_xupdate_ms += ms;
-        st_stats_.n_xupdate += 1;
-      }
-      timed_.clear();
-      evUsed_ = evMark;
+    if (timing) {  // resolved later (stats, reset, or a full pool): no event queries between steps
+      stepEv_.push_back({eStep0, eStep1});
+      if (evUsed_ >= kEvResolve) resolveTimed();
     }
     stepsTaken_++;
     if (bad) throwBad("in prox");
@@ -433,11 +437,11 @@ class Engine final : public EngineBase {
     clearInvFlag();
     int nb = 0;
     launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
-    launch_reduce_partials(partA_.p, nb, results_.p, st_);
+    launch_reduce_partials(partA_.p, nb, res_, st_, red_);
     exchange(1);
     launch_euler_apply<D>(m_, gs_.p, x_.p, prm_.dt / prm_.tau, st_);
     std::vector<double> rv;
-    fetchResults(results_.p, 1, rv);
+    fetchResults(res_, 1, rv);
     const double* r = rv.data();
     if (r[4] > 0) throwBad("in the explicit Euler gradient");
     return r[0];
@@ -470,8 +474,8 @@ class Engine final : public EngineBase {
     do {
       launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
       launch_be_residual<D>(m_, gs_.p, x_.p, xn_.p, dtot, rhs_.p, partB_.p, &nb2, st_);
-      launch_reduce_partials2(partA_.p, nb, results_.p, partB_.p, nb2, results_.p + kNumPartials, st_);
-      fetchResults(results_.p, 1, rv);
+      launch_reduce_partials2(partA_.p, nb, res_, partB_.p, nb2, res_ + kNumPartials, st_, red_);
+      fetchResults(res_, 1, rv);
       if (rv[4] > 0) throwBad("in backward Euler");
       Ih = rv[0];
       const double norm = rv[kNumPartials];
@@ -518,16 +522,16 @@ class Engine final : public EngineBase {
     if (op == 0) {
       MMX_HIP(hipMemcpyAsync(xn_.p, x_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, st_));
       launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
-      launch_reduce_partials(partA_.p, nb, results_.p, st_);
+      launch_reduce_partials(partA_.p, nb, res_, st_, red_);
       launch_euler_apply<D>(m_, gs_.p, x_.p, dt / prm_.tau, st_);
-      fetchResults(results_.p, 1, rv);
+      fetchResults(res_, 1, rv);
       if (rv[4] > 0) throwBad("in backward Euler");
       if (sc) sc[0] = rv[0];
     } else if (op == 1) {
       launch_grad_simplex<D>(m_, x_.p, gs_.p, false, partA_.p, &nb, st_);
       launch_be_residual<D>(m_, gs_.p, x_.p, xn_.p, dt / prm_.tau, rhs_.p, partB_.p, &nb2, st_);
-      launch_reduce_partials2(partA_.p, nb, results_.p, partB_.p, nb2, results_.p + kNumPartials, st_);
-      fetchResults(results_.p, 1, rv);
+      launch_reduce_partials2(partA_.p, nb, res_, partB_.p, nb2, res_ + kNumPartials, st_, red_);
+      fetchResults(res_, 1, rv);
       if (rv[4] > 0) throwBad("in backward Euler");
       std::vector<double> r((size_t)n);
       MMX_HIP(hipMemcpyAsync(r.data(), rhs_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st_));
@@ -569,9 +573,9 @@ class Engine final : public EngineBase {
     int nb = 0;
     launch_energy<D>(m_, Vp_.p, partA_.p, &nb, st_);
     clearInvFlag();  // energy() returns NaN for an inverted element without reporting it
-    launch_reduce_partials(partA_.p, nb, results_.p, st_);
+    launch_reduce_partials(partA_.p, nb, res_, st_, red_);
     std::vector<double> rv;
-    fetchResults(results_.p, 1, rv);
+    fetchResults(res_, 1, rv);
     return rv[0];
   }
 
@@ -637,9 +641,13 @@ class Engine final : public EngineBase {
     if (gridRows) *gridRows = (int)(grid_.vals.size() / (D * D));
   }
 
-  void setTiming(bool on) override { timing_ = on; }
+  void setTiming(bool on) override {
+    resolveTimed();
+    timing_ = on;
+  }
 
   void stats(mmadmm_stats* s) override {
+    resolveTimed();
     *s = st_stats_;
     // algorithmic HBM bytes per launch: prox reads F, sbits, z, u, Bkinv,
     // writes z, u, Bkinv; x is gathered once per node.  x-update reads the incidence CSR,
@@ -656,8 +664,33 @@ class Engine final : public EngineBase {
   }
 
   void resetStats() override {
+    resolveTimed();
     const mmadmm_stats z{};
     st_stats_ = z;
+  }
+
+  // the timed steps' HIP events -> the timers (every step ends with a stream synchronisation, so
+  // its events have completed); the pool is then reused
+  void resolveTimed() {
+    if (stepEv_.empty() && timed_.empty()) return;
+    MMX_HIP(hipStreamSynchronize(st_));
+    float ms = 0;
+    for (auto& p : stepEv_) {
+      MMX_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+      st_stats_.t_step_ms += ms;
+      st_stats_.n_steps_timed += 1;
+    }
+    for (auto& t : timed_) {
+      MMX_HIP(hipEventElapsedTime(&ms, t.a0, t.a1));
+      st_stats_.t_prox_ms += ms;
+      st_stats_.n_prox += 1;
+      MMX_HIP(hipEventElapsedTime(&ms, t.a1, t.b1));
+      st_stats_.t_xupdate_ms += ms;
+      st_stats_.n_xupdate += 1;
+    }
+    stepEv_.clear();
+    timed_.clear();
+    evUsed_ = 0;
   }
 
   void sync() override { MMX_HIP(hipStreamSynchronize(st_)); }
@@ -756,9 +789,28 @@ class Engine final : public EngineBase {
 
   // rows x 2*kNumPartials scalar records on the device -> combined over ranks on the host
   // (sums in rank order; the max-BFGS entry by max)
+  // the stream's work so far has completed: an event polled in a spin (low wake-up latency; the
+  // blocking stream wait costs tens of microseconds per step), or the stream wait (MMX_SPIN=0)
+  void waitStream() {
+    if (!spinWait_) {
+      MMX_HIP(hipStreamSynchronize(st_));
+      return;
+    }
+    if (!evSync_) MMX_HIP(hipEventCreateWithFlags(&evSync_, hipEventDisableTiming));
+    MMX_HIP(hipEventRecord(evSync_, st_));
+    hipError_t r;
+    while ((r = hipEventQuery(evSync_)) == hipErrorNotReady) __builtin_ia32_pause();
+    MMX_HIP(r);
+  }
+
   void fetchResults(const double* dev, int rows, std::vector<double>& out) {
     const size_t cnt = (size_t)rows * 2 * kNumPartials;
     out.resize(cnt);
+    if (resH_) {  // pinned, written by the reductions themselves
+      waitStream();
+      std::memcpy(out.data(), resH_ + (dev - res_), cnt * sizeof(double));
+      return;
+    }
     if (nranks_ == 1) {
       MMX_HIP(hipMemcpyAsync(out.data(), dev, cnt * sizeof(double), hipMemcpyDeviceToHost, st_));
       MMX_HIP(hipStreamSynchronize(st_));
@@ -1320,7 +1372,19 @@ class Engine final : public EngineBase {
   void ensureResults(int nIters) {
     if (nIters <= resultsCap_) return;
     resultsCap_ = std::max(nIters, 64);
-    results_.alloc((size_t)resultsCap_ * 2 * kNumPartials);
+    const size_t n = (size_t)resultsCap_ * 2 * kNumPartials;
+    // one rank: the reductions write their results straight into pinned host memory (no copy
+    // kernel) and the step waits for them by polling an event (MMX_SPIN=0: the stream wait and a
+    // device buffer); C3: the step boundary's host turnaround ~54 us ->
+    if (nranks_ == 1 && spinWait_) {
+      if (resH_) MMX_HIP(hipHostFree(resH_));
+      resH_ = nullptr;
+      MMX_HIP(hipHostMalloc((void**)&resH_, n * sizeof(double), hipHostMallocMapped));
+      MMX_HIP(hipHostGetDevicePointer((void**)&res_, resH_, 0));
+    } else {
+      results_.alloc(n);
+      res_ = results_.p;
+    }
   }
 
   // A NaN energy: an element met Edet <= 0 (the reference's assert(Edet > 0)) if a blockGrad set
@@ -1391,7 +1455,8 @@ class Engine final : public EngineBase {
   bool iso_ = false;
   std::vector<double> gcellH_[3];  // the cell tables' host images (kept until the async uploads finish)
   DevBuf<double> invdiag_, Vc_, gx_, gy_, gz_, gvals_, Vp_, x_, xPrev_, xBar_, z_, u_, gs_, B_, B2_, gcache_, gpad_;
-  DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_;
+  DevBuf<double> partA_, partB_, results_, export_, remote_, resAll_, redScratch_;
+  RedWork red_;  // the split reductions' work space (launch_reduce_*)
   DevBuf<int32_t> expOff_, tieList_, nodeOrder_;
   bool wave2d_ = false;  // 2D prox through k_prox_wave<2> (double-buffered Bkinv)
   DevBuf<unsigned> tieCount_;
@@ -1417,7 +1482,14 @@ class Engine final : public EngineBase {
   bool timing_ = false;
   std::vector<hipEvent_t> evPool_;
   size_t evUsed_ = 0;
+  bool zFromX_ = false;
+  bool spinWait_ = true;         // MMX_SPIN (waitStream)
+  double* res_ = nullptr;        // the reductions' results: results_.p, or the device view of resH_
+  double* resH_ = nullptr;       // pinned, mapped results (one rank)
+  hipEvent_t evSync_ = nullptr;
   std::vector<Timed> timed_;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> stepEv_;
+  static constexpr size_t kEvResolve = 4096;  // events outstanding before a resolution
   mmadmm_stats st_stats_{};
 };
 

@@ -23,6 +23,10 @@ struct DeviceMesh {
   // the x-update's term w (w (z - u)) of every local slot, written by the prox in the slot layout
   // of z: the x-update then gathers D values per slot instead of 2 D (nullptr: it gathers z and u)
   double* tslot;
+  // 2D, one rank: set for a step's first x-update and first prox only -- z = D zx (zx = xBar, or
+  // xPrev in the first step; src/MeshIntegrator.cpp:121,126) is gathered from these positions
+  // instead of read from z, so the step needs no k_gather_z pass; the prox then writes z as usual
+  const double* zx;
   double* gcache;         // per simplex K doubles: the unregularised gradient at the current z
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
@@ -93,14 +97,25 @@ void launch_energy(const DeviceMesh<D>& m, const double* x, double* partials, in
 template <int D>
 void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, double dt_over_tau,
                         hipStream_t st);
-void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st);
+// Work space of the split reductions: each set of partials is cut into kRedSplit fixed ranges, one
+// workgroup each, and a second launch combines the kRedSplit range results of each set in range
+// order -- a fixed shape, so the sums are deterministic.  scratch: kRedSets x kRedSplit x
+// kNumPartials doubles.  A null RedWork (or a set of fewer than kRedSplitMin partials) takes one
+// workgroup per set.
+constexpr int kRedSplit = 32;
+constexpr int kRedSplitMin = 4096;
+constexpr int kRedSets = 66;  // kDeferMax (engine.cpp) + 2
+struct RedWork {
+  double* scratch = nullptr;
+};
+void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st, const RedWork& w = {});
 // a step's reductions at once: results[i*2*kNumPartials ..] from partA slice i (i < n), the x-update's
 // set into the second half of row n-1
 void launch_reduce_steps(const double* partA, size_t stride, int nbA, const double* partB, int nbB, int n,
-                         double* results, hipStream_t st);
-// two reductions in one launch (one workgroup each)
+                         double* results, hipStream_t st, const RedWork& w = {});
+// two reductions in one launch
 void launch_reduce_partials2(const double* partials, int nblocks, double* out, const double* partials2, int nblocks2,
-                             double* out2, hipStream_t st);
+                             double* out2, hipStream_t st, const RedWork& w = {});
 // interface-slot values a rank contributes to the exchange: mode 0 the x-update term
 // w (w (z - u)) per slot, mode 1 the simplex gradient gs per slot (D values each)
 template <int D>

@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
 // A node's incident slots are taken 8 at a time: their offsets, then all their z and u values
 // are requested before the first is added (branch-free: lanes past the end re-read the last
 // slot, a slot of another rank reads its gathered row), then summed in ascending order.
-template <int D, bool RESID, bool TS, int CH = 8>
+template <int D, bool RESID, bool TS, int CH = 8, bool ZX = false>
 __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepScalars& sc,
                                              const double* __restrict__ xBar, const double* __restrict__ z,
                                              const double* __restrict__ u, double* __restrict__ x, int idx,
@@ -254,9 +254,14 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
 #pragma unroll
     for (int c = 0; c < D; ++c) acc[c] = 0.0;
     const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
-    double xb[D];
+    double xb[D], zn[D];
 #pragma unroll
     for (int c = 0; c < D; ++c) xb[c] = xBar[(size_t)v * D + c];
+    // ZX: a step's first x-update without z (DeviceMesh::zx): every local slot of node v holds z = zx_v
+    constexpr bool zv0 = ZX && !TS;
+    if constexpr (zv0)
+#pragma unroll
+      for (int c = 0; c < D; ++c) zn[c] = m.zx[(size_t)v * D + c];
     const double inv = m.invdiag[v];
     for (int t0 = b; t0 < e; t0 += CH) {
       int off[CH];
@@ -275,7 +280,10 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
           const double* pu = loc ? u + off[j] : pz;
 #pragma unroll
           for (int c = 0; c < D; ++c) {
-            zv[j][c] = pz[c];
+            if constexpr (zv0)  // (one rank only: no slot of another rank)
+              zv[j][c] = zn[c];
+            else
+              zv[j][c] = pz[c];
             uv[j][c] = pu[c];
           }
         }
@@ -330,7 +338,7 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
 #ifndef MMX_XU_CH2D
 #define MMX_XU_CH2D 6  // 2D: incident slots requested at once per node (C3: 8 0.066 ms, 6 0.0645, 4 0.079)
 #endif
-template <int D, bool RESID, bool TS>
+template <int D, bool RESID, bool TS, bool ZX = false>
 __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
                                                      const double* __restrict__ xBar,
                                                      const double* __restrict__ z,
@@ -339,7 +347,7 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
   const int lb = logical_block(xcd);
   const int idx = lb * kBlock + threadIdx.x;
   double pv[3] = {0, 0, 0};
-  if (idx < m.nP) xupdate_node<D, RESID, TS, (D == 2 ? MMX_XU_CH2D : 8)>(m, sc, xBar, z, u, x, idx, pv);
+  if (idx < m.nP) xupdate_node<D, RESID, TS, (D == 2 ? MMX_XU_CH2D : 8), ZX>(m, sc, xBar, z, u, x, idx, pv);
   if constexpr (RESID) block_partials<3>(pv, partials, lb);
 }
 // The slot-term x-update (no residual) as a sweep: XCD c (= blockIdx % 8) takes the node-order
@@ -877,10 +885,14 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
   gatherX<D>(x, f, dx);
   double* zs = zg + (size_t)s * K;
   double* us = ug + (size_t)s * K;
+  if (D == 2 && m.zx)
+    gatherX<D>(m.zx, f, z);  // the step's first prox: z = D zx (DeviceMesh::zx)
+  else
+#pragma unroll
+    for (int i = 0; i < K; ++i) z[i] = zs[i];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     dx[i] = dx[i] + us[i];  // DXpU = D x + uBar
-    z[i] = zs[i];
     zold[i] = z[i];
   }
   double B[K * K];
@@ -1015,9 +1027,13 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   double* us = ug + (size_t)s * K;
   double* gc = m.gcache + (size_t)s * K;
   double z[K], z0[K], dx[K], gcv[K];
+  if (m.zx)
+    gatherX<D>(m.zx, f, z);  // the step's first prox: z = D zx (DeviceMesh::zx)
+  else
+#pragma unroll
+    for (int i = 0; i < K; ++i) z[i] = zs[i];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    z[i] = zs[i];
     z0[i] = z[i];  // the entry z, for ||z - zPrev||^2 (no reload at the end)
     dx[i] = us[i];
   }
@@ -1977,6 +1993,55 @@ __global__ void __launch_bounds__(kRed) k_reduce_steps(const double* __restrict_
     reduce_set(partB, nbB, results + (size_t)(n - 1) * 2 * kNumPartials + kNumPartials);
 }
 
+// The split form, two launches (a kernel boundary orders them: no fences or counters, which on the
+// eight-XCD chip cost a device-wide L2 write-back each -- the one-launch form with an arrival counter
+// measured 93 us against 45 us for one workgroup per set): k_reduce_split's workgroup (set q, range
+// r) reduces range r of set q into the scratch, k_reduce_combine sums the kRedSplit range results of
+// each set in range order.  Sets: q < nA are slices of partA (stride apart), q = nA the set partB
+// (when nbB >= 0).
+constexpr int kRedLanes = 256;
+__global__ void __launch_bounds__(kRedLanes) k_reduce_split(const double* __restrict__ partA, size_t stride, int nbA,
+                                                            int nA, const double* __restrict__ partB, int nbB,
+                                                            double* __restrict__ scratch) {
+  __shared__ double red[kRedLanes / 64][kNumPartials];
+  const int q = (int)blockIdx.x / kRedSplit, r = (int)blockIdx.x % kRedSplit;
+  const bool isA = q < nA;
+  const double* p = isA ? partA + (size_t)q * stride : partB;
+  const int nb = isA ? nbA : nbB;
+  const int per = (nb + kRedSplit - 1) / kRedSplit, lo = min(nb, r * per), hi = min(nb, lo + per);
+  const int tid = (int)threadIdx.x;
+  double acc[kNumPartials];
+#pragma unroll
+  for (int i = 0; i < kNumPartials; ++i) acc[i] = 0.0;
+  for (int b = lo + tid; b < hi; b += kRedLanes)
+#pragma unroll
+    for (int i = 0; i < kNumPartials; ++i) {
+      const double v = p[(size_t)b * kNumPartials + i];
+      acc[i] = (i == 5) ? fmax(acc[i], v) : acc[i] + v;
+    }
+#pragma unroll
+  for (int i = 0; i < kNumPartials; ++i) acc[i] = (i == 5) ? wave_max(acc[i]) : wave_sum(acc[i]);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < kNumPartials; ++i) red[tid >> 6][i] = acc[i];
+  __syncthreads();
+  if (tid < kNumPartials) {
+    double v = red[0][tid];
+    for (int w = 1; w < kRedLanes / 64; ++w) v = (tid == 5) ? fmax(v, red[w][tid]) : v + red[w][tid];
+    scratch[(size_t)blockIdx.x * kNumPartials + tid] = v;
+  }
+}
+__global__ void __launch_bounds__(64) k_reduce_combine(const double* __restrict__ scratch, int nA,
+                                                       double* __restrict__ outA, size_t outStride,
+                                                       double* __restrict__ outB) {
+  const int q = (int)blockIdx.x, t = (int)threadIdx.x;
+  if (t >= kNumPartials) return;
+  const double* base = scratch + (size_t)q * kRedSplit * kNumPartials + t;
+  double acc = base[0];
+  for (int k = 1; k < kRedSplit; ++k) acc = (t == 5) ? fmax(acc, base[(size_t)k * kNumPartials]) : acc + base[(size_t)k * kNumPartials];
+  (q < nA ? outA + (size_t)q * outStride : outB)[t] = acc;
+}
+
 __device__ void reduce_set(const double* __restrict__ partials, int nblocks, double* __restrict__ out) {
   // one workgroup of 1024: lane-strided sums in a fixed order (four rows requested at a time),
   // then the wavefront butterflies and the 16 wavefront results in order -- a fixed shape
@@ -2130,6 +2195,11 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   *nblocks = nblk_xcd(m.nP);
   if (m.nP == 0) return;
   const bool ts = useTslot && m.tslot;
+  if (D == 2 && m.zx && !resid && !ts) {  // a step's first x-update: z from DeviceMesh::zx
+    hipLaunchKernelGGL((k_xupdate<D, false, false, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
+                       partials, xcd_map());
+    return;
+  }
   if (!resid && m.xupSweep > 0) {  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU
     const int n8 = ((m.nP + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
     const dim3 g(256 * m.xupSweep);
@@ -2352,16 +2422,37 @@ void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, dou
   if (m.nP == 0) return;
   hipLaunchKernelGGL(k_euler_apply<D>, dim3(nblk_xcd(m.nP)), dim3(kBlock), 0, st, m, gs, x, dt_over_tau, xcd_map());
 }
-void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kRed), 0, st, partials, nblocks, out, partials, nblocks, out);
+// one workgroup per set reads its partials at ~0.1 TB/s (C3: 10 sets of 31 k prox partials took 45 us
+// per step); the split form spreads each set over kRedSplit workgroups
+static bool split_ok(const RedWork& w, int nblocks) { return w.scratch && nblocks >= kRedSplitMin; }
+static void reduce_split(const double* partA, size_t stride, int nbA, int nA, double* outA, size_t outStride,
+                         const double* partB, int nbB, double* outB, const RedWork& w, hipStream_t st) {
+  const int sets = nA + (nbB >= 0 ? 1 : 0);
+  hipLaunchKernelGGL(k_reduce_split, dim3(sets * kRedSplit), dim3(kRedLanes), 0, st, partA, stride, nbA, nA, partB,
+                     nbB, w.scratch);
+  hipLaunchKernelGGL(k_reduce_combine, dim3(sets), dim3(64), 0, st, w.scratch, nA, outA, outStride, outB);
+}
+void launch_reduce_partials(const double* partials, int nblocks, double* out, hipStream_t st, const RedWork& w) {
+  if (split_ok(w, nblocks))
+    reduce_split(partials, 0, nblocks, 1, out, 0, partials, -1, out, w, st);
+  else
+    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kRed), 0, st, partials, nblocks, out, partials, nblocks, out);
 }
 void launch_reduce_steps(const double* partA, size_t stride, int nbA, const double* partB, int nbB, int n,
-                         double* results, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_steps, dim3(n + 1), dim3(kRed), 0, st, partA, stride, nbA, partB, nbB, n, results);
+                         double* results, hipStream_t st, const RedWork& w) {
+  if (split_ok(w, nbA) && n + 1 <= kRedSets)
+    reduce_split(partA, stride, nbA, n, results, (size_t)2 * kNumPartials, partB, nbB,
+                 results + (size_t)(n - 1) * 2 * kNumPartials + kNumPartials, w, st);
+  else
+    hipLaunchKernelGGL(k_reduce_steps, dim3(n + 1), dim3(kRed), 0, st, partA, stride, nbA, partB, nbB, n, results);
 }
 void launch_reduce_partials2(const double* partials, int nblocks, double* out, const double* partials2, int nblocks2,
-                             double* out2, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_partials, dim3(2), dim3(kRed), 0, st, partials, nblocks, out, partials2, nblocks2, out2);
+                             double* out2, hipStream_t st, const RedWork& w) {
+  if (split_ok(w, nblocks))
+    reduce_split(partials, 0, nblocks, 1, out, 0, partials2, nblocks2, out2, w, st);
+  else
+    hipLaunchKernelGGL(k_reduce_partials, dim3(2), dim3(kRed), 0, st, partials, nblocks, out, partials2, nblocks2,
+                       out2);
 }
 template <int D>
 void launch_debug_blockgrad(const DeviceMesh<D>& m, int s, const double* z, const double* dx, double* out, int flags,
