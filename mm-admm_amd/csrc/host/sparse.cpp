@@ -147,8 +147,9 @@ struct Timer {
   bool armed = false;
   void init() {
     if (!a) {
-      MMX_HIP(hipEventCreate(&a));
-      MMX_HIP(hipEventCreate(&b));
+      // timing only: no system-scope fence at the records (engine.cpp nextEvent)
+      MMX_HIP(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+      MMX_HIP(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
     }
   }
   ~Timer() {
