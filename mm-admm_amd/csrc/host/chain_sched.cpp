@@ -12,7 +12,14 @@ namespace mmx {
 
 namespace {
 constexpr int kChainLenCap = 1 << 20;  // longest chain (positions fit the schedule's ints)
-constexpr int kImportLatency = 8;      // iterations a global value takes to reach another band (model)
+// iterations a global value takes to reach another band (model; MMX_CHAIN_LAT overrides)
+static int import_latency() {
+  static int v = [] {
+    const char* e = getenv("MMX_CHAIN_LAT");
+    return e ? std::max(0, atoi(e)) : 8;
+  }();
+  return v;
+}
 int pow2_at_least(int v) {
   int r = 1;
   while (r < v) r <<= 1;
@@ -165,7 +172,7 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
               if (cj >= c0 && cj < c) {
                 sk = std::max<long long>(sk, S.laneSkew[(size_t)b * L + (cj - c0)] + posOf[j] - p + 1);
               } else if (align && cj < c0 && doneAt[j] >= 0) {
-                sk = std::max<long long>(sk, doneAt[j] + kImportLatency - off0 - p);
+                sk = std::max<long long>(sk, doneAt[j] + import_latency() - off0 - p);
               }
             }
           }
@@ -187,7 +194,7 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
               if (part(c, p, g, q, kb, ke) < 0) continue;
               for (int k = kb; k < ke; ++k) {
                 const int j = jaf[k];
-                if (chainOf[j] < c0 && doneAt[j] >= 0) off = std::max(off, doneAt[j] + kImportLatency - (p + sk));
+                if (chainOf[j] < c0 && doneAt[j] >= 0) off = std::max(off, doneAt[j] + import_latency() - (p + sk));
               }
             }
       }
