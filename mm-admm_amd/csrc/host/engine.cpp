@@ -241,16 +241,17 @@ class Engine final : public EngineBase {
       export_.alloc((size_t)std::max<size_t>(plan_.sendOff.size(), 1) * D);
       remote_.alloc((size_t)std::max(plan_.recvRows, 1) * D);
     }
-    z_.alloc((size_t)nF_ * K);
+    // 2D: z and u interleaved per vertex slot in z_ (admm_kernels.hip zu_*), u = z_ + D; 3D: z_, u_
+    z_.alloc((size_t)nF_ * K * (kZUInterleaved ? 2 : 1));
     gcache_.alloc((size_t)nF_ * K);
     tieList_.alloc((size_t)nF_ / 16 + 1);  // prox blocks queued for the exact recomputation
     // [0..1]: queued blocks, double-buffered over the steady proxes (k_prox_fix); [2]: the
     // inverted-element flag (GridView::invFlag), cleared when a failed step reads it
     tieCount_.alloc(3);
     MMX_HIP(hipMemsetAsync(tieCount_.p, 0, 3 * sizeof(unsigned), st_));
-    u_.alloc((size_t)nF_ * K);
+    if (!kZUInterleaved) u_.alloc((size_t)nF_ * K);
     gs_.alloc((size_t)nF_ * K);
-    MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
+    clearU();
     {
       // hessInvs = I (src/Mesh.cpp:456-464), wave-interleaved (bidx) and padded to whole chunks of
       // 256 simplices (the 2D prox copies whole chunks); 3D double-buffered (k_prox_wave)
@@ -315,17 +316,17 @@ class Engine final : public EngineBase {
     // x-update and first prox take z from these positions (DeviceMesh::zx; C3: -37 us per step)
     const double* zsrc = stepsTaken_ == 0 ? xPrev_.p : xBar_.p;
     const bool zFromX = zFromX_ && !wave2d_;
+    if (!stepTaken_) clearU();  // (before z: in 2D the clear takes the whole interleaved buffer)
     if (zFromX)
       m_.zx = zsrc;
     else
       launch_gather_z<D>(m_, zsrc, z_.p, st_);
     gcacheValid_ = false;  // z was reset
-    if (!stepTaken_) MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
     if (!zFromX) m_.zx = nullptr;
     StepScalars sc{prm_.tau, prm_.dt * prm_.dt, w_, dtOverTau};
     int nbx = 0, nbp = 0;
     exchange(0);
-    launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, false, st_);
+    launch_xupdate<D>(m_, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p, &nbx, false, st_);
     const bool early = tol >= 0;
     int done = 0;
     double primal = 0, dual = 0;
@@ -347,7 +348,7 @@ class Engine final : public EngineBase {
         tiePar_ ^= 1;
         std::swap(m_.tieCount, m_.tieStale);
       }
-      launch_prox<D>(m_, !hessComputed_, gcacheValid_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, u_.p, B_.p,
+      launch_prox<D>(m_, !hessComputed_, gcacheValid_, early ? tol / 100 : 1e-3 / 100, x_.p, z_.p, uPtr(), B_.p,
                      swapB ? B2_.p : B_.p, partA_.p + (deferRed ? slice * i : 0), &nbp, st_);
       m_.zx = nullptr;  // z is in z_ from the first prox on
       if (swapB) std::swap(B_.p, B2_.p);
@@ -362,7 +363,7 @@ class Engine final : public EngineBase {
       // the primal residual ||D x - z|| (src/MeshIntegrator.cpp:162) only feeds the early-exit test
       // and the reported last residual: without the early exit it is formed on the last iteration
       const bool resid = early || i == nIters - 1;
-      launch_xupdate<D>(m_, sc, xBar_.p, z_.p, u_.p, x_.p, partB_.p, &nbx, resid, st_, true);
+      launch_xupdate<D>(m_, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p, &nbx, resid, st_, true);
       if (timing) {
         b1 = nextEvent();
         MMX_HIP(hipEventRecord(b1, st_));
@@ -590,8 +591,19 @@ class Engine final : public EngineBase {
     if (what == "x") b = &x_;
     else if (what == "xPrev") b = &xPrev_;
     else if (what == "xBar") b = &xBar_;
-    else if (what == "z") b = &z_;
-    else if (what == "u") b = &u_;
+    else if (what == "z" || what == "u") {
+      if (!kZUInterleaved) {
+        b = what == "z" ? &z_ : &u_;
+      } else {  // de-interleave: slot i of simplex s at s 2K + (i / D) 2D + i % D (+ D for u)
+        std::vector<double> h(z_.n);
+        MMX_HIP(hipMemcpyAsync(h.data(), z_.p, z_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
+        MMX_HIP(hipStreamSynchronize(st_));
+        const int sh = what == "u" ? D : 0;
+        for (int s = 0; s < nF_; ++s)
+          for (int i = 0; i < K; ++i) out[(size_t)s * K + i] = h[(size_t)s * 2 * K + (i / D) * 2 * D + i % D + sh];
+        return;
+      }
+    }
     else if (what == "points") b = &Vp_;
     else if (what == "hess") b = &B_;
     else if (what == "gs") b = &gs_;
@@ -783,7 +795,7 @@ class Engine final : public EngineBase {
   // 1 simplex gradients
   void exchange(int mode) {
     if (nranks_ == 1) return;
-    launch_pack_export<D>(mode, (int)plan_.sendOff.size(), expOff_.p, z_.p, u_.p, gs_.p, w_, export_.p, st_);
+    launch_pack_export<D>(mode, (int)plan_.sendOff.size(), expOff_.p, z_.p, uPtr(), gs_.p, w_, export_.p, st_);
     comm_->exchange(rank_, export_.p, remote_.p, plan_.peers, D, st_);
   }
 
@@ -1485,6 +1497,14 @@ class Engine final : public EngineBase {
   std::vector<hipEvent_t> evPool_;
   size_t evUsed_ = 0;
   bool zFromX_ = false;
+  static constexpr bool kZUInterleaved = (D == 2);  // = kZUInter<D> (admm_kernels.hip)
+  double* uPtr() const { return kZUInterleaved ? z_.p + D : u_.p; }
+  void clearU() {  // u = 0 (2D: the whole interleaved buffer, z included)
+    if (kZUInterleaved)
+      MMX_HIP(hipMemsetAsync(z_.p, 0, z_.n * sizeof(double), st_));
+    else
+      MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
+  }
   bool spinWait_ = true;         // MMX_SPIN (waitStream)
   double* res_ = nullptr;        // the reductions' results: results_.p, or the device view of resH_
   double* resH_ = nullptr;       // pinned, mapped results (one rank)

@@ -71,6 +71,26 @@ __device__ __forceinline__ int logical_block_any() {
   return x * q + min(x, r) + (int)(blockIdx.x / 8);
 }
 
+// z and u of simplex s, slot layout i = n D + c (the reference's D x order).  2D (kZUInter): the two
+// interleaved per vertex slot, [z_n0 z_n1 u_n0 u_n1] (32 B), so the x-update's two gathers of a slot
+// fall in one cache line; the buffer then holds 2 K doubles per simplex and u = z + D.  3D: separate
+// arrays (the x-update reads the slot terms instead).
+template <int D>
+constexpr bool kZUInter = (D == 2);
+template <int D>
+__device__ __forceinline__ size_t zu_base(int s) {
+  return (size_t)s * (kZUInter<D> ? 2 : 1) * (D * (D + 1));
+}
+template <int D>
+__device__ __forceinline__ int zu_i(int i) {
+  return kZUInter<D> ? (i / D) * 2 * D + i % D : i;
+}
+// an incidence entry's slot offset s K + n D -> where its z values start
+template <int D>
+__device__ __forceinline__ size_t zu_off(int off) {
+  return kZUInter<D> ? 2 * (size_t)off : (size_t)off;
+}
+
 // ISO: -1 the monitor path chosen at run time from m.giso; 0 the full-row path only; 1 the
 // isotropic path only (m.giso set).  3D kernels are instantiated per path and launched by m.giso
 // (launch_iso3), so neither path's registers count against the other's.
@@ -175,7 +195,7 @@ __global__ void __launch_bounds__(kBlock) k_gather_z(DeviceMesh<D> m, const doub
   double v[K];
   gatherX<D>(x, f, v);
 #pragma unroll
-  for (int i = 0; i < K; ++i) z[(size_t)s * K + i] = v[i];
+  for (int i = 0; i < K; ++i) z[zu_base<D>(s) + zu_i<D>(i)] = v[i];
 }
 
 // per-simplex gradient of the unregularised functional (Mesh::eulerGrad / eulerStepMod)
@@ -276,8 +296,8 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
 #pragma unroll
           for (int c = 0; c < D; ++c) zv[j][c] = pt[c];
         } else {
-          const double* pz = loc ? z + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
-          const double* pu = loc ? u + off[j] : pz;
+          const double* pz = loc ? z + zu_off<D>(off[j]) : m.remote + (size_t)(-1 - off[j]) * D;
+          const double* pu = loc ? u + zu_off<D>(off[j]) : pz;
 #pragma unroll
           for (int c = 0; c < D; ++c) {
             if constexpr (zv0)  // (one rank only: no slot of another rank)
@@ -316,7 +336,7 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
         double zv[CH][D];
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-          const double* pz = z + (off[j] >= 0 ? off[j] : 0);
+          const double* pz = z + zu_off<D>(off[j] >= 0 ? off[j] : 0);
 #pragma unroll
           for (int c = 0; c < D; ++c) zv[j][c] = pz[c];
         }
@@ -883,16 +903,16 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
   loadXi<D>(m, f, xi);
   double dx[K], z[K], zold[K];
   gatherX<D>(x, f, dx);
-  double* zs = zg + (size_t)s * K;
-  double* us = ug + (size_t)s * K;
+  double* zs = zg + zu_base<D>(s);
+  double* us = ug + zu_base<D>(s);
   if (D == 2 && m.zx)
     gatherX<D>(m.zx, f, z);  // the step's first prox: z = D zx (DeviceMesh::zx)
   else
 #pragma unroll
-    for (int i = 0; i < K; ++i) z[i] = zs[i];
+    for (int i = 0; i < K; ++i) z[i] = zs[zu_i<D>(i)];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    dx[i] = dx[i] + us[i];  // DXpU = D x + uBar
+    dx[i] = dx[i] + us[zu_i<D>(i)];  // DXpU = D x + uBar
     zold[i] = z[i];
   }
   double B[K * K];
@@ -934,9 +954,9 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
   double un[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    zs[i] = z[i];
+    zs[zu_i<D>(i)] = z[i];
     un[i] = dx[i] - z[i];  // uBar = DXpU - z
-    us[i] = un[i];
+    us[zu_i<D>(i)] = un[i];
     const double d = z[i] - zold[i];
     dual2 += d * d;
   }
@@ -1023,19 +1043,19 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
   int f[D + 1];
   loadVerts<D>(m, s, f);
   const unsigned fixedBits = m.sbits[s] & 0xF;
-  double* zs = zg + (size_t)s * K;
-  double* us = ug + (size_t)s * K;
+  double* zs = zg + zu_base<D>(s);
+  double* us = ug + zu_base<D>(s);
   double* gc = m.gcache + (size_t)s * K;
   double z[K], z0[K], dx[K], gcv[K];
   if (m.zx)
     gatherX<D>(m.zx, f, z);  // the step's first prox: z = D zx (DeviceMesh::zx)
   else
 #pragma unroll
-    for (int i = 0; i < K; ++i) z[i] = zs[i];
+    for (int i = 0; i < K; ++i) z[i] = zs[zu_i<D>(i)];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     z0[i] = z[i];  // the entry z, for ||z - zPrev||^2 (no reload at the end)
-    dx[i] = us[i];
+    dx[i] = us[zu_i<D>(i)];
   }
   if (useCache) {
 #pragma unroll
@@ -1108,9 +1128,9 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     double un[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      zs[i] = z[i];
+      zs[zu_i<D>(i)] = z[i];
       un[i] = dx[i] - z[i];  // uBar = DXpU - z
-      us[i] = un[i];
+      us[zu_i<D>(i)] = un[i];
     }
     write_tslot<D>(m, s, z, un);
   }
@@ -1156,14 +1176,14 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
   int f[D + 1];
   loadVerts<D>(m, s, f);
   const unsigned fixedBits = m.sbits[s] & 0xF;
-  double* zs = zg + (size_t)s * K;
-  double* us = ug + (size_t)s * K;
+  double* zs = zg + zu_base<D>(s);
+  double* us = ug + zu_base<D>(s);
   double* gc = m.gcache + (size_t)s * K;
   double z[K], dx[K], gcv[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    z[i] = zs[i];
-    dx[i] = us[i];
+    z[i] = zs[zu_i<D>(i)];
+    dx[i] = us[zu_i<D>(i)];
   }
   if (!EXACT && useCache) {
 #pragma unroll
@@ -1219,7 +1239,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     double dual2 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      const double d = z[i] - zs[i];
+      const double d = z[i] - zs[zu_i<D>(i)];
       dual2 += d * d;
     }
     pv[0] = Ihsave;
@@ -1240,9 +1260,9 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     double un[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      zs[i] = z[i];  // (nontemporal z/u stores measured slower: the x-update and the next prox read them)
+      zs[zu_i<D>(i)] = z[i];  // (nontemporal z/u stores measured slower: the x-update and the next prox read them)
       un[i] = dx[i] - z[i];  // uBar = DXpU - z
-      us[i] = un[i];
+      us[zu_i<D>(i)] = un[i];
     }
     write_tslot<D>(m, s, z, un);
   }
@@ -1963,10 +1983,10 @@ __global__ void __launch_bounds__(kBlock) k_pack_export(int mode, int nExp, cons
                                                          double* __restrict__ out) {
   const int e = blockIdx.x * kBlock + threadIdx.x;
   if (e >= nExp) return;
-  const size_t off = (size_t)expOff[e];
+  const size_t off = (size_t)expOff[e], zo = zu_off<D>(expOff[e]);
 #pragma unroll
   for (int c = 0; c < D; ++c)
-    out[(size_t)e * D + c] = (mode == 0) ? w * (w * (z[off + c] - u[off + c])) : gs[off + c];
+    out[(size_t)e * D + c] = (mode == 0) ? w * (w * (z[zo + c] - u[zo + c])) : gs[off + c];
 }
 
 constexpr int kRed = 1024;
