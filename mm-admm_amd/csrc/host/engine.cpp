@@ -184,6 +184,8 @@ class Engine final : public EngineBase {
     sbits_.upload(sbits.data(), sbits.size(), st_);
     interior_.upload(interior.data(), interior.size(), st_);
     incPtr_.upload(plan_.incPtr.data(), plan_.incPtr.size(), st_);
+    for (size_t v = 0; v + 1 < plan_.incPtr.size(); ++v)
+      maxValence_ = std::max(maxValence_, plan_.incPtr[v + 1] - plan_.incPtr[v]);
     incOff_.upload(plan_.incSrc.data(), plan_.incSrc.size(), st_);
     {  // the x-update terms in the slot layout (DeviceMesh::tslot): 3D only (C4: prox +0.09 ms, x-update
        // 0.36 -> 0.18 ms; 2D C3: prox +0.027 ms, x-update -0.024 ms); MMX_TSLOT=0/1 overrides
@@ -1335,6 +1337,8 @@ class Engine final : public EngineBase {
     {
       const char* xs = getenv("MMX_XUP_SWEEP");  // 3D default: one workgroup per CU (profiles/r03/xupdate)
       m.xupSweep = xs ? std::max(0, atoi(xs)) : (D == 3 ? 1 : 0);
+      const char* xp = getenv("MMX_XUP_PAIR");
+      m.xupPair = (xp && atoi(xp) != 0 && maxValence_ <= 40) ? 1 : 0;
       const char* xc = getenv("MMX_XUP_CH");
       m.xupCh = xc ? atoi(xc) : 8;
     }
@@ -1496,8 +1500,9 @@ class Engine final : public EngineBase {
   bool timing_ = false;
   std::vector<hipEvent_t> evPool_;
   size_t evUsed_ = 0;
+  int maxValence_ = 0;  // largest number of incident slots of a local node
   bool zFromX_ = false;
-  static constexpr bool kZUInterleaved = (D == 2);  // = kZUInter<D> (admm_kernels.hip)
+  static constexpr bool kZUInterleaved = (D == 2) && MMX_ZU_INTER;  // = kZUInter<D> (admm_kernels.hip)
   double* uPtr() const { return kZUInterleaved ? z_.p + D : u_.p; }
   void clearU() {  // u = 0 (2D: the whole interleaved buffer, z included)
     if (kZUInterleaved)

@@ -10,6 +10,10 @@ namespace mmx {
 // v[3] = BFGS iterations, v[4] = error flags (inverted element), v[5] = max BFGS iters.
 constexpr int kNumPartials = 6;
 
+// 2D z / u layout: 1 = interleaved per vertex slot (admm_kernels.hip zu_*), 0 = two arrays
+#ifndef MMX_ZU_INTER
+#define MMX_ZU_INTER 1
+#endif
 template <int D>
 struct DeviceMesh {
   int nP, nF;
@@ -34,6 +38,7 @@ struct DeviceMesh {
   unsigned* invFlag;       // set by a blockGrad that meets Edet <= 0 (GridView::invFlag)
   int xupCh;              // slots requested at once per node in the sweep (8, 16, 24)
   int xupSweep;           // 3D slot-term x-update as a per-XCD sweep: workgroups per CU (0: one node per lane)
+  int xupPair;            // the sweep with two lanes per node (MMX_XUP_PAIR; every node <= 40 incident slots)
   int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
   const int* nodeOrder;   // x-update processing order (nodes by first incident simplex) or nullptr
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)

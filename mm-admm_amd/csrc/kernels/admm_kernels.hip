@@ -76,7 +76,7 @@ __device__ __forceinline__ int logical_block_any() {
 // fall in one cache line; the buffer then holds 2 K doubles per simplex and u = z + D.  3D: separate
 // arrays (the x-update reads the slot terms instead).
 template <int D>
-constexpr bool kZUInter = (D == 2);
+constexpr bool kZUInter = (D == 2) && MMX_ZU_INTER;
 template <int D>
 __device__ __forceinline__ size_t zu_base(int s) {
   return (size_t)s * (kZUInter<D> ? 2 : 1) * (D * (D + 1));
@@ -385,6 +385,62 @@ __global__ void __launch_bounds__(kBlock) k_xupdate_sweep(DeviceMesh<D> m, StepS
   double pv[3];
   for (int idx = lo + w * kBlock + (int)threadIdx.x; idx < hi; idx += per * kBlock)
     xupdate_node<D, false, TS, CH>(m, sc, xBar, z, u, x, idx, pv);
+}
+
+// The slot-term sweep with two lanes per node (MMX_XUP_PAIR, 3D): lanes 2k and 2k + 1 request the
+// first and the second half of the node's incident slot terms, so twice as many of a node's requests
+// are in flight at once; the even lane then adds all of them in ascending order, the odd lane's
+// through a lane swap -- the same sum, bit for bit.  Nodes with more than 2 kXuPairHalf slots are
+// not handed to this kernel (the host checks the largest valence).
+constexpr int kXuPairHalf = 20;
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_xupdate_sweep_pair(DeviceMesh<D> m, StepScalars sc,
+                                                                const double* __restrict__ xBar, double* __restrict__ x,
+                                                                int n8) {
+  constexpr int HN = kBlock / 2;  // nodes per workgroup round
+  const int c = (int)(blockIdx.x % 8), w = (int)(blockIdx.x / 8), per = (int)(gridDim.x / 8);
+  const int lo = c * n8, hi = min(lo + n8, m.nP);
+  const int h = (int)threadIdx.x & 1;
+  for (int base = lo + w * HN; base < hi; base += per * HN) {
+    const int idx = base + ((int)threadIdx.x >> 1);
+    const bool act = idx < hi;
+    const int v = act ? (m.nodeOrder ? m.nodeOrder[idx] : idx) : 0;
+    const int b = act ? m.inc_ptr[v] : 0, e = act ? m.inc_ptr[v + 1] : 0;
+    const int half = (e - b + 1) >> 1;
+    const int mb = b + (h ? half : 0), cnt = h ? (e - b - half) : half;  // my slots [mb, mb + cnt)
+    int off[kXuPairHalf];
+#pragma unroll
+    for (int j = 0; j < kXuPairHalf; ++j) off[j] = (j < cnt) ? m.inc_off[mb + j] : 0;
+    double tv[kXuPairHalf][D];
+#pragma unroll
+    for (int j = 0; j < kXuPairHalf; ++j) {
+      const double* pt = (off[j] >= 0) ? m.tslot + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
+#pragma unroll
+      for (int q = 0; q < D; ++q) tv[j][q] = (j < cnt) ? pt[q] : 0.0;
+    }
+    double acc[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) acc[q] = 0.0;
+#pragma unroll
+    for (int j = 0; j < kXuPairHalf; ++j)
+      if (j < cnt)
+#pragma unroll
+        for (int q = 0; q < D; ++q) acc[q] += tv[j][q];
+    const int cnt1 = e - b - half;  // the odd lane's count, known to both lanes
+#pragma unroll
+    for (int j = 0; j < kXuPairHalf; ++j) {
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        const double o = __shfl_xor(tv[j][q], 1, 64);
+        if (j < cnt1) acc[q] += o;
+      }
+    }
+    if (act && h == 0) {
+      const double inv = m.invdiag[v];
+#pragma unroll
+      for (int q = 0; q < D; ++q) x[(size_t)v * D + q] = ((sc.tau * xBar[(size_t)v * D + q]) + sc.dtsq * acc[q]) * inv;
+    }
+  }
 }
 
 // k x k inverse: unblocked partial-pivot LU + substitution (mirrors the oracle's restatement
@@ -2223,6 +2279,10 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   if (!resid && m.xupSweep > 0) {  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU
     const int n8 = ((m.nP + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
     const dim3 g(256 * m.xupSweep);
+    if (ts && m.xupPair) {
+      hipLaunchKernelGGL((k_xupdate_sweep_pair<D>), g, dim3(kBlock), 0, st, m, sc, xBar, x, n8);
+      return;
+    }
     if (ts && m.xupCh >= 24)
       hipLaunchKernelGGL((k_xupdate_sweep<D, true, 24>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
     else if (ts && m.xupCh >= 16)
