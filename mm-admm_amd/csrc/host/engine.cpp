@@ -184,8 +184,6 @@ class Engine final : public EngineBase {
     sbits_.upload(sbits.data(), sbits.size(), st_);
     interior_.upload(interior.data(), interior.size(), st_);
     incPtr_.upload(plan_.incPtr.data(), plan_.incPtr.size(), st_);
-    for (size_t v = 0; v + 1 < plan_.incPtr.size(); ++v)
-      maxValence_ = std::max(maxValence_, plan_.incPtr[v + 1] - plan_.incPtr[v]);
     incOff_.upload(plan_.incSrc.data(), plan_.incSrc.size(), st_);
     {  // the x-update terms in the slot layout (DeviceMesh::tslot): 3D only (C4: prox +0.09 ms, x-update
        // 0.36 -> 0.18 ms; 2D C3: prox +0.027 ms, x-update -0.024 ms); MMX_TSLOT=0/1 overrides
@@ -195,6 +193,8 @@ class Engine final : public EngineBase {
       spinWait_ = !(sp && atoi(sp) == 0);
       const char* zx = getenv("MMX_ZX");  // 0: the step's z = D x by k_gather_z (DeviceMesh::zx)
       zFromX_ = D == 2 && nranks_ == 1 && !(zx && atoi(zx) == 0);
+      const char* fp = getenv("MMX_FUSE_PRED");  // 0: k_predict runs in every step (DeviceMesh::predBar)
+      fusePred_ = !(fp && atoi(fp) == 0);
       if (tslotOn_) tslot_.alloc(std::max<size_t>((size_t)nF_ * K, 1));
     }
     {  // x-update order: nodes by their first incident (local) simplex, then id -- locality of the
@@ -243,7 +243,7 @@ class Engine final : public EngineBase {
       export_.alloc((size_t)std::max<size_t>(plan_.sendOff.size(), 1) * D);
       remote_.alloc((size_t)std::max(plan_.recvRows, 1) * D);
     }
-    // 2D: z and u interleaved per vertex slot in z_ (admm_kernels.hip zu_*), u = z_ + D; 3D: z_, u_
+    // z_, u_ (MMX_ZU_INTER=1 builds, 2D: the two interleaved per vertex slot in z_, u = z_ + D)
     z_.alloc((size_t)nF_ * K * (kZUInterleaved ? 2 : 1));
     gcache_.alloc((size_t)nF_ * K);
     tieList_.alloc((size_t)nF_ / 16 + 1);  // prox blocks queued for the exact recomputation
@@ -306,12 +306,14 @@ class Engine final : public EngineBase {
     }
     const double dtOverTau = prm_.dt / prm_.tau;
     // predictX (src/Mesh.cpp:649-674), then xPrev = x
+    // (2D, one rank: the extrapolation of steps after the third runs inside the step's first x-update)
+    const bool fusePred = zFromX_ && fusePred_ && !wave2d_ && !(prm_.grad_use || stepsTaken_ <= 2);
     if (prm_.grad_use || stepsTaken_ <= 2) {
       int nb = 0;
       launch_grad_simplex<D>(m_, x_.p, gs_.p, true, partA_.p, &nb, st_);
       exchange(1);
       launch_predict<D>(m_, 0, gs_.p, x_.p, xPrev_.p, xBar_.p, dtOverTau, st_);
-    } else {
+    } else if (!fusePred) {
       launch_predict<D>(m_, 1, nullptr, x_.p, xPrev_.p, xBar_.p, dtOverTau, st_);
     }
     // x = xBar; z = D x; first step: z = D xPrev.  2D on one rank: no pass over z -- the step's first
@@ -328,7 +330,12 @@ class Engine final : public EngineBase {
     StepScalars sc{prm_.tau, prm_.dt * prm_.dt, w_, dtOverTau};
     int nbx = 0, nbp = 0;
     exchange(0);
+    if (fusePred) {
+      m_.predPrev = xPrev_.p;
+      m_.predBar = xBar_.p;
+    }
     launch_xupdate<D>(m_, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p, &nbx, false, st_);
+    m_.predPrev = m_.predBar = nullptr;
     const bool early = tol >= 0;
     int done = 0;
     double primal = 0, dual = 0;
@@ -1337,8 +1344,6 @@ class Engine final : public EngineBase {
     {
       const char* xs = getenv("MMX_XUP_SWEEP");  // 3D default: one workgroup per CU (profiles/r03/xupdate)
       m.xupSweep = xs ? std::max(0, atoi(xs)) : (D == 3 ? 1 : 0);
-      const char* xp = getenv("MMX_XUP_PAIR");
-      m.xupPair = (xp && atoi(xp) != 0 && maxValence_ <= 40) ? 1 : 0;
       const char* xc = getenv("MMX_XUP_CH");
       m.xupCh = xc ? atoi(xc) : 8;
     }
@@ -1500,8 +1505,8 @@ class Engine final : public EngineBase {
   bool timing_ = false;
   std::vector<hipEvent_t> evPool_;
   size_t evUsed_ = 0;
-  int maxValence_ = 0;  // largest number of incident slots of a local node
   bool zFromX_ = false;
+  bool fusePred_ = true;
   static constexpr bool kZUInterleaved = (D == 2) && MMX_ZU_INTER;  // = kZUInter<D> (admm_kernels.hip)
   double* uPtr() const { return kZUInterleaved ? z_.p + D : u_.p; }
   void clearU() {  // u = 0 (2D: the whole interleaved buffer, z included)

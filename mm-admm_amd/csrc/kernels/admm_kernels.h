@@ -10,9 +10,10 @@ namespace mmx {
 // v[3] = BFGS iterations, v[4] = error flags (inverted element), v[5] = max BFGS iters.
 constexpr int kNumPartials = 6;
 
-// 2D z / u layout: 1 = interleaved per vertex slot (admm_kernels.hip zu_*), 0 = two arrays
+// 2D z / u layout: 1 = interleaved per vertex slot (admm_kernels.hip zu_*), 0 = two arrays (kept:
+// interleaved measured slower, C3 x-update 0.063 -> 0.068 ms, prox 0.325 -> 0.330 ms; profiles/r05/ab/)
 #ifndef MMX_ZU_INTER
-#define MMX_ZU_INTER 1
+#define MMX_ZU_INTER 0
 #endif
 template <int D>
 struct DeviceMesh {
@@ -31,6 +32,11 @@ struct DeviceMesh {
   // xPrev in the first step; src/MeshIntegrator.cpp:121,126) is gathered from these positions
   // instead of read from z, so the step needs no k_gather_z pass; the prox then writes z as usual
   const double* zx;
+  // 2D, one rank, steps after the third: the step's first x-update also does predictX's
+  // extrapolation (k_predict mode 1) for its node -- xBar = 2 x - xPrev, xPrev = x -- into these
+  // (nullptr: k_predict ran)
+  double* predPrev;
+  double* predBar;
   double* gcache;         // per simplex K doubles: the unregularised gradient at the current z
   int* tieList;           // prox blocks left to the exact recomputation (k_prox_fix), tieList[0..*tieCount)
   unsigned* tieCount;
@@ -38,7 +44,6 @@ struct DeviceMesh {
   unsigned* invFlag;       // set by a blockGrad that meets Edet <= 0 (GridView::invFlag)
   int xupCh;              // slots requested at once per node in the sweep (8, 16, 24)
   int xupSweep;           // 3D slot-term x-update as a per-XCD sweep: workgroups per CU (0: one node per lane)
-  int xupPair;            // the sweep with two lanes per node (MMX_XUP_PAIR; every node <= 40 incident slots)
   int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
   const int* nodeOrder;   // x-update processing order (nodes by first incident simplex) or nullptr
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)

@@ -71,10 +71,10 @@ __device__ __forceinline__ int logical_block_any() {
   return x * q + min(x, r) + (int)(blockIdx.x / 8);
 }
 
-// z and u of simplex s, slot layout i = n D + c (the reference's D x order).  2D (kZUInter): the two
-// interleaved per vertex slot, [z_n0 z_n1 u_n0 u_n1] (32 B), so the x-update's two gathers of a slot
-// fall in one cache line; the buffer then holds 2 K doubles per simplex and u = z + D.  3D: separate
-// arrays (the x-update reads the slot terms instead).
+// z and u of simplex s, slot layout i = n D + c (the reference's D x order).  With MMX_ZU_INTER=1
+// (2D, a build option, off: measured slower) the two are interleaved per vertex slot,
+// [z_n0 z_n1 u_n0 u_n1] (32 B), so the x-update's two gathers of a slot fall in one cache line; the
+// buffer then holds 2 K doubles per simplex and u = z + D.  Default: two arrays.
 template <int D>
 constexpr bool kZUInter = (D == 2) && MMX_ZU_INTER;
 template <int D>
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
 // A node's incident slots are taken 8 at a time: their offsets, then all their z and u values
 // are requested before the first is added (branch-free: lanes past the end re-read the last
 // slot, a slot of another rank reads its gathered row), then summed in ascending order.
-template <int D, bool RESID, bool TS, int CH = 8, bool ZX = false>
+template <int D, bool RESID, bool TS, int CH = 8, bool ZX = false, bool PRED = false>
 __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepScalars& sc,
                                              const double* __restrict__ xBar, const double* __restrict__ z,
                                              const double* __restrict__ u, double* __restrict__ x, int idx,
@@ -275,13 +275,34 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
     for (int c = 0; c < D; ++c) acc[c] = 0.0;
     const int b = m.inc_ptr[v], e = m.inc_ptr[v + 1];
     double xb[D], zn[D];
+    if constexpr (PRED) {  // predictX mode 1 for this node (k_predict): xBar = 2 x - xPrev, xPrev = x
+      double xv[D];
 #pragma unroll
-    for (int c = 0; c < D; ++c) xb[c] = xBar[(size_t)v * D + c];
+      for (int c = 0; c < D; ++c) {
+        xv[c] = x[(size_t)v * D + c];
+        xb[c] = 2 * xv[c] - m.predPrev[(size_t)v * D + c];
+      }
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        m.predBar[(size_t)v * D + c] = xb[c];
+        m.predPrev[(size_t)v * D + c] = xv[c];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < D; ++c) xb[c] = xBar[(size_t)v * D + c];
+    }
     // ZX: a step's first x-update without z (DeviceMesh::zx): every local slot of node v holds z = zx_v
+    // (with PRED, zx is this step's xBar: the node's own xb)
     constexpr bool zv0 = ZX && !TS;
-    if constexpr (zv0)
+    if constexpr (zv0) {
+      if constexpr (PRED) {
 #pragma unroll
-      for (int c = 0; c < D; ++c) zn[c] = m.zx[(size_t)v * D + c];
+        for (int c = 0; c < D; ++c) zn[c] = xb[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < D; ++c) zn[c] = m.zx[(size_t)v * D + c];
+      }
+    }
     const double inv = m.invdiag[v];
     for (int t0 = b; t0 < e; t0 += CH) {
       int off[CH];
@@ -358,7 +379,7 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
 #ifndef MMX_XU_CH2D
 #define MMX_XU_CH2D 6  // 2D: incident slots requested at once per node (C3: 8 0.066 ms, 6 0.0645, 4 0.079)
 #endif
-template <int D, bool RESID, bool TS, bool ZX = false>
+template <int D, bool RESID, bool TS, bool ZX = false, bool PRED = false>
 __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
                                                      const double* __restrict__ xBar,
                                                      const double* __restrict__ z,
@@ -367,7 +388,7 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
   const int lb = logical_block(xcd);
   const int idx = lb * kBlock + threadIdx.x;
   double pv[3] = {0, 0, 0};
-  if (idx < m.nP) xupdate_node<D, RESID, TS, (D == 2 ? MMX_XU_CH2D : 8), ZX>(m, sc, xBar, z, u, x, idx, pv);
+  if (idx < m.nP) xupdate_node<D, RESID, TS, (D == 2 ? MMX_XU_CH2D : 8), ZX, PRED>(m, sc, xBar, z, u, x, idx, pv);
   if constexpr (RESID) block_partials<3>(pv, partials, lb);
 }
 // The slot-term x-update (no residual) as a sweep: XCD c (= blockIdx % 8) takes the node-order
@@ -385,62 +406,6 @@ __global__ void __launch_bounds__(kBlock) k_xupdate_sweep(DeviceMesh<D> m, StepS
   double pv[3];
   for (int idx = lo + w * kBlock + (int)threadIdx.x; idx < hi; idx += per * kBlock)
     xupdate_node<D, false, TS, CH>(m, sc, xBar, z, u, x, idx, pv);
-}
-
-// The slot-term sweep with two lanes per node (MMX_XUP_PAIR, 3D): lanes 2k and 2k + 1 request the
-// first and the second half of the node's incident slot terms, so twice as many of a node's requests
-// are in flight at once; the even lane then adds all of them in ascending order, the odd lane's
-// through a lane swap -- the same sum, bit for bit.  Nodes with more than 2 kXuPairHalf slots are
-// not handed to this kernel (the host checks the largest valence).
-constexpr int kXuPairHalf = 20;
-template <int D>
-__global__ void __launch_bounds__(kBlock) k_xupdate_sweep_pair(DeviceMesh<D> m, StepScalars sc,
-                                                                const double* __restrict__ xBar, double* __restrict__ x,
-                                                                int n8) {
-  constexpr int HN = kBlock / 2;  // nodes per workgroup round
-  const int c = (int)(blockIdx.x % 8), w = (int)(blockIdx.x / 8), per = (int)(gridDim.x / 8);
-  const int lo = c * n8, hi = min(lo + n8, m.nP);
-  const int h = (int)threadIdx.x & 1;
-  for (int base = lo + w * HN; base < hi; base += per * HN) {
-    const int idx = base + ((int)threadIdx.x >> 1);
-    const bool act = idx < hi;
-    const int v = act ? (m.nodeOrder ? m.nodeOrder[idx] : idx) : 0;
-    const int b = act ? m.inc_ptr[v] : 0, e = act ? m.inc_ptr[v + 1] : 0;
-    const int half = (e - b + 1) >> 1;
-    const int mb = b + (h ? half : 0), cnt = h ? (e - b - half) : half;  // my slots [mb, mb + cnt)
-    int off[kXuPairHalf];
-#pragma unroll
-    for (int j = 0; j < kXuPairHalf; ++j) off[j] = (j < cnt) ? m.inc_off[mb + j] : 0;
-    double tv[kXuPairHalf][D];
-#pragma unroll
-    for (int j = 0; j < kXuPairHalf; ++j) {
-      const double* pt = (off[j] >= 0) ? m.tslot + off[j] : m.remote + (size_t)(-1 - off[j]) * D;
-#pragma unroll
-      for (int q = 0; q < D; ++q) tv[j][q] = (j < cnt) ? pt[q] : 0.0;
-    }
-    double acc[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) acc[q] = 0.0;
-#pragma unroll
-    for (int j = 0; j < kXuPairHalf; ++j)
-      if (j < cnt)
-#pragma unroll
-        for (int q = 0; q < D; ++q) acc[q] += tv[j][q];
-    const int cnt1 = e - b - half;  // the odd lane's count, known to both lanes
-#pragma unroll
-    for (int j = 0; j < kXuPairHalf; ++j) {
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        const double o = __shfl_xor(tv[j][q], 1, 64);
-        if (j < cnt1) acc[q] += o;
-      }
-    }
-    if (act && h == 0) {
-      const double inv = m.invdiag[v];
-#pragma unroll
-      for (int q = 0; q < D; ++q) x[(size_t)v * D + q] = ((sc.tau * xBar[(size_t)v * D + q]) + sc.dtsq * acc[q]) * inv;
-    }
-  }
 }
 
 // k x k inverse: unblocked partial-pivot LU + substitution (mirrors the oracle's restatement
@@ -2272,17 +2237,17 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   if (m.nP == 0) return;
   const bool ts = useTslot && m.tslot;
   if (D == 2 && m.zx && !resid && !ts) {  // a step's first x-update: z from DeviceMesh::zx
-    hipLaunchKernelGGL((k_xupdate<D, false, false, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u, x,
-                       partials, xcd_map());
+    if (m.predBar)  // ... and predictX's extrapolation fused in
+      hipLaunchKernelGGL((k_xupdate<D, false, false, true, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z,
+                         u, x, partials, xcd_map());
+    else
+      hipLaunchKernelGGL((k_xupdate<D, false, false, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u,
+                         x, partials, xcd_map());
     return;
   }
   if (!resid && m.xupSweep > 0) {  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU
     const int n8 = ((m.nP + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
     const dim3 g(256 * m.xupSweep);
-    if (ts && m.xupPair) {
-      hipLaunchKernelGGL((k_xupdate_sweep_pair<D>), g, dim3(kBlock), 0, st, m, sc, xBar, x, n8);
-      return;
-    }
     if (ts && m.xupCh >= 24)
       hipLaunchKernelGGL((k_xupdate_sweep<D, true, 24>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
     else if (ts && m.xupCh >= 16)

@@ -375,24 +375,6 @@ def test_xupdate_order_and_sweep_bitwise(order, sweep, monkeypatch):
     Q.close()
 
 
-def test_xupdate_pair_lanes_bitwise(monkeypatch):
-    """The 3D sweep with two lanes per node (MMX_XUP_PAIR=1: each lane requests half of a node's
-    slot terms, the even lane adds all of them in ascending order): bit-identical to the default."""
-    m = mx.MeshData.rect(3, 24)
-    M = mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(3, 6), rho=2000.0, tau=0.5)
-    W = mx.Engine(M, 0.025)
-    for _ in range(2):
-        W.step(10, -1.0)
-    monkeypatch.setenv("MMX_XUP_PAIR", "1")
-    Q = mx.Engine(M, 0.025)
-    for _ in range(2):
-        Q.step(10, -1.0)
-    for f in ("x", "z", "u"):
-        np.testing.assert_array_equal(Q.get(f), W.get(f), err_msg=f)
-    W.close()
-    Q.close()
-
-
 @pytest.mark.parametrize("order,sweep", [(1, 0), (0, 1), (1, 1), (1, 2)])
 def test_xupdate_order_and_sweep_bitwise_2d(order, sweep, monkeypatch):
     """The 2D x-update (z and u gathered) in the same forms (opt-in in 2D): bit-identical."""
