@@ -1183,7 +1183,9 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 // returns false, having written nothing, when a power met a near-midpoint (the block is queued).
 // EXACT = true (k_prox_wave_fix): the exact recomputation of a queued block, entry gradient
 // included (the fast pass may have left the cache at a point it then abandoned).
-template <int D, bool COMP, bool EXACT, bool ISO = false>
+// DRAIN = false (the persistent loop): the block ends without waiting for its stores, so they drain
+// while the wave's next block issues its loads
+template <int D, bool COMP, bool EXACT, bool ISO = false, bool DRAIN = true>
 __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double tol, const double* __restrict__ x,
                                                 double* __restrict__ zg, double* __restrict__ ug, const double* Bin,
                                                 double* Bout, double* __restrict__ partials, int useCache, int lb,
@@ -1288,7 +1290,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     write_tslot<D>(m, s, z, un);
   }
   block_partials<6, 64>(pv, partials, lb);
-  if constexpr (!EXACT) {
+  if constexpr (!EXACT && DRAIN) {
     __builtin_amdgcn_s_waitcnt(0);
     WPROF(6, pv[0]);
   }
@@ -1306,12 +1308,13 @@ __global__ void __launch_bounds__(64, D == 2 ? MMX_WAVE_OCC2 : MMX_WAVE_OCC) k_p
     // persistent waves (experiment): workgroup w on XCD c = w % 8 walks the XCD's contiguous range of
     // blocks with stride gridDim / 8, so a wave starts its next block without ending (no drain of its
     // stores before the next block's loads are issued by a new wave)
-    const int nb = (m.nF + 63) / 64, g8 = (int)gridDim.x / 8, c = (int)(blockIdx.x % 8), j = (int)(blockIdx.x / 8);
+    // (the grid is a multiple of 8: launch_prox rounds it up)
+    const int nb = (m.nF + 63) / 64, g8 = max(1, (int)gridDim.x / 8), c = (int)(blockIdx.x % 8), j = (int)(blockIdx.x / 8);
     const int q = nb / 8, r = nb % 8, lo = c * q + min(c, r), hi = lo + q + (c < r ? 1 : 0);
     for (int lb = lo + j; lb < hi; lb += g8) {
       // (the next block's held-row DMA into ldsHeld is issued after this block's last reads of it
       // have returned: the final rows' stores consume them)
-      prox_wave_block<D, COMP, false, ISO>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
+      prox_wave_block<D, COMP, false, ISO, false>(m, tol, x, zg, ug, Bin, Bout, partials, useCache, lb, ldsHeld);
     }
     return;
   }
@@ -2439,7 +2442,7 @@ void launch_prox(const DeviceMesh<D>& m, bool first, bool useCache, double tol, 
     }
 #define MMX_WAVE3(C, I)                                                                                            \
   do {                                                                                                           \
-    hipLaunchKernelGGL((k_prox_wave<D, C, I>), dim3(MMX_WAVE_PERSIST ? std::min(*nblocks, MMX_WAVE_PERSIST) : *nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc); \
+    hipLaunchKernelGGL((k_prox_wave<D, C, I>), dim3(MMX_WAVE_PERSIST ? (std::min(*nblocks, MMX_WAVE_PERSIST) + 7) / 8 * 8 : *nblocks), dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials, uc); \
     hipLaunchKernelGGL((k_prox_wave_fix<D, C, I>), fg, dim3(64), 0, st, m, tol, x, z, u, Bin, Bout, partials);          \
   } while (0)
     if (m.compMesh) {
