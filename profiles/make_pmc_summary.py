@@ -8,12 +8,12 @@ widths the same way (8 B per lane, 24-B records, random records: also half, 128-
 `hbm_bytes_per_launch` applies the x2 to every kernel's fetch side; `hbm_bytes_raw_per_launch` is
 the uncorrected figure.
 
-  python profiles/make_pmc_summary.py profiles/r04/pmc/fetch_counter_collection.csv.gz \
-         profiles/r04/pmc/write_counter_collection.csv.gz profiles/r04/pmc/f64_counter_collection.csv.gz \
-         bfgs_heavy=profiles/r04/pmc/f64b_counter_collection.csv.gz
+  python profiles/make_pmc_summary.py profiles/r05/pmc/fetch_counter_collection.csv.gz \
+         profiles/r05/pmc/write_counter_collection.csv.gz profiles/r05/pmc/f64_counter_collection.csv.gz \
+         bfgs_heavy=profiles/r05/pmc/f64b_counter_collection.csv.gz
 
-(round 4: each pass is its own rocprofv3 run of `bench.py --steps 10 --warmup 2 --no-cpu-baseline
---no-bfgs`, dev/final_pmc.sh; the f64 pass of the BFGS-heavy section alone is profiles/r04/bfgs_only.py;
+(round 5, as round 4: each pass is its own rocprofv3 run of `bench.py --steps 10 --warmup 2 --no-cpu-baseline
+--no-bfgs`, dev/r5_final_pmc.sh; the f64 pass of the BFGS-heavy section alone is profiles/r04/bfgs_only.py;
 the summary holds only the kernels those runs launched)
 
 The optional third pass (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, wave instructions) gives

@@ -6,7 +6,9 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_predict" in r["Kernel_Name"]]
+# a step starts at k_predict or, when the extrapolation is fused (2D, round 5), at the first x-update
+# (the z-from-positions instance, k_xupdate<2, false, false, true, ...>)
+idx = [i for i, r in enumerate(rows) if "k_predict" in r["Kernel_Name"] or "k_xupdate<2, false, false, true" in r["Kernel_Name"]]
 a, b = idx[k], idx[k + 1]
 prev = int(rows[a - 1]["End_Timestamp"])
 busy = gaps = 0
