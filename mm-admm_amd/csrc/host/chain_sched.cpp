@@ -77,8 +77,12 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   // the subtractions is unchanged); every row of a chain takes the chain's segment count ns.
   // Narrower rows (2D) are computed two per position (G = 2): the chain's next row takes the
   // first one's value straight from the register (MMX_CHAIN_PAIR=0: one row per position).
-  S.E = emax <= 8 ? 8 : emax <= 16 ? 16 : 32;
-  S.seg = emax > 32;
+  {
+    const char* we = getenv("MMX_CHAIN_E48");
+    const bool wide = emax > 32 && emax <= kChainWideE && !(we && atoi(we) == 0);
+    S.E = emax <= 8 ? 8 : emax <= 16 ? 16 : emax <= 32 ? 32 : wide ? kChainWideE : 32;
+    S.seg = emax > 32 && !wide;
+  }
   if (emax > kChainSegMax * 32) {
     S.why = "a row has more than " + std::to_string(kChainSegMax * 32) + " entries in the triangle";
     return S;
@@ -226,8 +230,9 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
     S.estIters = est;
   }
   // lane arrays, slots, ring distances (a ring slot of a lane is written again R / G positions
-  // after it is written)
+  // after it is written); a value further back than the ring holds is imported
   int maxDist = 1;
+  const int ringCap = E > 32 ? kChainRingWide : kChainRingMax;
   for (int b = 0; b < S.nbands; ++b) {
     const int c0 = b * L, nl = std::min(L, C - c0);
     for (int l = 0; l < nl; ++l) {
@@ -248,7 +253,7 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
             const int j = jaf[k], cj = chainOf[j];
             if (cj < c0 || cj > c) continue;
             const int d = (p + skl) - (posOf[j] + S.laneSkew[(size_t)b * L + (cj - c0)]);
-            if (d >= 1 && d * G <= kChainRingMax) maxDist = std::max(maxDist, d * G);
+            if (d >= 1 && d * G <= ringCap) maxDist = std::max(maxDist, d * G);
           }
         }
     }
@@ -411,6 +416,9 @@ std::string validate_chain_schedule(const ChainSchedule& S, int n, const std::ve
   const bool fwd = S.fwd;
   if (G != 1 && G != 2) return "bad rows per position";
   if (G == 2 && S.seg) return "pairs of segmented rows";
+  if (E != 8 && E != 16 && E != 32 && E != kChainWideE) return "no kernel for this stage width";
+  if (R < 1 || (R & (R - 1)) || R > (E > 32 ? kChainRingWide : kChainRingMax)) return "ring larger than the kernel's";
+  if (E > 32 && (S.seg || G != 1 || 1 + L * (R + 1) + S.RI >= 65536)) return "wide stage codes do not fit 16 bits";
   // where every row is computed: band, lane, position of its final value, ring sequence number,
   // part (pair half), segments
   std::vector<int> bandOf(n, -1), laneOf(n, -1), posOf(n, -1), ringOf(n, -1), partOf(n, 0), iterOf(n, -1),

@@ -34,6 +34,11 @@ constexpr int kChainImpMax = 2048;   // LDS import slots (16-byte granules) -- c
 constexpr int kChainPad = -2147483647 - 1;  // empty entry slot (schedule building only)
 constexpr int kChainFwd = -2147483647;      // entry whose value is the pair's first row (building only)
 constexpr int kChainSegMax = 4;      // segments of E = 32 entries a row may take (rows up to 128 entries)
+// rows of 33..48 entries (the 3D backward triangle: up to 44) take one position of a 48-entry stage
+// with 16-bit codes instead of two 32-entry segments; its LDS budget leaves a ring of 8 rows per lane
+// (chain_sweep.hip kRingWide; values farther back are imported).  MMX_CHAIN_E48=0: segments.
+constexpr int kChainWideE = 48;
+constexpr int kChainRingWide = 8;
 
 struct ChainSchedule {
   bool ok = false;

@@ -192,6 +192,7 @@ struct SparseMatrix {
     long long nent = 0, nslot = 0;
     DevBuf<int> bandSlot, bandT, bandImp, bandNImp, bandE, bandOrder, laneStart, laneLen, laneSkew, laneNs, code, src, dsrc,
         impRow, impSlot, impWait, impNeed;
+    DevBuf<uint16_t> code16;  // the codes of a 48-entry schedule (16-bit)
     DevBuf<double> val, dval;
     ChainArgs args{};
   };
@@ -397,6 +398,10 @@ struct SparseMatrix {
     symbolic = true;
   }
 
+  static int chain_trim() {
+    const char* e = getenv("MMX_CHAIN_TRIM");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }
   void upload_chain(const ChainSchedule& S, ChainDir& c) {
     auto up = [&](DevBuf<int>& d, const std::vector<int>& h) {
       if (h.empty()) {
@@ -414,7 +419,17 @@ struct SparseMatrix {
     up(c.laneLen, S.laneLen);
     up(c.laneSkew, S.laneSkew);
     up(c.laneNs, S.laneNs);
-    up(c.code, S.code);
+    const void* codePtr;
+    if (S.E > 32) {  // 16-bit codes (validate_chain_schedule: every index fits)
+      if (S.seg || S.G != 1 || S.R > kChainRingWide) throw Error(MMADMM_ERR_INVALID, "wide chain stage layout");
+      std::vector<uint16_t> c16(S.code.begin(), S.code.end());
+      c.code16.upload(c16.data(), std::max<size_t>(c16.size(), 1), st);
+      MMX_HIP(hipStreamSynchronize(st));
+      codePtr = c.code16.p;
+    } else {
+      up(c.code, S.code);
+      codePtr = c.code.p;
+    }
     up(c.src, S.src);
     up(c.dsrc, S.dsrc);
     up(c.impRow, S.impRow);
@@ -434,9 +449,10 @@ struct SparseMatrix {
       MMX_HIP(hipMemsetAsync(d_cprof.p, 0, 1024 * sizeof(unsigned long long), st));
     }
     c.args = ChainArgs{c.bandSlot.p, c.bandT.p, c.bandImp.p, c.bandNImp.p, c.laneStart.p, c.laneLen.p, c.laneSkew.p,
-                       c.laneNs.p, c.bandE.p, c.val.p, c.code.p, c.dval.p, c.impRow.p, c.impSlot.p, c.impWait.p, c.impNeed.p,
+                       c.laneNs.p, c.bandE.p, c.val.p, codePtr, c.dval.p, c.impRow.p, c.impSlot.p, c.impWait.p, c.impNeed.p,
                        c.bandOrder.p, S.nbands, S.R, S.RI, S.seg ? 1 : 0, S.G,
-                       d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr, (pe && atoi(pe) >= 2) ? 1 : 0};
+                       d_cprof.p ? d_cprof.p + (S.fwd ? 0 : 512) : nullptr, (pe && atoi(pe) >= 2) ? 1 : 0,
+                       chain_trim()};
   }
 
   void upload_factor(const FactorSchedule& F, const std::vector<int>& dg) {

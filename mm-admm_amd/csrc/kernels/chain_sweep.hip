@@ -15,11 +15,14 @@
 // Every row is x_i = (b_i - sum_k a_k x_jk) [/ d_i] with the terms subtracted in ascending column
 // order, exactly as the level-scheduled k_sweep and the reference.  SEG: a lane's rows take ns
 // positions each (32 entries per position, the partial sum carried in a register), for triangles
-// with rows wider than 32 entries (3D).  G = 2: a position computes two consecutive rows of the
+// with rows wider than 48 entries; rows of 33..48 entries (the 3D backward triangle) take one
+// position of a 48-entry stage whose codes are 16-bit (LDS budget).  G = 2: a position computes two consecutive rows of the
 // chain (rows of at most 16 entries, 2D), the second taking the first's value from the register,
 // which halves the iterations on the critical path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "sparse_kernels.h"
 
@@ -30,6 +33,7 @@ namespace {
 
 constexpr int kPad = -2147483647 - 1;
 constexpr int kRingMax = 32;    // = kChainRingMax (host/chain_sched.h)
+constexpr int kRingWide = 8;    // = kChainRingWide: the ring of the 48-entry stages
 constexpr int kImpMax = 2048;   // = kChainImpMax
 #ifndef MMX_IMP_Q
 #define MMX_IMP_Q 4
@@ -85,7 +89,20 @@ struct Aux {
   static constexpr int need = 384 * G;
   static constexpr int words = need + 64;
 };
-constexpr int kDepCells = 1 + 64 * (kRingMax + 1) + kImpMax + 1;  // + the pairs' forwarded cell
+// LDS cells of a lane ring of RM rows: [0] = +0.0, the rings, the import slots, the pairs' forwarded cell
+template <int RM>
+struct DepCells {
+  static constexpr int n = 1 + 64 * (RM + 1) + kImpMax + 1;
+};
+// entry codes: 32-bit, 16-bit in the 48-entry stages
+template <int EE>
+struct CodeOf {
+  typedef int T;
+};
+template <>
+struct CodeOf<48> {
+  typedef uint16_t T;
+};
 
 // abort protocol: a bounded wait that gives up sets err; everyone polls err now and then
 __device__ __forceinline__ bool aborted(unsigned* err) {
@@ -122,13 +139,12 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
   constexpr int DL = Geo<EE>::DL;
   constexpr int NAUX = AuxN<FWD, PRO, G>::n;
   constexpr int kAuxWords = Aux<G>::words;
-  constexpr int NI = EE / 2 + EE / 4 + NAUX;          // DMA instructions per stage
-  constexpr int LAG0 = 63 / NI < 1 ? 1 : 63 / NI;
-  constexpr int LAG = LAG0 < DL / 2 ? LAG0 : DL / 2;  // own stages in flight per loader
+  typedef typename CodeOf<EE>::T CodeT;
+  constexpr int RM = EE > 32 ? kRingWide : kRingMax;
   __shared__ double s_val[DL * EE * 64];
-  __shared__ int s_code[DL * EE * 64];
+  __shared__ CodeT s_code[DL * EE * 64];
   __shared__ uint32_t s_aux[DL * kAuxWords];
-  __shared__ double s_dep[kDepCells];  // [0] = +0.0, lane rings, import slots
+  __shared__ double s_dep[DepCells<RM>::n];  // [0] = +0.0, lane rings, import slots
   __shared__ int s_tag[DL];
   __shared__ int s_prog, s_band, s_impDone;
 
@@ -183,7 +199,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
         const uint32_t* sa0 = s_aux + st * kAuxWords;
         f.need = (int)sa0[Aux<G>::need + lane];  // the same in every lane; made scalar where it is used
         const double* sv = s_val + st * EE * 64;
-        const int* scd = s_code + st * EE * 64;
+        const CodeT* scd = s_code + st * EE * 64;
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -353,6 +369,16 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       }
     } else if (wave <= 2) {
       // ---------------- loaders (stages t = w, w+2, ...) ----------------
+      // A band whose rows use at most half the stage's entry slots (bandE; e.g. the 2D grid-line
+      // bands: <= 5 of 16) has only those moved: fewer DMA instructions per stage, so more stages
+      // fit the 6-bit vmcnt window in flight.  The compute wave reads entries < bandE only.
+      auto loader = [&](auto ebc) {
+      constexpr int EB = decltype(ebc)::value;  // entry slots moved per row
+      constexpr int NVb = EB / 2, NCb = EB * (int)sizeof(CodeT) / 16;
+      constexpr int NIb = G * (NVb + NCb) + NAUX;
+      constexpr int LAGb0 = 63 / NIb < 1 ? 1 : 63 / NIb;
+      constexpr int LAGb = LAGb0 < DL / 2 ? LAGb0 : DL / 2;
+      static_assert(EB <= E && EB % 4 == 0 && (EB * (int)sizeof(CodeT)) % 16 == 0, "stage entry slots");
       const int w = wave - 1;
       int nextPub = w;
       bool ok = true;
@@ -374,11 +400,17 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
         }
         const size_t slot = (size_t)(sb + t);
         const double* gv = ca.val + slot * EE * 64;
+        const char* gc = (const char*)ca.code + slot * EE * 64 * sizeof(CodeT);
 #pragma unroll
-        for (int i = 0; i < EE / 2; ++i) dma16(gv + i * 128 + lane * 2, s_val + st * EE * 64 + i * 128);
-        const int* gc = ca.code + slot * EE * 64;
+        for (int g = 0; g < G; ++g) {
 #pragma unroll
-        for (int i = 0; i < EE / 4; ++i) dma16(gc + i * 256 + lane * 4, s_code + st * EE * 64 + i * 256);
+          for (int i = 0; i < NVb; ++i)
+            dma16(gv + (g * E / 2 + i) * 128 + lane * 2, s_val + st * EE * 64 + (g * E / 2 + i) * 128);
+          constexpr int gcs = E * (int)sizeof(CodeT) / 16;  // code instructions per row block
+#pragma unroll
+          for (int i = 0; i < NCb; ++i)
+            dma16(gc + (g * gcs + i) * 1024 + lane * 16, (char*)(s_code + st * EE * 64) + (g * gcs + i) * 1024);
+        }
         const int p = t - skew;
         uint32_t* sa0 = s_aux + st * kAuxWords;
 #pragma unroll
@@ -407,11 +439,11 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           }
         }
         dma4(ca.impNeed + slot, sa0 + Aux<G>::need);  // the same word in every lane
-        if ((t - nextPub) / 2 + 1 > LAG) {
+        if ((t - nextPub) / 2 + 1 > LAGb) {
           const unsigned long long l0 = ca.prof ? clk() : 0;
-          wait_vm<NI * LAG>();
+          wait_vm<NIb * LAGb>();
           if (ca.prof) cin += clk() - l0;
-          for (; nextPub <= t - 2 * LAG; nextPub += 2)
+          for (; nextPub <= t - 2 * LAGb; nextPub += 2)
             if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
         }
       }
@@ -424,6 +456,12 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
         prof_add(ca.prof, 5, csl);
         prof_add(ca.prof, 6, cin);
       }
+      };
+      constexpr int EH = (E / 2) % 4 == 0 && ((E / 2) * (int)sizeof(CodeT)) % 16 == 0 ? E / 2 : E;
+      if (EH < E && ca.trim && ca.bandE[b] <= EH)
+        loader(std::integral_constant<int, EH>());
+      else
+        loader(std::integral_constant<int, E>());
     } else {
       // ---------------- importer ----------------
       // lane l delivers imports l, l + 64, l + 128, ... in order, polling its next kImpQ at once:
@@ -517,6 +555,8 @@ void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const dou
       MMX_CHAIN(F, P, 8, false, 1);      \
     else if (E == 16)                    \
       MMX_CHAIN(F, P, 16, false, 1);     \
+    else if (E == 48)                    \
+      MMX_CHAIN(F, P, 48, false, 1);     \
     else                                 \
       MMX_CHAIN(F, P, 32, false, 1);     \
   } while (0)

@@ -82,7 +82,7 @@ struct ChainArgs {
   const int* laneNs;   // per band * 64 + lane: segments per row (seg schedules; rows wider than 32 entries)
   const int* bandE;    // per band: entry slots in use (multiple of 4)
   const double* val;   // [slot][E][64] entry values (filled from the factor by launch_chain_fill)
-  const int* code;     // [slot][E][64] LDS index of the entry's value (0: the zero cell)
+  const void* code;    // [slot][E][64] LDS index of the entry's value (0: the zero cell): int32, uint16 at E = 48
   const double* dval;  // [slot][64] diagonals (backward)
   const int* impRow;
   const int* impSlot;  // per import: LDS import slot
@@ -94,6 +94,7 @@ struct ChainArgs {
   int G;               // rows per position (2: pairs of consecutive chain rows)
   unsigned long long* prof;  // optional cycle counters (MMX_CHAIN_PROF), see chain_sweep.hip
   int profIter;              // MMX_CHAIN_PROF=2: also time the waits inside iterations (perturbs them)
+  int trim;                  // loaders move only bandE entry slots of bands using at most half (MMX_CHAIN_TRIM=0: all)
 };
 void launch_chain_sweep(bool fwd, int pro, int E, const ChainArgs& ca, const double* src, double* p, const double* res,
                         const double* avbar, const CgsScalars* sc, const uint64_t* gin, uint64_t* gout, double* out,

@@ -225,15 +225,19 @@ def _sweep_run(la, ia, ja, a, b, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mesh", [("rect", 2, 45), ("hexdisc", 40), ("circle", "CircleEx24"), ("rect", 2, 300),
-                                  ("rect", 3, 12), ("rect", 3, 30)])
+                                  ("rect", 3, 12), ("rect", 3, 30), ("rect", 3, 63)])
 @pytest.mark.parametrize("pair", ["1", "0"])
 def test_chain_sweeps_equal_level_sweeps(la, mesh, pair, monkeypatch):
     """The chain/band-scheduled sweeps (chain_sweep.hip) and the level-scheduled ones compute every
     row with the same operations in the same order: ILU solves and CG-STAB iterates are identical.
-    3D: the upper rows (up to 44 entries) run as two 32-entry segments (k_chain_sweep<..., SEG>);
-    2D: two chain rows per iteration (pair 1, the default) or one."""
-    if mesh[1] == 3 and pair == "0":
-        pytest.skip("3D schedules have one row per position")
+    3D: the upper rows (up to 44 entries) take one position of a 48-entry stage (k_chain_sweep<...,
+    48, ...>, pair 1 = the default) or two 32-entry segments (k_chain_sweep<..., SEG>, MMX_CHAIN_E48=0);
+    rect 3 63 is the C4 bench's pattern (1,536,573 rows). 2D: two chain rows per iteration (pair 1,
+    the default) or one."""
+    if mesh[1] == 3:
+        if mesh[2] == 63 and pair == "0":
+            pytest.skip("the segmented layout is covered on the smaller cubes")
+        monkeypatch.setenv("MMX_CHAIN_E48", pair)
     monkeypatch.setenv("MMX_CHAIN_PAIR", pair)
     import mmadmm_amd as mx
     from conftest import circle_mesh

@@ -111,15 +111,28 @@ def test_chain_schedule_is_valid(mesh, level, pair, monkeypatch):
         info = _schedule_info(ia, ja, level, fwd)
         assert info["ok"] == 1, info
         if dim == 3:
-            # 3D: the upper rows (up to 44 entries) take two 32-entry segments, and each band's lanes
-            # wait for imports from several planes; the modelled path stays within a few DAG depths
-            assert info["E"] == 32 and info["estIters"] <= 4 * info["levels"] + 64, info
+            # 3D: the lower rows fit 32-entry stages, the upper rows (up to 44 entries) 48-entry ones
+            # (one position per row); each band's lanes wait for imports from several planes, and the
+            # modelled path stays within two DAG depths
+            assert info["E"] == (32 if fwd else 48) and info["estIters"] <= 2 * info["levels"] + 64, info
         elif pair == "1":
             # two chain rows per iteration: the critical path is about half the DAG's depth
             assert info["estIters"] <= 0.7 * info["levels"] + 64, info
         else:
             # the critical path stays close to the dependency DAG's depth
             assert info["estIters"] <= 1.3 * info["levels"] + 64, info
+
+
+@pytest.mark.parametrize("n", [6, 14])
+def test_segmented_schedule_is_valid(n, monkeypatch):
+    """MMX_CHAIN_E48=0: the 3D upper rows take two 32-entry segments at consecutive positions (the
+    round-3 layout) -- still a valid schedule, only a longer one."""
+    m = oracle_py.Mesh.rect(3, n)
+    ia, ja = L.mesh_pattern(3, m.nP, m.F)
+    monkeypatch.setenv("MMX_CHAIN_E48", "0")
+    info = _schedule_info(ia, ja, 0, False)
+    assert info["ok"] == 1 and info["E"] == 32, info
+    assert info["estIters"] <= 4 * info["levels"] + 64, info
 
 
 @pytest.mark.parametrize("mesh", [("rect", 2, 20), ("rect", 2, 57), ("hexdisc", 30), ("circle", "CircleEx24"),
