@@ -209,6 +209,8 @@ struct SparseMatrix {
     FactorArgs args{};
   } chfac;
   bool useChainFactor = false;
+  bool facWave = false;     // k_ilu_factor_wave (one wavefront per row) over d_permw
+  DevBuf<int> d_permw;
   DevBuf<unsigned long long> d_cprof;  // MMX_CHAIN_PROF: 2 x 512 counters (forward, backward)
   // numeric factor cache: the ILU of unchanged values is the same, so a solve re-factors only
   // after set_values / sfac (the reference re-factors in every solve, MatrixIter.cpp:684)
@@ -380,6 +382,7 @@ struct SparseMatrix {
       }
     }
     useChainFactor = false;
+    facWave = false;
     {
       // default where the rows fit its layout (2D): bit-identical to the level schedule and
       // 12.3 ms against 25.0 ms at n = 2 M (profiles/r03/chain_factor/);
@@ -387,9 +390,40 @@ struct SparseMatrix {
       const char* fm = getenv("MMX_FACTOR");
       if (useChain && !(fm && (std::strcmp(fm, "level") == 0 || std::strcmp(fm, "global") == 0))) {
         const FactorSchedule FS = build_factor_schedule(n, iaf, jaf, dg);
-        if (FS.ok) {
+        if (FS.ok && !(fm && std::strcmp(fm, "wave") == 0)) {
           upload_factor(FS, dg);
           useChainFactor = true;
+        }
+      }
+      // otherwise one wavefront per row (3D rows: 45 ms -> see DESIGN.md §7) where the rows fit it;
+      // MMX_FACTOR=level keeps the level-scheduled lane-per-row factor
+      if (!useChainFactor && facLds && !(fm && (std::strcmp(fm, "level") == 0 || std::strcmp(fm, "global") == 0))) {
+        bool fits = true;
+        std::vector<int> stamp(jaf.size(), -1);
+        for (int i = 0; i < n && fits; ++i) {
+          if (dg[i] - iaf[i] > kFacWaveNL || iaf[i + 1] - dg[i] - 1 > 64) fits = false;
+          // the row image is scattered by all lanes at once: no two entries of A onto one factor slot
+          for (int k = ia[i]; k < ia[i + 1] && fits; ++k) {
+            if (stamp[amap[k]] == i) fits = false;
+            stamp[amap[k]] = i;
+          }
+        }
+        if (fits) {  // every row once, in forward level order
+          std::vector<int> lv(n, 0), cnt;
+          int nl = 0;
+          for (int i = 0; i < n; ++i) {
+            int l = 0;
+            for (int k = iaf[i]; k < dg[i]; ++k) l = std::max(l, lv[jaf[k]] + 1);
+            lv[i] = l;
+            nl = std::max(nl, l + 1);
+          }
+          cnt.assign(nl + 1, 0);
+          for (int i = 0; i < n; ++i) cnt[lv[i] + 1]++;
+          for (int l = 0; l < nl; ++l) cnt[l + 1] += cnt[l];
+          std::vector<int> pw(n);
+          for (int i = 0; i < n; ++i) pw[cnt[lv[i]]++] = i;
+          d_permw.upload(pw.data(), pw.size(), st);
+          facWave = true;
         }
       }
     }
@@ -538,6 +572,9 @@ struct SparseMatrix {
       launch_scatter_a((long long)nnz, d_amap.p, d_a.p, chfac.af0.p, st);
       launch_chain_fill((long long)chfac.vsrc.n, chfac.vsrc.p, chfac.af0.p, chfac.val.p, 0.0, st);
       launch_chain_factor(chfac.args, d_af.p, chfac.gU.p, fepoch, tickets(), errw(), st);
+    } else if (facWave) {
+      launch_ilu_factor_wave(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_dg.p, d_piv.p, d_jaf.p, d_toff.p, d_tgt.p, d_permw.p, n,
+                             d_af.p, d_flags.p, fepoch, errw(), st);
     } else if (facLds)
       launch_ilu_factor_lds(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_toff.p, d_tgt.p, d_permf.p, nchf,
                             d_af.p, d_flags.p, fepoch, tickets(), errw(), st);
@@ -1033,7 +1070,7 @@ int mmx_matrix_stats_get(mmx_matrix m, mmx_sparse_stats* out) {
     if (out) {
       *out = M.stats;
       out->sweep_mode = M.useChain ? 1 : 0;
-      out->factor_mode = M.useChainFactor ? 1 : 0;
+      out->factor_mode = M.useChainFactor ? 1 : M.facWave ? 2 : 0;
       out->sweep_e = M.useChain ? M.chf.E : 0;
     }
   });

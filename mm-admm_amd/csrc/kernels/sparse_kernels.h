@@ -61,6 +61,14 @@ void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, cons
                            const int2* piv, const int* toff, const signed char* tgt, const int* perm, int nchunks,
                            double* af, unsigned* flags, unsigned epoch, unsigned* ticket, unsigned* err, hipStream_t st);
 
+// One wavefront per row (k_ilu_factor_wave): perm = every row once in forward level order (no
+// padding); rows of at most kFacW entries, kFacWaveNL lower entries and 64 upper entries per pivot
+// row.  Bit-identical to the other factors.
+constexpr int kFacWaveNL = 32;
+void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, const int* iaf, const int* dg,
+                            const int2* piv, const int* jaf, const int* toff, const signed char* tgt, const int* perm,
+                            int nrows, double* af, unsigned* flags, unsigned epoch, unsigned* err, hipStream_t st);
+
 // Sweep over the rows of perm (forward or backward level order).  Forward: unit L into granules
 // gout, right-hand side per pro (0: src; 1: p = res + beta (p - omega avbar); 2: s = res - alpha
 // avbar, stored to p).  Backward: U from the forward granules gin into out and granules gout.

@@ -16,6 +16,8 @@
 // wavefront are forwarded through LDS.  Every wait is bounded and reports through *err.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdlib>
 
 #include "sparse_kernels.h"
@@ -502,6 +504,77 @@ __global__ void __launch_bounds__(kSweepRows) k_ilu_factor_lds(const int* __rest
   }
 }
 
+// The same factor with one wavefront per row (rows wider than a lane can take in reasonable time:
+// 3D mesh rows have up to 26 lower and 71 entries).  The rows are dealt round-robin in forward
+// level order to a grid that is resident at once (sized by the occupancy query), so a row only
+// waits for rows earlier in that order.  Per row: its image in LDS (entry e at w[e]); lane q polls
+// the flag of lower entry q's pivot row until all are published; then, for every lower entry q,
+// lane u holds U(j_q, .)'s u-th upper value and its position tgt[] in row i (-1: not held),
+// requested together.  The eliminations run in ascending q: mult = w[q] / U(j_q, j_q), w[q] = mult,
+// and every lane with a target subtracts mult * U at once (distinct targets; LDS in order within
+// the wavefront) -- the operations of k_ilu_factor in the same order, so bit-identical.  NL: lower
+// entries per row, at most; upper parts of at most 64 entries (host-checked).
+template <int NL>
+__global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__ ia, const double* __restrict__ a,
+                                                         const int* __restrict__ amap, const int* __restrict__ iaf,
+                                                         const int* __restrict__ dg, const int2* __restrict__ piv,
+                                                         const int* __restrict__ jaf, const int* __restrict__ toff,
+                                                         const signed char* __restrict__ tgt, const int* __restrict__ perm,
+                                                         int nrows, int nwaves, double* af, unsigned* flags, unsigned epoch,
+                                                         unsigned* err) {
+  __shared__ double s_row[4][kFacW + 1];
+  const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
+  double* w = s_row[wv];
+  const int gw = (int)blockIdx.x * 4 + wv;
+  for (int x = gw; x < nrows; x += nwaves) {
+    const int i = perm[x];
+    const int kb = iaf[i], kd = dg[i], ke = iaf[i + 1];
+    const int W = ke - kb, nl = kd - kb;
+    for (int e = lane; e < W; e += 64) w[e] = 0.0;
+    for (int ii = ia[i] + lane; ii < ia[i + 1]; ii += 64) w[amap[ii] - kb] = a[ii];
+    // lane q: lower entry q's pivot row (flag, diagonal position, end of its upper part, targets)
+    const bool low = lane < nl;
+    const int pj = low ? jaf[kb + lane] : 0;
+    const int2 pv = low ? piv[kb + lane] : make_int2(0, 0);
+    const int to = low ? toff[kb + lane] : 0;
+    unsigned spins = 0;
+    bool ready = !low, give_up = false;
+    while (true) {
+      if (!ready) ready = __hip_atomic_load(&flags[pj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (__all(ready)) break;
+      backoff(spins, false, err, 4u, give_up);
+      if (give_up) break;
+    }
+    if (give_up) return;
+    const double pvt = low ? ld_agent(&af[pv.x]) : 1.0;
+    double uu[NL];
+    int tg[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      uu[q] = 0.0;
+      tg[q] = -1;
+      if (q < nl) {
+        const int px = __shfl(pv.x, q), m = __shfl(pv.y, q) - px - 1, tq = __shfl(to, q);
+        if (lane < m) {
+          uu[q] = ld_agent(&af[px + 1 + lane]);
+          tg[q] = tgt[tq + lane];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NL; ++q)
+      if (q < nl) {
+        const double mult = w[q] / __shfl(pvt, q);
+        if (lane == 0) w[q] = mult;
+        if (tg[q] >= 0) w[tg[q]] = w[tg[q]] - mult * uu[q];
+      }
+    // publish: agent-scope (write-through) stores, drained, then the flag
+    for (int e = lane; e < W; e += 64) st_agent(&af[kb + e], w[e]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&flags[i], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Triangular sweeps (scaler_ILU::solve, ILU_class.cpp:470-499).  Forward (unit L):
 // y_i = b_i - sum_{k<diag} af_k y_jk; backward (U): x_i = (y_i - sum_{k>diag} af_k x_jk) / af_diag;
 // the terms are subtracted one at a time in ascending column order.  The forward sweep fuses the
@@ -734,6 +807,28 @@ void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, cons
   const int grid = nchunks < sweep_grid() ? nchunks : sweep_grid();
   hipLaunchKernelGGL((k_ilu_factor_lds<8, 8>), dim3(grid), dim3(kSweepRows), 0, st, ia, a, amap, iaf, jaf, dg, piv, toff,
                      tgt, perm, nchunks, af, flags, epoch, ticket, err);
+}
+
+int ilu_factor_wave_grid() {
+  static int g = [] {
+    int dev = 0, cus = 0, nb = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ilu_factor_wave<kFacWaveNL>, 256, 0);
+    nb = nb < 1 ? 1 : (nb > 8 ? 8 : nb);
+    return (cus > 0 ? cus : 1) * nb;
+  }();
+  return g;
+}
+
+void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, const int* iaf, const int* dg,
+                            const int2* piv, const int* jaf, const int* toff, const signed char* tgt, const int* perm,
+                            int nrows, double* af, unsigned* flags, unsigned epoch, unsigned* err, hipStream_t st) {
+  if (nrows <= 0) return;
+  // every workgroup resident at once: a row waits only for rows dealt before it
+  const int blocks = std::min(ilu_factor_wave_grid(), (nrows + 3) / 4);
+  hipLaunchKernelGGL(k_ilu_factor_wave<kFacWaveNL>, dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv, jaf, toff,
+                     tgt, perm, nrows, blocks * 4, af, flags, epoch, err);
 }
 
 void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
