@@ -39,6 +39,9 @@ constexpr int kImpMax = 2048;   // = kChainImpMax
 #define MMX_IMP_Q 4
 #endif
 constexpr int kImpQ = MMX_IMP_Q;  // imports each importer lane polls per round
+#ifndef MMX_CHAIN_SPEC
+#define MMX_CHAIN_SPEC 1  // compute loop bodies per entry-count class (no per-group branches)
+#endif
 constexpr unsigned kChainSpinMax = 1u << 22;
 
 template <typename T>
@@ -141,6 +144,8 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
   constexpr int kAuxWords = Aux<G>::words;
   typedef typename CodeOf<EE>::T CodeT;
   constexpr int RM = EE > 32 ? kRingWide : kRingMax;
+  // half-stage class: entry slots per row moved and read for a band using at most half of them
+  constexpr int EH = (E / 2) % 4 == 0 && ((E / 2) * (int)sizeof(CodeT)) % 16 == 0 ? E / 2 : E;
   __shared__ double s_val[DL * EE * 64];
   __shared__ CodeT s_code[DL * EE * 64];
   __shared__ uint32_t s_aux[DL * kAuxWords];
@@ -179,13 +184,22 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
     // waitcnt pass waits for every younger store/DMA (vmcnt(0)) at each iteration
     asm volatile("" : "+v"(cst), "+v"(len), "+v"(skew), "+v"(ns));
 
+    const bool half = EH < E && ca.trim && ca.bandE[b] <= EH;
     if (skip) {
       // nothing: an earlier wait gave up; the host reports it
     } else if (wave == 0) {
       // ---------------- compute ----------------
       // iteration t + 1's stage (entries, addresses, operands) is read before iteration t is
       // computed, so an iteration costs one LDS round trip (its dependency values) plus the chain
+      // 3D stages (E >= 32): the band's entry count selects the loop body at compile time (EB entry
+      // slots per row, pads included: 0 * (+0.0) changes nothing), so the iteration has no
+      // per-group branches (C4 sweeps 1.88 -> 1.80 ms).  2D stages keep one body with run-time
+      // checks against bandE: two bodies measured slower there (2.68 -> 2.80 ms; the instruction
+      // cache).  MMX_CHAIN_SPEC=0 (build option): one body everywhere.
+      constexpr bool kSpec = MMX_CHAIN_SPEC && E >= 32;
       const int Eb = ca.bandE[b];
+      auto compute = [&](auto ebc) {
+      constexpr int EB = decltype(ebc)::value;
       wait_vm<0>();  // nothing in flight here; tells the waitcnt pass so the loop needs no vmcnt waits
       unsigned long long c0 = ca.prof ? clk() : 0, cstage = 0, cimp = 0;
       bool ok = true;
@@ -203,8 +217,8 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-          for (int e0 = 0; e0 < E; e0 += 4)
-            if (e0 < Eb) {
+          for (int e0 = 0; e0 < EB; e0 += 4)
+            if (kSpec || e0 < Eb) {
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
                 f.a[g * E + e0 + q] = sv[(g * E + e0 + q) * 64 + lane];
@@ -279,8 +293,8 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-          for (int e0 = 0; e0 < E; e0 += 4)
-            if (e0 < Eb) {
+          for (int e0 = 0; e0 < EB; e0 += 4)
+            if (kSpec || e0 < Eb) {
 #pragma unroll
               for (int q = 0; q < 4; ++q) v[g * E + e0 + q] = s_dep[f.c[g * E + e0 + q]];
             }
@@ -307,8 +321,8 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
             // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
             double acc = (SEG && sg != 0) ? carry : f.init[g];
 #pragma unroll
-            for (int e0 = 0; e0 < E; e0 += 4)
-              if (e0 < Eb) {
+            for (int e0 = 0; e0 < EB; e0 += 4)
+              if (kSpec || e0 < Eb) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                   const int e = g * E + e0 + q;
@@ -366,6 +380,15 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           prof_add(ca.prof, 16 + 4 * pi + 2, cimp);
           prof_add(ca.prof, 16 + 4 * pi + 3, (unsigned long long)T);
         }
+      }
+      };
+      if constexpr (kSpec) {
+        if (half)
+          compute(std::integral_constant<int, EH>());
+        else
+          compute(std::integral_constant<int, E>());
+      } else {
+        compute(std::integral_constant<int, E>());
       }
     } else if (wave <= 2) {
       // ---------------- loaders (stages t = w, w+2, ...) ----------------
@@ -457,8 +480,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
         prof_add(ca.prof, 6, cin);
       }
       };
-      constexpr int EH = (E / 2) % 4 == 0 && ((E / 2) * (int)sizeof(CodeT)) % 16 == 0 ? E / 2 : E;
-      if (EH < E && ca.trim && ca.bandE[b] <= EH)
+      if (half)
         loader(std::integral_constant<int, EH>());
       else
         loader(std::integral_constant<int, E>());
