@@ -183,11 +183,35 @@ def spmv_bench(torch, la, mx, with_cpu):
     xs = np.zeros(n)
     nitr = A.solve(p, xs)
     st = A.stats()
-    out["cgstab"] = {"nitr": nitr, "solve_ms": round(st["t_solve_ms"], 2), "factor_ms": round(st["t_factor_ms"], 2),
-                     "sweep_ms": round(st["t_sweep_ms"] / max(st["n_sweep_timed"], 1), 3),
-                     "sweep_kernel": "k_chain_sweep (E=%d)" % st["sweep_e"] if st["sweep_mode"] else "k_sweep",
-                     "factor_kernel": "k_chain_factor" if st["factor_mode"] else "k_ilu_factor_lds",
-                     "ms_per_iter": round((st["t_solve_ms"] - st["t_factor_ms"]) / max(nitr, 1), 2)}
+    out["cgstab"] = _solve_stats(st, nitr)
+    A.close()
+    # the same solve on the C4 cube's Jacobian pattern (3D SquareGrid n = 63, 1,536,573 rows; the
+    # backward-Euler C4 line's solver), diagonally dominant values of the same form
+    mesh3 = mx.MeshData.rect(3, 63)
+    s3 = la.MatrixStruc(3 * mesh3.nP)
+    s3.mesh_pattern(3, mesh3.F)
+    s3.pack()
+    ia3, ja3 = s3.getia(), s3.getja()
+    n3 = len(ia3) - 1
+    rng3 = np.random.default_rng(5)
+    a3 = rng3.uniform(-1.0, 1.0, len(ja3))
+    d3 = np.nonzero(ja3 == np.repeat(np.arange(n3), np.diff(ia3)))[0]
+    a3[d3] = np.add.reduceat(np.abs(a3), ia3[:-1]) * 0.5 + 1.0
+    b3 = rng3.uniform(-1.0, 1.0, n3)
+    A3 = la.MatrixIter(s3)
+    A3.a[:] = a3
+    A3.b[:] = b3
+    A3.sfac(p)
+    A3.set_timing(True)
+    xs3 = np.zeros(n3)
+    A3.solve(p, xs3)
+    A3.reset_stats()
+    xs3 = np.zeros(n3)
+    nitr3 = A3.solve(p, xs3)
+    out["cgstab_c4"] = dict(_solve_stats(A3.stats(), nitr3), rows=n3, nnz=int(len(ja3)),
+                            matrix="3D SquareGrid n=63 (C4) Jacobian pattern, diagonally dominant U(-1,1) values")
+    A3.close()
+    A = None
     def _cpu():
         import time as _t
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -202,17 +226,32 @@ def spmv_bench(torch, la, mx, with_cpu):
         out["cpu_baseline"] = {"matmult_ms": round(cms, 2), "solve_ms": round(csolve, 1), "nitr": cit, "cores": 1,
                                "kind": "port", "sample": "oracle/lasolver.cpp (bit-identical restatement of "
                                "lib/LASolver, itself pinned to the reference build): 3 matmults + 1 solve"}
+        t0 = _t.perf_counter()
+        _, cit3, _ = L.solve(ia3, ja3, a3, b3)
+        c3 = (_t.perf_counter() - t0) * 1e3
+        out["cgstab_c4"]["cpu_baseline"] = {"solve_ms": round(c3, 1), "nitr": cit3, "cores": 1, "kind": "port",
+                                            "gpu_speedup": round(c3 / out["cgstab_c4"]["solve_ms"], 1),
+                                            "sample": "oracle/lasolver.cpp, the same C4-pattern solve"}
     if with_cpu:  # CPU baselines run after every GPU measurement (main)
         DEFERRED.append(_cpu)
-    A.close()
     return out
+
+
+def _solve_stats(st, nitr):
+    fk = {0: "k_ilu_factor_lds", 1: "k_chain_factor", 2: "k_ilu_factor_wave"}
+    return {"nitr": nitr, "solve_ms": round(st["t_solve_ms"], 2), "factor_ms": round(st["t_factor_ms"], 2),
+            "sweep_ms": round(st["t_sweep_ms"] / max(st["n_sweep_timed"], 1), 3),
+            "sweep_kernel": ("k_chain_sweep (E=%d/%d fwd/bwd)" % (st["sweep_e"], st["sweep_e_bwd"])
+                             if st["sweep_mode"] else "k_sweep"),
+            "factor_kernel": fk.get(st["factor_mode"], "?"),
+            "ms_per_iter": round((st["t_solve_ms"] - st["t_factor_ms"]) / max(nitr, 1), 2)}
 
 
 def be_bench(mx, with_cpu, dim=2):
     """Method 2 (Mesh::backwardsEulerStep, src/Mesh.cpp:1263-1341) on the device.  dim 2: SquareGrid
     n = 707 (1,001,113 nodes, the SpMV matrix's mesh), MEx3, dt 0.025, tau 0.5, rho 100 (the
     Monitor220 family).  dim 3: the C4 cube (3D SquareGrid n = 63, 512,191 nodes, a 1,536,573-row
-    Jacobian whose upper rows take the segmented chain sweeps), the C4 monitor (MonType 6), dt 0.025,
+    Jacobian whose upper rows take the 48-entry chain-sweep stages), the C4 monitor (MonType 6), dt 0.025,
     tau 0.5.  First step (pattern, symbolic ILU, sweep schedules, FD Jacobian) and the steady steps
     after it are timed separately; the CPU leg runs the oracle on the same mesh."""
     if dim == 2:

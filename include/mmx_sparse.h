@@ -70,9 +70,10 @@ typedef struct mmx_sparse_stats {
   double spmv_bytes;  /* algorithmic bytes of one SpMV: 12 nnz + 4 (n+1) + 16 n */
   double last_rms, rmsi;
   int sweep_mode;     /* triangular sweeps: 0 level-scheduled, 1 chain/band-scheduled */
-  int sweep_e;        /* chain sweeps: entry slots per row (8, 16, 32) */
+  int sweep_e;        /* chain sweeps: entry slots per row of the forward stages (8, 16, 32, 48) */
   int factor_mode;    /* numeric factor: 0 level-scheduled (a row per lane), 1 chain/band-scheduled,
                         2 level order with a wavefront per row */
+  int sweep_e_bwd;    /* the same for the backward stages */
 } mmx_sparse_stats;
 
 void mmx_param_iter_default(mmx_param_iter* p);

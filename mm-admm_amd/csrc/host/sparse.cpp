@@ -1072,6 +1072,7 @@ int mmx_matrix_stats_get(mmx_matrix m, mmx_sparse_stats* out) {
       out->sweep_mode = M.useChain ? 1 : 0;
       out->factor_mode = M.useChainFactor ? 1 : M.facWave ? 2 : 0;
       out->sweep_e = M.useChain ? M.chf.E : 0;
+      out->sweep_e_bwd = M.useChain ? M.chb.E : 0;
     }
   });
 }

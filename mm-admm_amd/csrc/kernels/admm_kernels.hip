@@ -1043,6 +1043,9 @@ __global__ void __launch_bounds__(BS) k_prox_fix(DeviceMesh<D> m, double tol, co
 // meets a near-midpoint power the whole block writes nothing back and is queued for k_prox_fix,
 // which recomputes it exactly from the untouched inputs.
 typedef double v2nt __attribute__((ext_vector_type(2)));
+#ifndef MMX_ZU_NT
+#define MMX_ZU_NT 0  // 2D prox: z and u written with nontemporal stores (experiment)
+#endif
 #ifndef MMX_LDS_DMA
 #define MMX_LDS_DMA 0  // 1: the chunk DMA'd to LDS after the gathers (C3 prox 0.380 ms); 0: through registers, requested before them (0.370 ms)
 #endif
@@ -1149,9 +1152,14 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
     double un[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      zs[zu_i<D>(i)] = z[i];
       un[i] = dx[i] - z[i];  // uBar = DXpU - z
-      us[zu_i<D>(i)] = un[i];
+      if constexpr (MMX_ZU_NT) {
+        __builtin_nontemporal_store(z[i], &zs[zu_i<D>(i)]);
+        __builtin_nontemporal_store(un[i], &us[zu_i<D>(i)]);
+      } else {
+        zs[zu_i<D>(i)] = z[i];
+        us[zu_i<D>(i)] = un[i];
+      }
     }
     write_tslot<D>(m, s, z, un);
   }

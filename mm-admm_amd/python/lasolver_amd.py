@@ -43,7 +43,8 @@ class SparseStats(ctypes.Structure):
                 ("t_solve_ms", ctypes.c_double), ("n_spmv_timed", ctypes.c_longlong),
                 ("n_sweep_timed", ctypes.c_longlong), ("n_factor_timed", ctypes.c_longlong),
                 ("spmv_bytes", ctypes.c_double), ("last_rms", ctypes.c_double), ("rmsi", ctypes.c_double),
-                ("sweep_mode", ctypes.c_int), ("sweep_e", ctypes.c_int), ("factor_mode", ctypes.c_int)]
+                ("sweep_mode", ctypes.c_int), ("sweep_e", ctypes.c_int), ("factor_mode", ctypes.c_int),
+                ("sweep_e_bwd", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

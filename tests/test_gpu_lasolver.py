@@ -303,6 +303,7 @@ def test_full_size_factor_sweeps_and_solve_bitwise(la, shift, factor, monkeypatc
     st = A.stats()
     assert st["sweep_mode"] == 1  # the chain/band sweeps
     assert st["factor_mode"] == (0 if factor == "level" else 1)  # no silent fallback at this size
+    assert st["sweep_e"] == 16 and st["sweep_e_bwd"] == 16
     af = L.ilu0(ia, ja, a)
     assert _bit(A.get_factor()[2], af)
     assert _bit(A.ilu_solve(b), L.ilu_solve(ia, ja, af, b))
