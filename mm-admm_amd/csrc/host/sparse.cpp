@@ -211,6 +211,7 @@ struct SparseMatrix {
   bool useChainFactor = false;
   bool facWave = false;     // k_ilu_factor_wave (one wavefront per row) over d_permw
   DevBuf<int> d_permw;
+  DevBuf<uint64_t> d_gF;    // the wave factor's granules (MMX_FACTOR_GRAN=0: flags + drained stores)
   DevBuf<unsigned long long> d_cprof;  // MMX_CHAIN_PROF: 2 x 512 counters (forward, backward)
   // numeric factor cache: the ILU of unchanged values is the same, so a solve re-factors only
   // after set_values / sfac (the reference re-factors in every solve, MatrixIter.cpp:684)
@@ -424,6 +425,16 @@ struct SparseMatrix {
           for (int i = 0; i < n; ++i) pw[cnt[lv[i]]++] = i;
           d_permw.upload(pw.data(), pw.size(), st);
           facWave = true;
+          // MMX_FACTOR_GRAN=1: publish through tagged granules instead of drained stores + a flag
+          // (measured: C4 factor 11.1 -> 12.0 ms, 2D 13.4 -> 13.5 ms; profiles/r05/experiments/
+          // lasolver3d/factor_gran_ab.jsonl)
+          const char* fg = getenv("MMX_FACTOR_GRAN");
+          if (fg && atoi(fg) == 1) {
+            d_gF.alloc(2 * jaf.size());
+            MMX_HIP(hipMemsetAsync(d_gF.p, 0, d_gF.n * sizeof(uint64_t), st));
+          } else {
+            d_gF.alloc(0);
+          }
         }
       }
     }
@@ -564,6 +575,7 @@ struct SparseMatrix {
     if (++fepoch == 0) {
       MMX_HIP(hipMemsetAsync(d_flags.p, 0, sizeof(unsigned) * n, st));
       if (useChainFactor) MMX_HIP(hipMemsetAsync(chfac.gU.p, 0, chfac.gU.n * sizeof(uint64_t), st));
+      if (d_gF.n) MMX_HIP(hipMemsetAsync(d_gF.p, 0, d_gF.n * sizeof(uint64_t), st));
       fepoch = 1;
     }
     begin(2);
@@ -574,7 +586,7 @@ struct SparseMatrix {
       launch_chain_factor(chfac.args, d_af.p, chfac.gU.p, fepoch, tickets(), errw(), st);
     } else if (facWave) {
       launch_ilu_factor_wave(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_dg.p, d_piv.p, d_jaf.p, d_toff.p, d_tgt.p, d_permw.p, n,
-                             d_af.p, d_flags.p, fepoch, errw(), st);
+                             d_af.p, d_flags.p, d_gF.n ? d_gF.p : nullptr, fepoch, errw(), st);
     } else if (facLds)
       launch_ilu_factor_lds(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_toff.p, d_tgt.p, d_permf.p, nchf,
                             d_af.p, d_flags.p, fepoch, tickets(), errw(), st);

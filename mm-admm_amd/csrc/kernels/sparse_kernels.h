@@ -63,11 +63,13 @@ void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, cons
 
 // One wavefront per row (k_ilu_factor_wave): perm = every row once in forward level order (no
 // padding); rows of at most kFacW entries, kFacWaveNL lower entries and 64 upper entries per pivot
-// row.  Bit-identical to the other factors.
+// row.  Bit-identical to the other factors.  gF (2 x nnz(factor) words, or null): rows publish their
+// diagonal and upper part as epoch-tagged granules there instead of drained stores + a flag.
 constexpr int kFacWaveNL = 32;
 void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, const int* iaf, const int* dg,
                             const int2* piv, const int* jaf, const int* toff, const signed char* tgt, const int* perm,
-                            int nrows, double* af, unsigned* flags, unsigned epoch, unsigned* err, hipStream_t st);
+                            int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* err,
+                            hipStream_t st);
 
 // Sweep over the rows of perm (forward or backward level order).  Forward: unit L into granules
 // gout, right-hand side per pro (0: src; 1: p = res + beta (p - omega avbar); 2: s = res - alpha

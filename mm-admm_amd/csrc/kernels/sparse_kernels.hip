@@ -514,14 +514,14 @@ __global__ void __launch_bounds__(kSweepRows) k_ilu_factor_lds(const int* __rest
 // and every lane with a target subtracts mult * U at once (distinct targets; LDS in order within
 // the wavefront) -- the operations of k_ilu_factor in the same order, so bit-identical.  NL: lower
 // entries per row, at most; upper parts of at most 64 entries (host-checked).
-template <int NL>
+template <int NL, bool GR>
 __global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__ ia, const double* __restrict__ a,
                                                          const int* __restrict__ amap, const int* __restrict__ iaf,
                                                          const int* __restrict__ dg, const int2* __restrict__ piv,
                                                          const int* __restrict__ jaf, const int* __restrict__ toff,
                                                          const signed char* __restrict__ tgt, const int* __restrict__ perm,
-                                                         int nrows, int nwaves, double* af, unsigned* flags, unsigned epoch,
-                                                         unsigned* err) {
+                                                         int nrows, int nwaves, double* af, unsigned* flags, uint64_t* gF,
+                                                         unsigned epoch, unsigned* err) {
   __shared__ double s_row[4][kFacW + 1];
   const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
   double* w = s_row[wv];
@@ -539,25 +539,59 @@ __global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__
     const int to = low ? toff[kb + lane] : 0;
     unsigned spins = 0;
     bool ready = !low, give_up = false;
+    double pvt = 1.0;
     while (true) {
-      if (!ready) ready = __hip_atomic_load(&flags[pj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (!ready) {
+        if constexpr (GR)
+          ready = load_granule(gF + 2 * (size_t)pv.x, epoch, pvt);  // the pivot's diagonal, self-validating
+        else
+          ready = __hip_atomic_load(&flags[pj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      }
       if (__all(ready)) break;
       backoff(spins, false, err, 4u, give_up);
       if (give_up) break;
     }
     if (give_up) return;
-    const double pvt = low ? ld_agent(&af[pv.x]) : 1.0;
+    if constexpr (!GR) pvt = low ? ld_agent(&af[pv.x]) : 1.0;
     double uu[NL];
     int tg[NL];
+    // GR: the upper values carry their own tags (stored in no particular order): all requested at
+    // once, then the lane repeats its requests until every tag is this factor's (rare)
+    bool okU = true;
+    auto fetch_upper = [&](bool first) {
 #pragma unroll
-    for (int q = 0; q < NL; ++q) {
-      uu[q] = 0.0;
-      tg[q] = -1;
-      if (q < nl) {
-        const int px = __shfl(pv.x, q), m = __shfl(pv.y, q) - px - 1, tq = __shfl(to, q);
-        if (lane < m) {
-          uu[q] = ld_agent(&af[px + 1 + lane]);
-          tg[q] = tgt[tq + lane];
+      for (int q = 0; q < NL; ++q) {
+        if (first) {
+          uu[q] = 0.0;
+          tg[q] = -1;
+        }
+        if (q < nl) {
+          const int px = __shfl(pv.x, q), m = __shfl(pv.y, q) - px - 1, tq = __shfl(to, q);  // (all lanes)
+          if (lane < m) {
+            if constexpr (GR) {
+              const uint64_t* g = gF + 2 * ((size_t)px + 1 + lane);
+              const uint64_t lo = __hip_atomic_load(const_cast<uint64_t*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const uint64_t hi = __hip_atomic_load(const_cast<uint64_t*>(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              okU = okU && (unsigned)(lo >> 32) == epoch && (unsigned)(hi >> 32) == epoch;
+              uu[q] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+            } else {
+              uu[q] = ld_agent(&af[px + 1 + lane]);
+            }
+            if (first) tg[q] = tgt[tq + lane];
+          }
+        }
+      }
+    };
+    fetch_upper(true);
+    if constexpr (GR) {
+      unsigned sp = 0;
+      bool gu = false;
+      while (!__all(okU)) {
+        backoff(sp, false, err, 4u, gu);
+        if (gu) return;
+        if (!okU) {
+          okU = true;
+          fetch_upper(false);
         }
       }
     }
@@ -568,10 +602,16 @@ __global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__
         if (lane == 0) w[q] = mult;
         if (tg[q] >= 0) w[tg[q]] = w[tg[q]] - mult * uu[q];
       }
-    // publish: agent-scope (write-through) stores, drained, then the flag
-    for (int e = lane; e < W; e += 64) st_agent(&af[kb + e], w[e]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(&flags[i], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (GR) {
+      // publish: the factor's values, and the diagonal + upper part as tagged granules (no drain)
+      for (int e = lane; e < W; e += 64) af[kb + e] = w[e];
+      for (int e = nl + lane; e < W; e += 64) store_granule(gF + 2 * ((size_t)kb + e), epoch, w[e]);
+    } else {
+      // publish: agent-scope (write-through) stores, drained, then the flag
+      for (int e = lane; e < W; e += 64) st_agent(&af[kb + e], w[e]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&flags[i], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -814,7 +854,10 @@ int ilu_factor_wave_grid() {
     int dev = 0, cus = 0, nb = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ilu_factor_wave<kFacWaveNL>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ilu_factor_wave<kFacWaveNL, true>, 256, 0);
+    int nb2 = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_ilu_factor_wave<kFacWaveNL, false>, 256, 0);
+    nb = nb < nb2 ? nb : nb2;
     nb = nb < 1 ? 1 : (nb > 8 ? 8 : nb);
     return (cus > 0 ? cus : 1) * nb;
   }();
@@ -823,12 +866,17 @@ int ilu_factor_wave_grid() {
 
 void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, const int* iaf, const int* dg,
                             const int2* piv, const int* jaf, const int* toff, const signed char* tgt, const int* perm,
-                            int nrows, double* af, unsigned* flags, unsigned epoch, unsigned* err, hipStream_t st) {
+                            int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* err,
+                            hipStream_t st) {
   if (nrows <= 0) return;
   // every workgroup resident at once: a row waits only for rows dealt before it
   const int blocks = std::min(ilu_factor_wave_grid(), (nrows + 3) / 4);
-  hipLaunchKernelGGL(k_ilu_factor_wave<kFacWaveNL>, dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv, jaf, toff,
-                     tgt, perm, nrows, blocks * 4, af, flags, epoch, err);
+  if (gF)
+    hipLaunchKernelGGL((k_ilu_factor_wave<kFacWaveNL, true>), dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv,
+                       jaf, toff, tgt, perm, nrows, blocks * 4, af, flags, gF, epoch, err);
+  else
+    hipLaunchKernelGGL((k_ilu_factor_wave<kFacWaveNL, false>), dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv,
+                       jaf, toff, tgt, perm, nrows, blocks * 4, af, flags, gF, epoch, err);
 }
 
 void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,

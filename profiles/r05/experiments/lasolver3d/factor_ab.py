@@ -7,7 +7,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import numpy as np
 import lasolver_amd as la
 import mmadmm_amd as mx
+MODES = sys.argv[1:] or None
 for dim, n, modes in ((3, 63, ["wave", "level", "wave"]), (2, 707, ["chain", "wave", "level", "chain", "wave"])):
+    if MODES:
+        modes = [m for m in MODES if not (dim == 3 and m.startswith("chain"))]
     mesh = mx.MeshData.rect(dim, n)
     s = la.MatrixStruc(dim * mesh.nP)
     s.mesh_pattern(dim, mesh.F)
@@ -21,10 +24,12 @@ for dim, n, modes in ((3, 63, ["wave", "level", "wave"]), (2, 707, ["chain", "wa
     a[d] = np.add.reduceat(np.abs(a), ia[:-1]) * 0.5 + 1.0
     ref = None
     for mode in modes:
-        if mode == "chain":
+        os.environ["MMX_FACTOR_GRAN"] = "1" if mode.endswith("-gran") else "0"
+        mode0 = mode.split("-")[0]
+        if mode0 == "chain":
             os.environ.pop("MMX_FACTOR", None)
         else:
-            os.environ["MMX_FACTOR"] = mode
+            os.environ["MMX_FACTOR"] = mode0
         A = la.MatrixIter(s)
         A.a[:] = a
         A.b[:] = np.ones(N)
