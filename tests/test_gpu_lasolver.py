@@ -233,7 +233,8 @@ def test_chain_sweeps_equal_level_sweeps(la, mesh, pair, monkeypatch):
     3D: the upper rows (up to 44 entries) take one position of a 48-entry stage (k_chain_sweep<...,
     48, ...>, pair 1 = the default) or two 32-entry segments (k_chain_sweep<..., SEG>, MMX_CHAIN_E48=0);
     rect 3 63 is the C4 bench's pattern (1,536,573 rows). 2D: two chain rows per iteration (pair 1,
-    the default) or one."""
+    the default) or one. Pair 0 also has the loaders move whole stages (MMX_CHAIN_TRIM=0)."""
+    monkeypatch.setenv("MMX_CHAIN_TRIM", pair)
     if mesh[1] == 3:
         if mesh[2] == 63 and pair == "0":
             pytest.skip("the segmented layout is covered on the smaller cubes")
@@ -363,14 +364,19 @@ def test_chain_factor_equals_level_factor(la, mesh, monkeypatch):
         assert _bit(af_c, L.ilu0(ia, ja, a))
 
 
-@pytest.mark.parametrize("mesh", [("rect", 2, 45), ("hexdisc", 40), ("rect", 3, 6), ("rect", 3, 20), ("rect", 3, 63)])
-def test_wave_factor_equals_level_factor(la, mesh, monkeypatch):
+@pytest.mark.parametrize("mesh,gran", [(("rect", 2, 45), "0"), (("hexdisc", 40), "0"), (("rect", 3, 6), "0"),
+                                       (("rect", 3, 20), "0"), (("rect", 3, 63), "0"), (("rect", 2, 45), "1"),
+                                       (("rect", 3, 20), "1")])
+def test_wave_factor_equals_level_factor(la, mesh, gran, monkeypatch):
     """The numeric ILU(0) factor with one wavefront per row (k_ilu_factor_wave, the 3D default:
     rows dealt in forward level order to a resident grid, the eliminations of a row in ascending
     lower entry with every target of one pivot row updated at once) is bit-identical to the
     level-scheduled lane-per-row k_ilu_factor_lds (MMX_FACTOR=level) and, at small sizes, to the
-    restatement of the reference; rect 3 63 is the C4 bench's Jacobian pattern (1,536,573 rows)."""
+    restatement of the reference; rect 3 63 is the C4 bench's Jacobian pattern (1,536,573 rows).
+    gran 1: rows publish through epoch-tagged granules (MMX_FACTOR_GRAN=1) instead of drained stores
+    and a flag."""
     import mmadmm_amd as mx
+    monkeypatch.setenv("MMX_FACTOR_GRAN", gran)
     if mesh[0] == "rect":
         m = oracle_py.Mesh.rect(mesh[1], mesh[2])
         dim, F, nP = mesh[1], m.F, m.nP
