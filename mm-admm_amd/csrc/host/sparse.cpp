@@ -12,6 +12,10 @@
 #include "chain_sched.h"
 #include "common.h"
 
+#ifndef MMX_CHAIN_VEC
+#define MMX_CHAIN_VEC 1  // = chain_sweep.hip: stage images lane-interleaved for 16-byte LDS reads
+#endif
+
 namespace mmx {
 namespace {
 
@@ -464,18 +468,42 @@ struct SparseMatrix {
     up(c.laneLen, S.laneLen);
     up(c.laneSkew, S.laneSkew);
     up(c.laneNs, S.laneNs);
+    // the stage images as the kernel reads them (MMX_CHAIN_VEC, chain_sweep.hip): within each
+    // [slot][g] block of E entries x 64 lanes, values [e / 2][lane][2] and codes [e / W][lane][W]
+    // (W = 4 for 32-bit codes, 8 for 16-bit) instead of [e][lane]; the DMA instructions move the
+    // same entry ranges either way
+    const int EEs = S.E * S.G;
+    const size_t blocks = S.code.size() / ((size_t)S.E * kChainLanes);
+    auto permute = [&](const std::vector<int>& lg, int W) {
+      std::vector<int> ph(lg.size());
+      if (!MMX_CHAIN_VEC) {
+        ph = lg;
+        return ph;
+      }
+      const int E = S.E, L = kChainLanes;
+#pragma omp parallel for schedule(static)
+      for (long long bk = 0; bk < (long long)blocks; ++bk) {
+        const size_t base = (size_t)bk * E * L;
+        for (int e = 0; e < E; ++e)
+          for (int l = 0; l < L; ++l) ph[base + (size_t)(e / W) * W * L + (size_t)l * W + (e % W)] = lg[base + (size_t)e * L + l];
+      }
+      return ph;
+    };
+    (void)EEs;
     const void* codePtr;
+    const std::vector<int> pcode = permute(S.code, S.E > 32 ? 8 : 4), psrc = permute(S.src, 2);
+    std::vector<uint16_t> c16;
     if (S.E > 32) {  // 16-bit codes (validate_chain_schedule: every index fits)
       if (S.seg || S.G != 1 || S.R > kChainRingWide) throw Error(MMADMM_ERR_INVALID, "wide chain stage layout");
-      std::vector<uint16_t> c16(S.code.begin(), S.code.end());
+      c16.assign(pcode.begin(), pcode.end());
       c.code16.upload(c16.data(), std::max<size_t>(c16.size(), 1), st);
-      MMX_HIP(hipStreamSynchronize(st));
       codePtr = c.code16.p;
     } else {
-      up(c.code, S.code);
+      up(c.code, pcode);
       codePtr = c.code.p;
     }
-    up(c.src, S.src);
+    up(c.src, psrc);
+    MMX_HIP(hipStreamSynchronize(st));  // (the host images above go out of scope)
     up(c.dsrc, S.dsrc);
     up(c.impRow, S.impRow);
     up(c.impSlot, S.impSlot);

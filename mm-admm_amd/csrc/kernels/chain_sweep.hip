@@ -39,6 +39,9 @@ constexpr int kImpMax = 2048;   // = kChainImpMax
 #define MMX_IMP_Q 4
 #endif
 constexpr int kImpQ = MMX_IMP_Q;  // imports each importer lane polls per round
+#ifndef MMX_CHAIN_VEC
+#define MMX_CHAIN_VEC 1  // = host/sparse.cpp: stage images lane-interleaved for 16-byte LDS reads
+#endif
 #ifndef MMX_CHAIN_SPEC
 #define MMX_CHAIN_SPEC 1  // compute loop bodies per entry-count class (no per-group branches)
 #endif
@@ -146,8 +149,8 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
   constexpr int RM = EE > 32 ? kRingWide : kRingMax;
   // half-stage class: entry slots per row moved and read for a band using at most half of them
   constexpr int EH = (E / 2) % 4 == 0 && ((E / 2) * (int)sizeof(CodeT)) % 16 == 0 ? E / 2 : E;
-  __shared__ double s_val[DL * EE * 64];
-  __shared__ CodeT s_code[DL * EE * 64];
+  __shared__ __attribute__((aligned(16))) double s_val[DL * EE * 64];
+  __shared__ __attribute__((aligned(16))) CodeT s_code[DL * EE * 64];
   __shared__ uint32_t s_aux[DL * kAuxWords];
   __shared__ double s_dep[DepCells<RM>::n];  // [0] = +0.0, lane rings, import slots
   __shared__ int s_tag[DL];
@@ -219,10 +222,35 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
 #pragma unroll
           for (int e0 = 0; e0 < EB; e0 += 4)
             if (kSpec || e0 < Eb) {
+              if constexpr (MMX_CHAIN_VEC) {
+                // stage image [g][e / 2][lane][2] (values), [g][e / 4][lane][4] (32-bit codes),
+                // [g][e / 8][lane][8] (16-bit codes): four entries of a lane in three LDS reads
+                const double2 a01 = *reinterpret_cast<const double2*>(sv + (g * E + e0) * 64 + lane * 2);
+                const double2 a23 = *reinterpret_cast<const double2*>(sv + (g * E + e0 + 2) * 64 + lane * 2);
+                f.a[g * E + e0] = a01.x;
+                f.a[g * E + e0 + 1] = a01.y;
+                f.a[g * E + e0 + 2] = a23.x;
+                f.a[g * E + e0 + 3] = a23.y;
+                if constexpr (sizeof(CodeT) == 4) {
+                  const int4 c4 = *reinterpret_cast<const int4*>(scd + (g * E + e0) * 64 + lane * 4);
+                  f.c[g * E + e0] = c4.x;
+                  f.c[g * E + e0 + 1] = c4.y;
+                  f.c[g * E + e0 + 2] = c4.z;
+                  f.c[g * E + e0 + 3] = c4.w;
+                } else {
+                  const ushort4 c4 =
+                      *reinterpret_cast<const ushort4*>(scd + (g * E + (e0 & ~7)) * 64 + lane * 8 + (e0 & 4));
+                  f.c[g * E + e0] = c4.x;
+                  f.c[g * E + e0 + 1] = c4.y;
+                  f.c[g * E + e0 + 2] = c4.z;
+                  f.c[g * E + e0 + 3] = c4.w;
+                }
+              } else {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                f.a[g * E + e0 + q] = sv[(g * E + e0 + q) * 64 + lane];
-                f.c[g * E + e0 + q] = scd[(g * E + e0 + q) * 64 + lane];
+                for (int q = 0; q < 4; ++q) {
+                  f.a[g * E + e0 + q] = sv[(g * E + e0 + q) * 64 + lane];
+                  f.c[g * E + e0 + q] = scd[(g * E + e0 + q) * 64 + lane];
+                }
               }
             }
 #pragma unroll
