@@ -16,9 +16,9 @@
 // order, exactly as the level-scheduled k_sweep and the reference.  SEG: a lane's rows take ns
 // positions each (32 entries per position, the partial sum carried in a register), for triangles
 // with rows wider than 48 entries; rows of 33..48 entries (the 3D backward triangle) take one
-// position of a 48-entry stage whose codes are 16-bit (LDS budget).  G = 2: a position computes two consecutive rows of the
-// chain (rows of at most 16 entries, 2D), the second taking the first's value from the register,
-// which halves the iterations on the critical path.
+// position of a 48-entry stage whose codes are 16-bit (LDS budget).  G = 2: a position computes
+// two consecutive rows of the chain (rows of at most 16 entries, 2D), the second taking the first's
+// value from the register, which halves the iterations on the critical path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -202,213 +202,213 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       constexpr bool kSpec = MMX_CHAIN_SPEC && E >= 32;
       const int Eb = ca.bandE[b];
       auto compute = [&](auto ebc) {
-      constexpr int EB = decltype(ebc)::value;
-      wait_vm<0>();  // nothing in flight here; tells the waitcnt pass so the loop needs no vmcnt waits
-      unsigned long long c0 = ca.prof ? clk() : 0, cstage = 0, cimp = 0;
-      bool ok = true;
-      struct Fetched {
-        double a[EE];
-        int c[EE];
-        double init[G], diag[G];
-        int need;
-      };
-      auto load_stage = [&](int st, Fetched& f) {
-        const uint32_t* sa0 = s_aux + st * kAuxWords;
-        f.need = (int)sa0[Aux<G>::need + lane];  // the same in every lane; made scalar where it is used
-        const double* sv = s_val + st * EE * 64;
-        const CodeT* scd = s_code + st * EE * 64;
+        constexpr int EB = decltype(ebc)::value;
+        wait_vm<0>();  // nothing in flight here; tells the waitcnt pass so the loop needs no vmcnt waits
+        unsigned long long c0 = ca.prof ? clk() : 0, cstage = 0, cimp = 0;
+        bool ok = true;
+        struct Fetched {
+          double a[EE];
+          int c[EE];
+          double init[G], diag[G];
+          int need;
+        };
+        auto load_stage = [&](int st, Fetched& f) {
+          const uint32_t* sa0 = s_aux + st * kAuxWords;
+          f.need = (int)sa0[Aux<G>::need + lane];  // the same in every lane; made scalar where it is used
+          const double* sv = s_val + st * EE * 64;
+          const CodeT* scd = s_code + st * EE * 64;
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+          for (int g = 0; g < G; ++g)
 #pragma unroll
-          for (int e0 = 0; e0 < EB; e0 += 4)
-            if (kSpec || e0 < Eb) {
-              if constexpr (MMX_CHAIN_VEC) {
-                // stage image [g][e / 2][lane][2] (values), [g][e / 4][lane][4] (32-bit codes),
-                // [g][e / 8][lane][8] (16-bit codes): four entries of a lane in three LDS reads
-                const double2 a01 = *reinterpret_cast<const double2*>(sv + (g * E + e0) * 64 + lane * 2);
-                const double2 a23 = *reinterpret_cast<const double2*>(sv + (g * E + e0 + 2) * 64 + lane * 2);
-                f.a[g * E + e0] = a01.x;
-                f.a[g * E + e0 + 1] = a01.y;
-                f.a[g * E + e0 + 2] = a23.x;
-                f.a[g * E + e0 + 3] = a23.y;
-                if constexpr (sizeof(CodeT) == 4) {
-                  const int4 c4 = *reinterpret_cast<const int4*>(scd + (g * E + e0) * 64 + lane * 4);
-                  f.c[g * E + e0] = c4.x;
-                  f.c[g * E + e0 + 1] = c4.y;
-                  f.c[g * E + e0 + 2] = c4.z;
-                  f.c[g * E + e0 + 3] = c4.w;
+            for (int e0 = 0; e0 < EB; e0 += 4)
+              if (kSpec || e0 < Eb) {
+                if constexpr (MMX_CHAIN_VEC) {
+                  // stage image [g][e / 2][lane][2] (values), [g][e / 4][lane][4] (32-bit codes),
+                  // [g][e / 8][lane][8] (16-bit codes): four entries of a lane in three LDS reads
+                  const double2 a01 = *reinterpret_cast<const double2*>(sv + (g * E + e0) * 64 + lane * 2);
+                  const double2 a23 = *reinterpret_cast<const double2*>(sv + (g * E + e0 + 2) * 64 + lane * 2);
+                  f.a[g * E + e0] = a01.x;
+                  f.a[g * E + e0 + 1] = a01.y;
+                  f.a[g * E + e0 + 2] = a23.x;
+                  f.a[g * E + e0 + 3] = a23.y;
+                  if constexpr (sizeof(CodeT) == 4) {
+                    const int4 c4 = *reinterpret_cast<const int4*>(scd + (g * E + e0) * 64 + lane * 4);
+                    f.c[g * E + e0] = c4.x;
+                    f.c[g * E + e0 + 1] = c4.y;
+                    f.c[g * E + e0 + 2] = c4.z;
+                    f.c[g * E + e0 + 3] = c4.w;
+                  } else {
+                    const ushort4 c4 =
+                        *reinterpret_cast<const ushort4*>(scd + (g * E + (e0 & ~7)) * 64 + lane * 8 + (e0 & 4));
+                    f.c[g * E + e0] = c4.x;
+                    f.c[g * E + e0 + 1] = c4.y;
+                    f.c[g * E + e0 + 2] = c4.z;
+                    f.c[g * E + e0 + 3] = c4.w;
+                  }
                 } else {
-                  const ushort4 c4 =
-                      *reinterpret_cast<const ushort4*>(scd + (g * E + (e0 & ~7)) * 64 + lane * 8 + (e0 & 4));
-                  f.c[g * E + e0] = c4.x;
-                  f.c[g * E + e0 + 1] = c4.y;
-                  f.c[g * E + e0 + 2] = c4.z;
-                  f.c[g * E + e0 + 3] = c4.w;
-                }
-              } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  f.a[g * E + e0 + q] = sv[(g * E + e0 + q) * 64 + lane];
-                  f.c[g * E + e0 + q] = scd[(g * E + e0 + q) * 64 + lane];
+                  for (int q = 0; q < 4; ++q) {
+                    f.a[g * E + e0 + q] = sv[(g * E + e0 + q) * 64 + lane];
+                    f.c[g * E + e0 + q] = scd[(g * E + e0 + q) * 64 + lane];
+                  }
                 }
               }
-            }
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const uint32_t* sa = sa0 + g * 384;
-          if (FWD) {
-            const double r0 = join_words(sa[lane], sa[64 + lane]);
-            if (PRO == 0) {
-              f.init[g] = r0;
-            } else if (PRO == 1) {
-              const double pv = join_words(sa[128 + lane], sa[192 + lane]);
-              const double av = join_words(sa[256 + lane], sa[320 + lane]);
-              f.init[g] = r0 + beta * (pv - omega * av);
+          for (int g = 0; g < G; ++g) {
+            const uint32_t* sa = sa0 + g * 384;
+            if (FWD) {
+              const double r0 = join_words(sa[lane], sa[64 + lane]);
+              if (PRO == 0) {
+                f.init[g] = r0;
+              } else if (PRO == 1) {
+                const double pv = join_words(sa[128 + lane], sa[192 + lane]);
+                const double av = join_words(sa[256 + lane], sa[320 + lane]);
+                f.init[g] = r0 + beta * (pv - omega * av);
+              } else {
+                const double av = join_words(sa[128 + lane], sa[192 + lane]);
+                f.init[g] = r0 - alpha * av;
+              }
+              f.diag[g] = 1.0;
             } else {
-              const double av = join_words(sa[128 + lane], sa[192 + lane]);
-              f.init[g] = r0 - alpha * av;
+              f.init[g] = join_words(sa[4 * lane], sa[4 * lane + 2]);  // granule {tag|lo, tag|hi}
+              f.diag[g] = join_words(sa[256 + 2 * lane], sa[256 + 2 * lane + 1]);
             }
-            f.diag[g] = 1.0;
-          } else {
-            f.init[g] = join_words(sa[4 * lane], sa[4 * lane + 2]);  // granule {tag|lo, tag|hi}
-            f.diag[g] = join_words(sa[256 + 2 * lane], sa[256 + 2 * lane + 1]);
           }
-        }
-      };
-      auto fetch = [&](int t, Fetched& f) {  // blocking: wait for stage t, then read it
-        const int st = t & (DL - 1);
-        unsigned spins = 0;
-        const unsigned long long w0 = ca.profIter ? clk() : 0;
-        while (lds_read(&s_tag[st]) != t)
-          if (!(ok = spin(spins, err, 8u))) break;
-        if (ca.profIter) cstage += clk() - w0;
-        load_stage(st, f);
-      };
-      // one iteration: a single batch of LDS reads -- this iteration's dependency values, the next
-      // stage's tag, the import count, and the next stage's contents (valid when that tag, read
-      // first and served first, says the stage has landed) -- then the chain
-      int seen = 0;  // import count read by the previous batch
-      double carry = 0.0;  // SEG: the partial sum of a row whose next segment comes at the next position
+        };
+        auto fetch = [&](int t, Fetched& f) {  // blocking: wait for stage t, then read it
+          const int st = t & (DL - 1);
+          unsigned spins = 0;
+          const unsigned long long w0 = ca.profIter ? clk() : 0;
+          while (lds_read(&s_tag[st]) != t)
+            if (!(ok = spin(spins, err, 8u))) break;
+          if (ca.profIter) cstage += clk() - w0;
+          load_stage(st, f);
+        };
+        // one iteration: a single batch of LDS reads -- this iteration's dependency values, the next
+        // stage's tag, the import count, and the next stage's contents (valid when that tag, read
+        // first and served first, says the stage has landed) -- then the chain
+        int seen = 0;  // import count read by the previous batch
+        double carry = 0.0;  // SEG: the partial sum of a row whose next segment comes at the next position
 #ifdef MMX_CHAIN_FINE
-      // probe (dev builds only): cycles of the step's segments, each closed by a full wait
-      unsigned long long fq[5] = {0, 0, 0, 0, 0};
+        // probe (dev builds only): cycles of the step's segments, each closed by a full wait
+        unsigned long long fq[5] = {0, 0, 0, 0, 0};
 #define MMX_FINE_MARK(k)                                     \
-  do {                                                       \
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
-    const unsigned long long _c = clk();                     \
-    fq[k] += _c - fqt;                                       \
-    fqt = _c;                                                \
-  } while (0)
+    do {                                                       \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+      const unsigned long long _c = clk();                     \
+      fq[k] += _c - fqt;                                       \
+      fqt = _c;                                                \
+    } while (0)
 #else
 #define MMX_FINE_MARK(k) \
-  do {                   \
-  } while (0)
+    do {                   \
+    } while (0)
 #endif
-      auto step = [&](int t, const Fetched& f, Fetched& nx) {
-        const int need = __builtin_amdgcn_readfirstlane(f.need);
-        if (need >= 0 && seen <= need) {  // imports this iteration reads: wait for their delivery
-          unsigned spins = 0;
-          const unsigned long long i0 = ca.profIter ? clk() : 0;
-          while ((seen = lds_read(&s_impDone)) <= need)
-            if (!(ok = spin(spins, err, 16u))) break;
-          if (ca.profIter) cimp += clk() - i0;
-          if (!ok) return;
-        }
+        auto step = [&](int t, const Fetched& f, Fetched& nx) {
+          const int need = __builtin_amdgcn_readfirstlane(f.need);
+          if (need >= 0 && seen <= need) {  // imports this iteration reads: wait for their delivery
+            unsigned spins = 0;
+            const unsigned long long i0 = ca.profIter ? clk() : 0;
+            while ((seen = lds_read(&s_impDone)) <= need)
+              if (!(ok = spin(spins, err, 16u))) break;
+            if (ca.profIter) cimp += clk() - i0;
+            if (!ok) return;
+          }
 #ifdef MMX_CHAIN_FINE
-        unsigned long long fqt = clk();
+          unsigned long long fqt = clk();
 #endif
-        double v[EE];
+          double v[EE];
 #pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int e0 = 0; e0 < EB; e0 += 4)
-            if (kSpec || e0 < Eb) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) v[g * E + e0 + q] = s_dep[f.c[g * E + e0 + q]];
-            }
-        MMX_FINE_MARK(0);
-        const bool hasNext = t + 1 < T;
-        const int stn = (t + 1) & (DL - 1);
-        const int tagN = __hip_atomic_load(&s_tag[stn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const int doneN = __hip_atomic_load(&s_impDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");  // keep the stage reads behind the tag read (LDS serves them in order)
-        if (hasNext) load_stage(stn, nx);
-        MMX_FINE_MARK(1);
-        const int p = t - skew;
-        double prev = 0.0;  // G = 2: the pair's first row
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const bool on = (G == 2) ? (p >= 0 && 2 * p + g < len) : (p >= 0 && p < len);
-          if (on) {
-            int ri = (G == 2) ? 2 * p + g : p, sg = 0;  // row of the chain, segment of the row
-            if constexpr (SEG) {
-              ri = p / ns;
-              sg = p - ri * ns;
-            }
-            const int row = FWD ? cst + ri : cst - ri;
-            // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
-            double acc = (SEG && sg != 0) ? carry : f.init[g];
+          for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int e0 = 0; e0 < EB; e0 += 4)
               if (kSpec || e0 < Eb) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  const int e = g * E + e0 + q;
-                  const double val = (G == 2 && g == 1 && f.c[e] == fwdCell) ? prev : v[e];
-                  acc -= f.a[e] * val;
-                }
+                for (int q = 0; q < 4; ++q) v[g * E + e0 + q] = s_dep[f.c[g * E + e0 + q]];
               }
-            if (SEG && sg != ns - 1) {
-              carry = acc;  // the row goes on at the next position
-            } else {
-              if (!FWD) acc = acc / f.diag[g];
+          MMX_FINE_MARK(0);
+          const bool hasNext = t + 1 < T;
+          const int stn = (t + 1) & (DL - 1);
+          const int tagN = __hip_atomic_load(&s_tag[stn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int doneN = __hip_atomic_load(&s_impDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          asm volatile("" ::: "memory");  // keep the stage reads behind the tag read (LDS serves them in order)
+          if (hasNext) load_stage(stn, nx);
+          MMX_FINE_MARK(1);
+          const int p = t - skew;
+          double prev = 0.0;  // G = 2: the pair's first row
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const bool on = (G == 2) ? (p >= 0 && 2 * p + g < len) : (p >= 0 && p < len);
+            if (on) {
+              int ri = (G == 2) ? 2 * p + g : p, sg = 0;  // row of the chain, segment of the row
+              if constexpr (SEG) {
+                ri = p / ns;
+                sg = p - ri * ns;
+              }
+              const int row = FWD ? cst + ri : cst - ri;
+              // acc -= a_e * value_e in entry order; pads are 0 * (+0.0) and change nothing
+              double acc = (SEG && sg != 0) ? carry : f.init[g];
+#pragma unroll
+              for (int e0 = 0; e0 < EB; e0 += 4)
+                if (kSpec || e0 < Eb) {
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) {
+                    const int e = g * E + e0 + q;
+                    const double val = (G == 2 && g == 1 && f.c[e] == fwdCell) ? prev : v[e];
+                    acc -= f.a[e] * val;
+                  }
+                }
+              if (SEG && sg != ns - 1) {
+                carry = acc;  // the row goes on at the next position
+              } else {
+                if (!FWD) acc = acc / f.diag[g];
 #ifdef MMX_CHAIN_FINE
-              asm volatile("" ::"v"(acc));
-              MMX_FINE_MARK(2);
+                asm volatile("" ::"v"(acc));
+                MMX_FINE_MARK(2);
 #endif
-              s_dep[1 + lane * (R + 1) + (((G == 2) ? ri : p) & (R - 1))] = acc;
-              const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
-              __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-              if (!FWD) out[row] = acc;
-              if (FWD && PRO != 0) pvec[row] = f.init[g];
-              prev = acc;
+                s_dep[1 + lane * (R + 1) + (((G == 2) ? ri : p) & (R - 1))] = acc;
+                const uint64_t bits = (uint64_t)__double_as_longlong(acc), tag = (uint64_t)epoch << 32;
+                __hip_atomic_store(gout + 2 * (size_t)row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if (!FWD) out[row] = acc;
+                if (FWD && PRO != 0) pvec[row] = f.init[g];
+                prev = acc;
+              }
             }
           }
+          if (lane == 0) lds_write(&s_prog, t + 1);
+          MMX_FINE_MARK(3);
+          seen = doneN;
+          if (hasNext && __builtin_amdgcn_readfirstlane(tagN) != t + 1) fetch(t + 1, nx);  // not landed yet
+          MMX_FINE_MARK(4);
+        };
+        Fetched fa, fb;
+        if (T > 0) fetch(0, fa);
+        for (int t = 0; t < T && ok; t += 2) {
+          step(t, fa, fb);
+          if (t + 1 >= T || !ok) break;
+          step(t + 1, fb, fa);
         }
-        if (lane == 0) lds_write(&s_prog, t + 1);
-        MMX_FINE_MARK(3);
-        seen = doneN;
-        if (hasNext && __builtin_amdgcn_readfirstlane(tagN) != t + 1) fetch(t + 1, nx);  // not landed yet
-        MMX_FINE_MARK(4);
-      };
-      Fetched fa, fb;
-      if (T > 0) fetch(0, fa);
-      for (int t = 0; t < T && ok; t += 2) {
-        step(t, fa, fb);
-        if (t + 1 >= T || !ok) break;
-        step(t + 1, fb, fa);
-      }
-      if (ca.prof && lane == 0) {
-        const unsigned long long tot = clk() - c0;
-        prof_add(ca.prof, 0, tot);
-        prof_add(ca.prof, 1, cstage);
-        prof_add(ca.prof, 2, cimp);
-        prof_add(ca.prof, 3, (unsigned long long)T);
-        prof_add(ca.prof, 8, 1ull);
+        if (ca.prof && lane == 0) {
+          const unsigned long long tot = clk() - c0;
+          prof_add(ca.prof, 0, tot);
+          prof_add(ca.prof, 1, cstage);
+          prof_add(ca.prof, 2, cimp);
+          prof_add(ca.prof, 3, (unsigned long long)T);
+          prof_add(ca.prof, 8, 1ull);
 #ifdef MMX_CHAIN_FINE
-        for (int k = 0; k < 5; ++k) prof_add(ca.prof, 9 + k, fq[k]);
+          for (int k = 0; k < 5; ++k) prof_add(ca.prof, 9 + k, fq[k]);
 #endif
-        const int pi = b < 32 ? b : (b >= ca.nbands - 32 ? 64 + b - ca.nbands : -1);
-        if (pi >= 0) {
-          prof_add(ca.prof, 16 + 4 * pi, tot);
-          prof_add(ca.prof, 16 + 4 * pi + 1, cstage);
-          prof_add(ca.prof, 16 + 4 * pi + 2, cimp);
-          prof_add(ca.prof, 16 + 4 * pi + 3, (unsigned long long)T);
+          const int pi = b < 32 ? b : (b >= ca.nbands - 32 ? 64 + b - ca.nbands : -1);
+          if (pi >= 0) {
+            prof_add(ca.prof, 16 + 4 * pi, tot);
+            prof_add(ca.prof, 16 + 4 * pi + 1, cstage);
+            prof_add(ca.prof, 16 + 4 * pi + 2, cimp);
+            prof_add(ca.prof, 16 + 4 * pi + 3, (unsigned long long)T);
+          }
         }
-      }
       };
       if constexpr (kSpec) {
         if (half)
@@ -424,89 +424,89 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
       // bands: <= 5 of 16) has only those moved: fewer DMA instructions per stage, so more stages
       // fit the 6-bit vmcnt window in flight.  The compute wave reads entries < bandE only.
       auto loader = [&](auto ebc) {
-      constexpr int EB = decltype(ebc)::value;  // entry slots moved per row
-      constexpr int NVb = EB / 2, NCb = EB * (int)sizeof(CodeT) / 16;
-      constexpr int NIb = G * (NVb + NCb) + NAUX;
-      constexpr int LAGb0 = 63 / NIb < 1 ? 1 : 63 / NIb;
-      constexpr int LAGb = LAGb0 < DL / 2 ? LAGb0 : DL / 2;
-      static_assert(EB <= E && EB % 4 == 0 && (EB * (int)sizeof(CodeT)) % 16 == 0, "stage entry slots");
-      const int w = wave - 1;
-      int nextPub = w;
-      bool ok = true;
-      unsigned long long cfl = 0, csl = 0, cin = 0;
-      for (int t = w; t < T && ok; t += 2) {
-        const int st = t & (DL - 1);
-        if (lds_read(&s_prog) < t - DL + 1) {  // slot busy: publish what is in flight, then wait
-          const unsigned long long f0 = ca.prof ? clk() : 0;
-          wait_vm<0>();
-          if (ca.prof) cfl += clk() - f0;
-          for (; nextPub < t; nextPub += 2)
-            if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
-          unsigned spins = 0;
-          const unsigned long long s0 = ca.prof ? clk() : 0;
-          while (lds_read(&s_prog) < t - DL + 1)
-            if (!(ok = spin(spins, err, 32u))) break;
-          if (ca.prof) csl += clk() - s0;
-          if (!ok) break;
-        }
-        const size_t slot = (size_t)(sb + t);
-        const double* gv = ca.val + slot * EE * 64;
-        const char* gc = (const char*)ca.code + slot * EE * 64 * sizeof(CodeT);
+        constexpr int EB = decltype(ebc)::value;  // entry slots moved per row
+        constexpr int NVb = EB / 2, NCb = EB * (int)sizeof(CodeT) / 16;
+        constexpr int NIb = G * (NVb + NCb) + NAUX;
+        constexpr int LAGb0 = 63 / NIb < 1 ? 1 : 63 / NIb;
+        constexpr int LAGb = LAGb0 < DL / 2 ? LAGb0 : DL / 2;
+        static_assert(EB <= E && EB % 4 == 0 && (EB * (int)sizeof(CodeT)) % 16 == 0, "stage entry slots");
+        const int w = wave - 1;
+        int nextPub = w;
+        bool ok = true;
+        unsigned long long cfl = 0, csl = 0, cin = 0;
+        for (int t = w; t < T && ok; t += 2) {
+          const int st = t & (DL - 1);
+          if (lds_read(&s_prog) < t - DL + 1) {  // slot busy: publish what is in flight, then wait
+            const unsigned long long f0 = ca.prof ? clk() : 0;
+            wait_vm<0>();
+            if (ca.prof) cfl += clk() - f0;
+            for (; nextPub < t; nextPub += 2)
+              if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
+            unsigned spins = 0;
+            const unsigned long long s0 = ca.prof ? clk() : 0;
+            while (lds_read(&s_prog) < t - DL + 1)
+              if (!(ok = spin(spins, err, 32u))) break;
+            if (ca.prof) csl += clk() - s0;
+            if (!ok) break;
+          }
+          const size_t slot = (size_t)(sb + t);
+          const double* gv = ca.val + slot * EE * 64;
+          const char* gc = (const char*)ca.code + slot * EE * 64 * sizeof(CodeT);
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
+          for (int g = 0; g < G; ++g) {
 #pragma unroll
-          for (int i = 0; i < NVb; ++i)
-            dma16(gv + (g * E / 2 + i) * 128 + lane * 2, s_val + st * EE * 64 + (g * E / 2 + i) * 128);
-          constexpr int gcs = E * (int)sizeof(CodeT) / 16;  // code instructions per row block
+            for (int i = 0; i < NVb; ++i)
+              dma16(gv + (g * E / 2 + i) * 128 + lane * 2, s_val + st * EE * 64 + (g * E / 2 + i) * 128);
+            constexpr int gcs = E * (int)sizeof(CodeT) / 16;  // code instructions per row block
 #pragma unroll
-          for (int i = 0; i < NCb; ++i)
-            dma16(gc + (g * gcs + i) * 1024 + lane * 16, (char*)(s_code + st * EE * 64) + (g * gcs + i) * 1024);
-        }
-        const int p = t - skew;
-        uint32_t* sa0 = s_aux + st * kAuxWords;
+            for (int i = 0; i < NCb; ++i)
+              dma16(gc + (g * gcs + i) * 1024 + lane * 16, (char*)(s_code + st * EE * 64) + (g * gcs + i) * 1024);
+          }
+          const int p = t - skew;
+          uint32_t* sa0 = s_aux + st * kAuxWords;
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          // the row's operands (at each of its segments; a missing second row of a pair: row 0)
-          const int ri = (G == 2) ? 2 * p + g : (SEG ? p / ns : p);
-          const bool on = (G == 2) ? (p >= 0 && ri < len) : (p >= 0 && p < len);
-          const int row = on ? (FWD ? cst + ri : cst - ri) : 0;
-          uint32_t* sa = sa0 + g * 384;
-          if (FWD) {
-            const double* v0 = (PRO == 0) ? src : res;
-            dma4((const char*)(v0 + row), sa);
-            dma4((const char*)(v0 + row) + 4, sa + 64);
-            if (PRO == 1) {
-              dma4((const char*)(pvec + row), sa + 128);
-              dma4((const char*)(pvec + row) + 4, sa + 192);
-              dma4((const char*)(avbar + row), sa + 256);
-              dma4((const char*)(avbar + row) + 4, sa + 320);
-            } else if (PRO == 2) {
-              dma4((const char*)(avbar + row), sa + 128);
-              dma4((const char*)(avbar + row) + 4, sa + 192);
+          for (int g = 0; g < G; ++g) {
+            // the row's operands (at each of its segments; a missing second row of a pair: row 0)
+            const int ri = (G == 2) ? 2 * p + g : (SEG ? p / ns : p);
+            const bool on = (G == 2) ? (p >= 0 && ri < len) : (p >= 0 && p < len);
+            const int row = on ? (FWD ? cst + ri : cst - ri) : 0;
+            uint32_t* sa = sa0 + g * 384;
+            if (FWD) {
+              const double* v0 = (PRO == 0) ? src : res;
+              dma4((const char*)(v0 + row), sa);
+              dma4((const char*)(v0 + row) + 4, sa + 64);
+              if (PRO == 1) {
+                dma4((const char*)(pvec + row), sa + 128);
+                dma4((const char*)(pvec + row) + 4, sa + 192);
+                dma4((const char*)(avbar + row), sa + 256);
+                dma4((const char*)(avbar + row) + 4, sa + 320);
+              } else if (PRO == 2) {
+                dma4((const char*)(avbar + row), sa + 128);
+                dma4((const char*)(avbar + row) + 4, sa + 192);
+              }
+            } else {
+              dma16(gin + 2 * (size_t)row, sa);  // 64 x 16 B: words 0..255
+              if (lane < 32) dma16(ca.dval + (slot * G + g) * 64 + lane * 2, sa + 256);  // 64 diagonals: words 256..383
             }
-          } else {
-            dma16(gin + 2 * (size_t)row, sa);  // 64 x 16 B: words 0..255
-            if (lane < 32) dma16(ca.dval + (slot * G + g) * 64 + lane * 2, sa + 256);  // 64 diagonals: words 256..383
+          }
+          dma4(ca.impNeed + slot, sa0 + Aux<G>::need);  // the same word in every lane
+          if ((t - nextPub) / 2 + 1 > LAGb) {
+            const unsigned long long l0 = ca.prof ? clk() : 0;
+            wait_vm<NIb * LAGb>();
+            if (ca.prof) cin += clk() - l0;
+            for (; nextPub <= t - 2 * LAGb; nextPub += 2)
+              if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
           }
         }
-        dma4(ca.impNeed + slot, sa0 + Aux<G>::need);  // the same word in every lane
-        if ((t - nextPub) / 2 + 1 > LAGb) {
-          const unsigned long long l0 = ca.prof ? clk() : 0;
-          wait_vm<NIb * LAGb>();
-          if (ca.prof) cin += clk() - l0;
-          for (; nextPub <= t - 2 * LAGb; nextPub += 2)
+        wait_vm<0>();
+        if (ok)
+          for (; nextPub < T; nextPub += 2)
             if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
+        if (ca.prof && lane == 0) {
+          prof_add(ca.prof, 4, cfl);
+          prof_add(ca.prof, 5, csl);
+          prof_add(ca.prof, 6, cin);
         }
-      }
-      wait_vm<0>();
-      if (ok)
-        for (; nextPub < T; nextPub += 2)
-          if (lane == 0) lds_write(&s_tag[nextPub & (DL - 1)], nextPub);
-      if (ca.prof && lane == 0) {
-        prof_add(ca.prof, 4, cfl);
-        prof_add(ca.prof, 5, csl);
-        prof_add(ca.prof, 6, cin);
-      }
       };
       if (half)
         loader(std::integral_constant<int, EH>());
