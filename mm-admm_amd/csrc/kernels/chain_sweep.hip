@@ -114,15 +114,19 @@ struct CodeOf<48> {
 __device__ __forceinline__ bool aborted(unsigned* err) {
   return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
+template <bool SLEEP = true>
 __device__ __forceinline__ bool spin(unsigned& spins, unsigned* err, unsigned code) {
   if ((++spins & 255u) == 0 && aborted(err)) return false;
-  if (spins > kChainSpinMax) {
+  if (spins > (SLEEP ? kChainSpinMax : kChainSpinMax * 16u)) {
     atomicOr(err, code);
     return false;
   }
-  __builtin_amdgcn_s_sleep(1);
+  if constexpr (SLEEP) __builtin_amdgcn_s_sleep(1);
   return true;
 }
+#ifndef MMX_CHAIN_HOTSPIN
+#define MMX_CHAIN_HOTSPIN 1  // the compute wave polls its stage / import counters without s_sleep
+#endif
 
 // profiling counters (ca.prof, s_memtime cycles): 0 compute cycles, 1 compute waiting for stages,
 // 2 compute waiting for imports, 3 compute iterations, 4 loader flush waits, 5 loader slot waits,
@@ -280,7 +284,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
           unsigned spins = 0;
           const unsigned long long w0 = ca.profIter ? clk() : 0;
           while (lds_read(&s_tag[st]) != t)
-            if (!(ok = spin(spins, err, 8u))) break;
+            if (!(ok = spin<!MMX_CHAIN_HOTSPIN>(spins, err, 8u))) break;
           if (ca.profIter) cstage += clk() - w0;
           load_stage(st, f);
         };
@@ -310,7 +314,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
             unsigned spins = 0;
             const unsigned long long i0 = ca.profIter ? clk() : 0;
             while ((seen = lds_read(&s_impDone)) <= need)
-              if (!(ok = spin(spins, err, 16u))) break;
+              if (!(ok = spin<!MMX_CHAIN_HOTSPIN>(spins, err, 16u))) break;
             if (ca.profIter) cimp += clk() - i0;
             if (!ok) return;
           }
