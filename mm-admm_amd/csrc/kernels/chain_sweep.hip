@@ -125,7 +125,7 @@ __device__ __forceinline__ bool spin(unsigned& spins, unsigned* err, unsigned co
   return true;
 }
 #ifndef MMX_CHAIN_HOTSPIN
-#define MMX_CHAIN_HOTSPIN 1  // the compute wave polls its stage / import counters without s_sleep
+#define MMX_CHAIN_HOTSPIN 0  // 1: the compute wave polls its stage / import counters without s_sleep
 #endif
 
 // profiling counters (ca.prof, s_memtime cycles): 0 compute cycles, 1 compute waiting for stages,
