@@ -418,7 +418,8 @@ std::string validate_chain_schedule(const ChainSchedule& S, int n, const std::ve
   if (G == 2 && S.seg) return "pairs of segmented rows";
   if (E != 8 && E != 16 && E != 32 && E != kChainWideE) return "no kernel for this stage width";
   if (R < 1 || (R & (R - 1)) || R > (E > 32 ? kChainRingWide : kChainRingMax)) return "ring larger than the kernel's";
-  if (E > 32 && (S.seg || G != 1 || 1 + L * (R + 1) + S.RI >= 65536)) return "wide stage codes do not fit 16 bits";
+  if (E > 32 && (S.seg || G != 1)) return "wide stages with segments or pairs";
+  if (1 + L * (R + 1) + S.RI >= 65536) return "stage codes do not fit 16 bits";  // (the kernel's codes are 16-bit)
   // where every row is computed: band, lane, position of its final value, ring sequence number,
   // part (pair half), segments
   std::vector<int> bandOf(n, -1), laneOf(n, -1), posOf(n, -1), ringOf(n, -1), partOf(n, 0), iterOf(n, -1),

@@ -12,10 +12,6 @@
 #include "chain_sched.h"
 #include "common.h"
 
-#ifndef MMX_CHAIN_VEC
-#define MMX_CHAIN_VEC 1  // = chain_sweep.hip: stage images lane-interleaved for 16-byte LDS reads
-#endif
-
 namespace mmx {
 namespace {
 
@@ -491,10 +487,12 @@ struct SparseMatrix {
     };
     (void)EEs;
     const void* codePtr;
-    const std::vector<int> pcode = permute(S.code, S.E > 32 ? 8 : 4), psrc = permute(S.src, 2);
+    const bool c16on = chain_code16(S.E * S.G);
+    const std::vector<int> pcode = permute(S.code, c16on ? 8 : 4), psrc = permute(S.src, 2);
     std::vector<uint16_t> c16;
-    if (S.E > 32) {  // 16-bit codes (validate_chain_schedule: every index fits)
-      if (S.seg || S.G != 1 || S.R > kChainRingWide) throw Error(MMADMM_ERR_INVALID, "wide chain stage layout");
+    if (S.E > 32 && (S.seg || S.G != 1 || S.R > kChainRingWide))
+      throw Error(MMADMM_ERR_INVALID, "wide chain stage layout");
+    if (c16on) {  // 16-bit codes (validate_chain_schedule: every index fits)
       c16.assign(pcode.begin(), pcode.end());
       c.code16.upload(c16.data(), std::max<size_t>(c16.size(), 1), st);
       codePtr = c.code16.p;

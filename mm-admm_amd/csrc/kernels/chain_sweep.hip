@@ -39,9 +39,6 @@ constexpr int kImpMax = 2048;   // = kChainImpMax
 #define MMX_IMP_Q 4
 #endif
 constexpr int kImpQ = MMX_IMP_Q;  // imports each importer lane polls per round
-#ifndef MMX_CHAIN_VEC
-#define MMX_CHAIN_VEC 1  // = host/sparse.cpp: stage images lane-interleaved for 16-byte LDS reads
-#endif
 #ifndef MMX_CHAIN_SPEC
 #define MMX_CHAIN_SPEC 1  // compute loop bodies per entry-count class (no per-group branches)
 #endif
@@ -100,14 +97,10 @@ template <int RM>
 struct DepCells {
   static constexpr int n = 1 + 64 * (RM + 1) + kImpMax + 1;
 };
-// entry codes: 32-bit, 16-bit in the 48-entry stages
+// entry codes: 16-bit (32-bit in MMX_CHAIN_CODE16=0 builds, except the 48-entry stages)
 template <int EE>
 struct CodeOf {
-  typedef int T;
-};
-template <>
-struct CodeOf<48> {
-  typedef uint16_t T;
+  typedef typename std::conditional<chain_code16(EE), uint16_t, int>::type T;
 };
 
 // abort protocol: a bounded wait that gives up sets err; everyone polls err now and then

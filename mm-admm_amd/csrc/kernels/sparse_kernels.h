@@ -81,6 +81,17 @@ void launch_sweep(bool fwd, int pro, const int* iaf, const int* jaf, const int* 
 
 // Band/chain-scheduled sweeps (chain_sweep.hip, schedule host/chain_sched.h): the same rows and
 // arithmetic as launch_sweep, with intra-band dependencies resolved in LDS.
+// chain-sweep stage images (chain_sweep.hip, host/sparse.cpp upload_chain): entries lane-interleaved
+// for 16-byte LDS reads (MMX_CHAIN_VEC), entry codes 16-bit (MMX_CHAIN_CODE16; 32-bit otherwise,
+// except the 48-entry stages, always 16-bit)
+#ifndef MMX_CHAIN_VEC
+#define MMX_CHAIN_VEC 1
+#endif
+#ifndef MMX_CHAIN_CODE16
+#define MMX_CHAIN_CODE16 1
+#endif
+inline constexpr bool chain_code16(int ee) { return MMX_CHAIN_CODE16 || ee > 32; }
+
 struct ChainArgs {
   const int* bandSlot;
   const int* bandT;
@@ -92,7 +103,7 @@ struct ChainArgs {
   const int* laneNs;   // per band * 64 + lane: segments per row (seg schedules; rows wider than 32 entries)
   const int* bandE;    // per band: entry slots in use (multiple of 4)
   const double* val;   // [slot][E][64] entry values (filled from the factor by launch_chain_fill)
-  const void* code;    // [slot][E][64] LDS index of the entry's value (0: the zero cell): int32, uint16 at E = 48
+  const void* code;    // [slot][E][64] LDS index of the entry's value (0: the zero cell): uint16 (chain_code16) or int32
   const double* dval;  // [slot][64] diagonals (backward)
   const int* impRow;
   const int* impSlot;  // per import: LDS import slot
