@@ -379,12 +379,8 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
 #ifndef MMX_XU_CH2D
 #define MMX_XU_CH2D 6  // 2D: incident slots requested at once per node (C3: 8 0.066 ms, 6 0.0645, 4 0.079)
 #endif
-#ifndef MMX_XU_OCC
-#define MMX_XU_OCC 0  // waves per SIMD the x-update is register-bounded to (0: the compiler's choice, 6 in 2D;
-                      // 8: 64 VGPRs + 2 spills, C3 0.063 -> 0.067 ms, profiles/r05/ab/xupdate_occ/)
-#endif
 template <int D, bool RESID, bool TS, bool ZX = false, bool PRED = false>
-__global__ void __launch_bounds__(kBlock, MMX_XU_OCC > 0 ? MMX_XU_OCC : 1) k_xupdate(DeviceMesh<D> m, StepScalars sc,
+__global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
                                                      const double* __restrict__ xBar,
                                                      const double* __restrict__ z,
                                                      const double* __restrict__ u, double* __restrict__ x,
