@@ -16,7 +16,7 @@
 // order, exactly as the level-scheduled k_sweep and the reference.  SEG: a lane's rows take ns
 // positions each (32 entries per position, the partial sum carried in a register), for triangles
 // with rows wider than 48 entries; rows of 33..48 entries (the 3D backward triangle) take one
-// position of a 48-entry stage whose codes are 16-bit (LDS budget).  G = 2: a position computes
+// position of a 48-entry stage (entry codes are 16-bit in every stage).  G = 2: a position computes
 // two consecutive rows of the chain (rows of at most 16 entries, 2D), the second taking the first's
 // value from the register, which halves the iterations on the critical path.
 #include <hip/hip_runtime.h>
