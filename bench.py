@@ -60,6 +60,16 @@ def parse():
     ap.add_argument("--no-bfgs", action="store_true", help="skip the BFGS-heavy (rho = 1) 2D section")
     ap.add_argument("--c5", action="store_true",
                     help="add BASELINE config 5 on one GPU: 3D 5.09M-node mesh, time-varying monitor")
+    ap.add_argument("--budget-s", type=float, default=1500.0,
+                    help="N > 1: wall-clock budget of every rank (a watchdog ends a rank that exceeds it with exit "
+                         "status 124, naming its phase) and of the re-launched job (the launcher's process group is "
+                         "killed after the budget + 60 s, naming the ranks that never finished set-up)")
+    ap.add_argument("--comm-timeout", type=float, default=300.0,
+                    help="N > 1: deadline (s) of the RCCL communicator's creation and of every wait of a "
+                         "partitioned step (MMADMM_ERR_RCCL after ncclCommAbort, never a hang)")
+    ap.add_argument("--rendezvous-only", action="store_true",
+                    help="N > 1: launch the ranks, rendezvous over gloo, report the phases and exit (no GPU; a CI "
+                         "check of the launch path and its failure handling)")
     ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
                     help="c3: 2D 1M-node disc (the headline); c4: 3D 512k-node cube per GPU, anisotropic monitor "
                          "(weak scaling); c5: 3D 5.09M-node cube, time-varying monitor rebuilt every step, fixed "
@@ -69,6 +79,67 @@ def parse():
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+T_START = time.time()
+_PHASE = {"name": "start"}
+
+
+def phase(name):
+    """One stderr progress line per rank per phase, also appended to $MMX_BENCH_PROGRESS/rank<r> when
+    bench.py re-launched itself (so that the parent can name a rank that never got past a phase)."""
+    rank = os.environ.get("RANK", "0")
+    _PHASE["name"] = name
+    log("rank %s/%s: phase %s (+%.1f s)" % (rank, os.environ.get("WORLD_SIZE", "1"), name, time.time() - T_START))
+    d = os.environ.get("MMX_BENCH_PROGRESS")
+    if d:
+        try:
+            with open(os.path.join(d, "rank%s" % rank), "a") as f:
+                f.write(name + "\n")
+        except OSError:
+            pass
+
+
+def start_watchdog(budget_s, rank):
+    """A rank that is still running after budget_s seconds (a peer that never joined, a collective
+    that never completed) prints its phase and exits with status 124 -- the launcher then ends the
+    other ranks.  os._exit: no interpreter shutdown, which could itself wait on the stuck call."""
+    import threading
+
+    def run():
+        if threading.Event().wait(budget_s):
+            return
+        log("rank %d: wall-clock budget of %.0f s exceeded in phase '%s' -- a peer rank missing or stuck? "
+            "exiting with status 124" % (rank, budget_s, _PHASE["name"]))
+        os._exit(124)
+
+    threading.Thread(target=run, name="bench-watchdog", daemon=True).start()
+
+
+def rank_phases(progress_dir, n):
+    """the phases each rank reported (rank -> list)"""
+    out = {}
+    for r in range(n):
+        try:
+            with open(os.path.join(progress_dir, "rank%d" % r)) as f:
+                out[r] = [ln.strip() for ln in f if ln.strip()]
+        except OSError:
+            out[r] = []
+    return out
+
+
+def report_ranks(progress_dir, n):
+    """stderr: the ranks that never finished set-up, with their last phase; returns that list"""
+    ph = rank_phases(progress_dir, n)
+    missing = [r for r in range(n) if "setup" not in ph[r]]
+    absent = [r for r in range(n) if "rendezvous" not in ph[r]]
+    for r in range(n):
+        log("rank %d: last phase %s" % (r, ph[r][-1] if ph[r] else "none (never started)"))
+    if absent:
+        log("ranks that never reached the rendezvous: %s" % ", ".join(str(r) for r in absent))
+    if missing:
+        log("ranks that printed no 'setup' line: %s" % ", ".join(str(r) for r in missing))
+    return missing
 
 
 def launch_plan(gpus, env, n_visible, share=False):
@@ -123,14 +194,71 @@ def free_port():
         return s.getsockname()[1]
 
 
-def relaunch(n):
+def relaunch(n, budget_s=None):
     """N ranks under torch.distributed.run (127.0.0.1 rendezvous); this process only waits for them
-    and exits with their status (a child process, not an exec)."""
+    and exits with their status (a child process, not an exec).  With a budget the launcher runs in
+    its own process group; past budget_s + 60 s the group is killed (SIGTERM, then SIGKILL) and the
+    call returns 124.  On any failure the ranks' last phases are printed and the ranks that never
+    finished set-up are named."""
+    import shutil
+    import signal
     import subprocess
+    import tempfile
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
            "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
     log("re-launching %d ranks:" % n, " ".join(cmd))
-    return subprocess.run(cmd).returncode
+    if budget_s is None:
+        return subprocess.run(cmd).returncode
+    prog = tempfile.mkdtemp(prefix="mmx_bench_progress_")
+    try:
+        p = subprocess.Popen(cmd, env=dict(os.environ, MMX_BENCH_PROGRESS=prog), start_new_session=True)
+        try:
+            rc = p.wait(timeout=budget_s + 60.0)
+        except subprocess.TimeoutExpired:
+            log("the %d-rank job exceeded its budget of %.0f s (+60 s): killing its process group" % (n, budget_s))
+            report_ranks(prog, n)
+            for sig, grace in ((signal.SIGTERM, 15.0), (signal.SIGKILL, 15.0)):
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    break
+                try:
+                    p.wait(timeout=grace)
+                    break
+                except subprocess.TimeoutExpired:
+                    continue
+            return 124
+        if rc != 0:
+            log("the %d-rank job failed with status %d" % (n, rc))
+            report_ranks(prog, n)
+        return rc
+    finally:
+        shutil.rmtree(prog, ignore_errors=True)
+
+
+def rendezvous_only(world, budget_s):
+    """--rendezvous-only: the N-rank launch and its failure handling without a GPU -- each rank
+    reports its phases, meets the others over gloo (bounded by the budget) and exits.
+    MMX_BENCH_TEST_STALL_RANK=r makes rank r stall before the rendezvous (test hook)."""
+    import datetime
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        start_watchdog(budget_s, rank)
+    phase("start")
+    stall = os.environ.get("MMX_BENCH_TEST_STALL_RANK")
+    if stall is not None and int(stall) == rank:
+        log("rank %d: stalling before the rendezvous (MMX_BENCH_TEST_STALL_RANK)" % rank)
+        time.sleep(10 * budget_s + 600)
+    import torch.distributed as dist
+    phase("rendezvous")
+    if world > 1:
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(budget_s, 1.0)))
+        dist.barrier()
+    phase("setup")
+    if world > 1:
+        dist.destroy_process_group()
+    phase("done")
+    return 0
 
 
 def spmv_bench(torch, la, mx, with_cpu):
@@ -653,24 +781,34 @@ def pmc_flops(kernel):
 def main():
     args = parse()
     # before anything touches the GPU: a --gpus N run is N ranks, or it fails
-    plan, val = launch_plan(args.gpus, os.environ, visible_gpus, share=args.comm == "host")
+    share = args.comm == "host" or args.rendezvous_only
+    plan, val = launch_plan(args.gpus, os.environ, visible_gpus, share=share)
     if plan == "error":
         log(val)
         sys.exit(2)
     if plan == "spawn":
-        sys.exit(relaunch(val))
+        sys.exit(relaunch(val, args.budget_s))
     world = val
+    if args.rendezvous_only:
+        sys.exit(rendezvous_only(world, args.budget_s))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        start_watchdog(args.budget_s, rank)
+        phase("start")
+    import datetime
+
     import torch  # first, so libmmadmm binds to the same HIP runtime
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     host_comm = world > 1 and args.comm == "host"
     if host_comm:  # rehearsal: ranks may share the visible GPUs
         local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("gloo" if host_comm else "nccl")
+        phase("rendezvous")
+        dist.init_process_group("gloo" if host_comm else "nccl",
+                                timeout=datetime.timedelta(seconds=max(args.budget_s, 60.0)))
     import mmadmm_amd as mx
     import lasolver_amd as la
 
@@ -701,30 +839,39 @@ def main():
         m = mx.MeshData.hexdisc(n, 0.5, 0.5, 0.5)
         return m, mx.Mesh(m.Xp, m.F, m.mask, mx.BuiltinMonitor(2, 1), rho=50.0, tau=0.5, device=local)
 
+    if world > 1:
+        phase("mesh")
     mesh, M = make_mesh(world)
     t_setup = time.perf_counter()
     parallelism = parallelism_label(world, args.comm)
     comm = None
-    rccl_nranks = None
+    rccl_nranks = comm_nranks = None
     if world > 1:
         # the element-partitioned engine or nothing: a failure here ends the run with a non-zero
         # exit status (no silent fallback to replicas)
+        phase("communicator")
         if host_comm:
             comm = mx.Comm.host(world, rank, mx.TorchDistTransport())
         else:
             uid = [mx.Comm.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            comm = mx.Comm.rccl(world, rank, uid[0], local)
+            comm = mx.Comm.rccl(world, rank, uid[0], local, timeout_s=args.comm_timeout)
+        phase("engine")
         eng = mx.Engine(M, dt, rank=rank, nranks=world, comm=comm)
-        rccl_nranks = comm.nranks()  # ncclCommCount (host transport: the ranks it was made with)
-        if rccl_nranks != world:
-            raise RuntimeError("communicator has %d ranks, expected %d" % (rccl_nranks, world))
+        # ncclCommCount for RCCL; the host transport only knows the count it was made with
+        comm_nranks = comm.nranks()
+        rccl_nranks = None if host_comm else comm_nranks
+        if comm_nranks != world:
+            raise RuntimeError("communicator has %d ranks, expected %d" % (comm_nranks, world))
     else:
         eng = mx.Engine(M, dt)
     if c5:
         eng.set_regrid(True)  # the monitor grid rebuilt on the device at every step start
     t_setup = time.perf_counter() - t_setup
     log(f"rank {rank}: setup {t_setup:.1f}s, local nodes {eng.nP}, local simplices {eng.nF}")
+    if world > 1:
+        phase("setup")
+        phase("warmup")
 
     first_ms = None
     for w in range(max(args.warmup, 1)):
@@ -739,6 +886,8 @@ def main():
         if world > 1:
             dist.barrier()
 
+    if world > 1:
+        phase("timed")
     barrier()
     torch.cuda.synchronize()
     eng.sync()
@@ -754,6 +903,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if world > 1:
+        phase("report")
     st = eng.stats()
     per_rank = [(eng.nP, eng.nF)]
     if world > 1:
@@ -805,6 +956,7 @@ def main():
                    "global_nodes": mesh.nP, "global_simplices": mesh.nF, "nodes_rank0": eng.nP,
                    "simplices_rank0": eng.nF, "nodes_per_rank": [p[0] for p in per_rank],
                    "simplices_per_rank": [p[1] for p in per_rank], "rccl_nranks": rccl_nranks,
+                   "comm_nranks": (comm_nranks if world > 1 else None),
                    "admm_iter": args.admm_iter, "parallelism": parallelism,
                    "comm": (args.comm if world > 1 else None),
                    "value_unit_note": "ADMM it/s x global nodes / %d" % base_nodes},
@@ -900,6 +1052,7 @@ def main():
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+        phase("done")
 
 
 if __name__ == "__main__":

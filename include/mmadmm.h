@@ -103,6 +103,15 @@ typedef struct mmadmm_stats {
   long long regrid_fallbacks;  /* element partition: rebuilds that fell back to all-gathering every vertex */
   int monitor_iso;             /* 1: the monitor grid is isotropic (every point a multiple of the identity,
                                   bit for bit) and kept as one value per point; MMX_ISO=0 disables it */
+  /* element partition (round 6): the halo exchange of an ADMM iteration (pack + send/recv, device
+   * time on its stream, timing on), the bytes this rank sends / receives per exchange, and the
+   * nodes whose x-update runs while the exchange is in flight (no slot of another rank) */
+  double t_exchange_ms;
+  long long n_exchange;
+  double halo_send_bytes;
+  double halo_recv_bytes;
+  int interior_nodes;
+  int overlap;                 /* 1: the interior x-update overlaps the exchange (MMX_OVERLAP=0: serial) */
 } mmadmm_stats;
 
 /* Time-varying monitors (the reference's Mesh<D>::setUp hook, commented out at
@@ -228,9 +237,21 @@ int mmadmm_debug_blockgrad(mmadmm_handle h, int s, const double* z, const double
 #define MMADMM_UNIQUE_ID_BYTES 128
 typedef struct mmadmm_comm_s* mmadmm_comm;
 typedef struct mmadmm_plan_s* mmadmm_plan;
+/* The layout word of the host code (kernels/layout.h: every compile-time switch that changes a buffer
+ * shared by host and kernels) into *host_word; MMADMM_ERR_INVALID when a kernel object of this
+ * library was built with another (mmadmm_create*, mmx_matrix_create* check the same, first). */
+int mmadmm_layout_check(unsigned* host_word);
 /* RCCL: rank 0 makes the id, every rank creates its communicator with it (collective) */
 int mmadmm_comm_unique_id(void* out, int len);
 int mmadmm_comm_create_rccl(int nranks, int rank, const void* uid, int device, mmadmm_comm* out);
+/* the same with an explicit deadline (seconds; <= 0: none).  The communicator is non-blocking: its
+ * creation, every RCCL call that reports ncclInProgress and every stream wait of a partitioned
+ * step are bounded by the deadline, after which the communicator is aborted (ncclCommAbort) and the
+ * call returns MMADMM_ERR_RCCL naming the rank and the call -- a missing or stuck peer ends the run,
+ * never hangs it.  mmadmm_comm_create_rccl takes MMX_COMM_TIMEOUT_S from the environment (default
+ * 300 s). */
+int mmadmm_comm_create_rccl_timeout(int nranks, int rank, const void* uid, int device, double timeout_s,
+                                    mmadmm_comm* out);
 /* one communicator shared by nranks engines driven from threads of one process (tests) */
 int mmadmm_comm_create_loopback(int nranks, mmadmm_comm* out);
 /* transfers done by the caller's host transport (one process per rank, e.g. torch.distributed over

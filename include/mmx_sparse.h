@@ -142,6 +142,12 @@ int mmx_factor_schedule_info(int n, const int32_t* ia, const int32_t* ja, int le
  * 8 B per lane (plain / nontemporal), 8 reads a random 24-B record per lane; each touches 8 n bytes
  * (8: n/3 records). */
 int mmx_stream_copy(int device, const double* d_src, double* d_dst, long long n, int reps, int variant, double* ms);
+/* test hook: a kernel of `blocks` workgroups (1024 lanes, 64 KB LDS each) on a stream of its own
+ * that holds their CUs for ms milliseconds (asynchronous; mmx_occupy_wait waits for it).  The
+ * solver's kernels must complete beside it (the wave factor takes rows by ticket: no co-residency
+ * assumed; tests/test_gpu_lasolver.py). */
+int mmx_occupy(int device, int blocks, double ms);
+int mmx_occupy_wait(void);
 
 #ifdef __cplusplus
 }

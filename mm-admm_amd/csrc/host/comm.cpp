@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 
+#include "comm_poll.h"
 #include "common.h"
 
 namespace mmx {
@@ -19,37 +20,116 @@ namespace {
       throw ::mmx::Error(MMADMM_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));      \
   } while (0)
 
+// RCCL over xGMI, one process per GPU.  The communicator is non-blocking (config.blocking = 0):
+// its creation and every call that reports ncclInProgress are polled against a deadline
+// (comm_poll.h), and so is every stream wait of a partitioned step (wait()), so a rank that never
+// joins or stops half-way ends the job with MMADMM_ERR_RCCL and a message naming the call, after
+// ncclCommAbort -- not with a hang.
 struct RcclComm final : Comm {
   ncclComm_t comm = nullptr;
-  RcclComm(int n, int rank, const void* uid, int device) {
+  int rank = 0;
+  double timeout = 300.0;
+  hipEvent_t ev = nullptr;
+  RcclComm(int n, int r, const void* uid, int device, double timeout_s) {
     nranks = n;
+    rank = r;
+    timeout = timeout_s;
     MMX_HIP(hipSetDevice(device));
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
-    MMX_NCCL(ncclCommInitRank(&comm, n, id, rank));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r0 = ncclCommInitRankConfig(&comm, n, id, r, &cfg);
+    check(r0, "ncclCommInitRankConfig (every rank must create its communicator)");
   }
   ~RcclComm() override {
-    if (comm) (void)ncclCommDestroy(comm);
+    if (ev) (void)hipEventDestroy(ev);
+    if (!comm) return;
+    // flush, then destroy; a peer that is gone makes the flush time out: abort instead
+    ncclResult_t a = ncclCommFinalize(comm);
+    if (a == ncclInProgress) a = settle_state();
+    if (a == ncclSuccess)
+      (void)ncclCommDestroy(comm);
+    else
+      (void)ncclCommAbort(comm);
+  }
+  // ncclCommGetAsyncError polled until it leaves ncclInProgress (or the deadline passes:
+  // ncclInProgress is returned)
+  ncclResult_t settle_state() {
+    ncclResult_t last = ncclInProgress;
+    const int pr = poll_bounded(
+        [&] {
+          ncclResult_t a = ncclInProgress;
+          if (ncclCommGetAsyncError(comm, &a) != ncclSuccess) a = ncclInternalError;
+          last = a;
+          return a == ncclInProgress ? kPollBusy : a == ncclSuccess ? kPollReady : kPollFailed;
+        },
+        timeout, steady_seconds, short_sleep);
+    return pr == kPollTimeout ? ncclInProgress : last;
+  }
+  [[noreturn]] void fail(const std::string& msg) {
+    if (comm) (void)ncclCommAbort(comm);
+    comm = nullptr;
+    throw Error(MMADMM_ERR_RCCL, "rank " + std::to_string(rank) + " of " + std::to_string(nranks) + ": " + msg);
+  }
+  void check(ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) r = settle_state();
+    if (r == ncclInProgress)
+      fail(std::string(what) + ": not complete after " + std::to_string(timeout) +
+           " s (MMX_COMM_TIMEOUT_S) -- a peer rank is missing or stuck; communicator aborted");
+    if (r != ncclSuccess) fail(std::string(what) + ": " + ncclGetErrorString(r));
+  }
+  void live(const char* what) {
+    if (!comm) throw Error(MMADMM_ERR_RCCL, std::string(what) + ": the communicator was aborted by an earlier failure");
   }
   int transport_ranks() override {
+    live("ncclCommCount");
     int n = 0;
-    MMX_NCCL(ncclCommCount(comm, &n));
+    check(ncclCommCount(comm, &n), "ncclCommCount");
     return n;
   }
   void allgather(int, const double* dsend, double* drecv, size_t count, hipStream_t st) override {
-    MMX_NCCL(ncclAllGather(dsend, drecv, count, ncclDouble, comm, st));
+    live("ncclAllGather");
+    check(ncclAllGather(dsend, drecv, count, ncclDouble, comm, st), "ncclAllGather");
   }
   void exchange(int, const double* dsend, double* drecv, const std::vector<HaloPeer>& peers, int rowLen,
                 hipStream_t st) override {
     if (peers.empty()) return;
-    MMX_NCCL(ncclGroupStart());
+    live("halo exchange");
+    check(ncclGroupStart(), "ncclGroupStart");
     for (const HaloPeer& p : peers) {
       if (p.sendCount)
-        MMX_NCCL(ncclSend(dsend + (size_t)p.sendOff * rowLen, (size_t)p.sendCount * rowLen, ncclDouble, p.rank, comm, st));
+        check(ncclSend(dsend + (size_t)p.sendOff * rowLen, (size_t)p.sendCount * rowLen, ncclDouble, p.rank, comm, st),
+              "ncclSend");
       if (p.recvCount)
-        MMX_NCCL(ncclRecv(drecv + (size_t)p.recvOff * rowLen, (size_t)p.recvCount * rowLen, ncclDouble, p.rank, comm, st));
+        check(ncclRecv(drecv + (size_t)p.recvOff * rowLen, (size_t)p.recvCount * rowLen, ncclDouble, p.rank, comm, st),
+              "ncclRecv");
     }
-    MMX_NCCL(ncclGroupEnd());
+    check(ncclGroupEnd(), "ncclGroupEnd (halo send/recv)");
+  }
+  // the stream's work so far has completed, or the deadline passed (a peer's matching send/recv
+  // never came) -- then the communicator is aborted, which also ends its kernels
+  void wait(hipStream_t st) override {
+    live("stream wait");
+    if (!ev) MMX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    MMX_HIP(hipEventRecord(ev, st));
+    hipError_t herr = hipSuccess;
+    ncclResult_t nerr = ncclSuccess;
+    const int pr = poll_bounded(
+        [&] {
+          herr = hipEventQuery(ev);
+          if (herr == hipSuccess) return kPollReady;
+          if (herr != hipErrorNotReady) return kPollFailed;
+          if (ncclCommGetAsyncError(comm, &nerr) == ncclSuccess && nerr != ncclSuccess && nerr != ncclInProgress)
+            return kPollFailed;
+          return kPollBusy;
+        },
+        timeout, steady_seconds, short_sleep, 20000);
+    if (pr == kPollTimeout)
+      fail("the partitioned step's stream did not complete within " + std::to_string(timeout) +
+           " s (MMX_COMM_TIMEOUT_S) -- a peer rank is missing or stuck; communicator aborted");
+    if (herr != hipSuccess && herr != hipErrorNotReady) MMX_HIP(herr);
+    if (pr == kPollError) fail(std::string("asynchronous RCCL error: ") + ncclGetErrorString(nerr));
   }
 };
 
@@ -182,8 +262,10 @@ struct HostComm final : Comm {
 
 }  // namespace
 
-Comm* make_rccl_comm(int nranks, int rank, const void* uid, int device) {
-  return new RcclComm(nranks, rank, uid, device);
+void Comm::throw_hip(hipError_t e) { throw Error(MMADMM_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e)); }
+
+Comm* make_rccl_comm(int nranks, int rank, const void* uid, int device, double timeout_s) {
+  return new RcclComm(nranks, rank, uid, device, timeout_s);
 }
 Comm* make_loopback_comm(int nranks) { return new LoopbackComm(nranks); }
 void rccl_unique_id(void* out128) {
@@ -208,13 +290,18 @@ int mmadmm_comm_unique_id(void* out, int len) {
 }
 
 int mmadmm_comm_create_rccl(int nranks, int rank, const void* uid, int device, mmadmm_comm* out) {
+  return mmadmm_comm_create_rccl_timeout(nranks, rank, uid, device, mmx::comm_timeout_default(), out);
+}
+
+int mmadmm_comm_create_rccl_timeout(int nranks, int rank, const void* uid, int device, double timeout_s,
+                                    mmadmm_comm* out) {
   return mmx::guarded([&] {
     if (!out || !uid || nranks < 1 || rank < 0 || rank >= nranks)
       throw mmx::Error(MMADMM_ERR_INVALID, "mmadmm_comm_create_rccl: bad arguments");
     *out = nullptr;
     auto* h = new mmadmm_comm_s{nullptr};
     try {
-      h->c = mmx::make_rccl_comm(nranks, rank, uid, device);
+      h->c = mmx::make_rccl_comm(nranks, rank, uid, device, timeout_s);
     } catch (...) {
       delete h;
       throw;

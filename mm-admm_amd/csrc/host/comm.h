@@ -27,9 +27,17 @@ struct Comm {
   // pointers, stream-ordered)
   virtual void exchange(int rank, const double* dsend, double* drecv, const std::vector<HaloPeer>& peers, int rowLen,
                         hipStream_t st) = 0;
+  // the stream's work so far has completed (RCCL: bounded by the communicator's deadline, then
+  // MMADMM_ERR_RCCL after an abort -- comm_poll.h; the host transports complete their transfers
+  // inside the calls above)
+  virtual void wait(hipStream_t st) {
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) throw_hip(e);
+  }
+  static void throw_hip(hipError_t e);
 };
 
-Comm* make_rccl_comm(int nranks, int rank, const void* uid, int device);
+Comm* make_rccl_comm(int nranks, int rank, const void* uid, int device, double timeout_s);
 Comm* make_loopback_comm(int nranks);
 void rccl_unique_id(void* out128);
 

@@ -16,6 +16,9 @@ struct Error : std::runtime_error {
 };
 
 void set_last_error(const std::string& msg);
+// every kernel object's layout word equals the calling host TU's (kernels/layout.h kLayoutWord as
+// that TU was compiled), else MMADMM_ERR_INVALID
+void check_kernel_layout(unsigned hostWord);
 
 #define MMX_HIP(expr)                                                                        \
   do {                                                                                      \

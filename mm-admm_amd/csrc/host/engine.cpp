@@ -94,6 +94,11 @@ class Engine final : public EngineBase {
     if (nranks_ > 1 && !comm_) throw Error(MMADMM_ERR_INVALID, "partitioned engine needs a communicator");
     if (p.device >= 0) MMX_HIP(hipSetDevice(p.device));
     MMX_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    if (nranks_ > 1) {  // the halo exchange's stream (overlapped with the interior x-update)
+      MMX_HIP(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+      MMX_HIP(hipEventCreateWithFlags(&evProx_, hipEventDisableTiming));
+      MMX_HIP(hipEventCreateWithFlags(&evEx_, hipEventDisableTiming));
+    }
     compMesh_ = (Xc != nullptr);
     std::vector<double> Vp(Xp, Xp + (size_t)nP * D);
     Fh_.assign(F, F + (size_t)nF * (D + 1));
@@ -149,7 +154,7 @@ class Engine final : public EngineBase {
       ownAllGid_.upload(all.data(), all.size(), st_);
       ownAllGidH_ = all;
       ownLocal_.upload(mine.data(), std::max<size_t>(mine.size(), 1), st_);
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
     }
     const int nl = nP_;
     // t = M + dt^2 WD_T W D is block diagonal: t_vv = tau + dt^2 * (w*w summed valence times)
@@ -192,7 +197,9 @@ class Engine final : public EngineBase {
       const char* sp = getenv("MMX_SPIN");
       spinWait_ = !(sp && atoi(sp) == 0);
       const char* zx = getenv("MMX_ZX");  // 0: the step's z = D x by k_gather_z (DeviceMesh::zx)
-      zFromX_ = D == 2 && nranks_ == 1 && !(zx && atoi(zx) == 0);
+      zFromX_ = D == 2 && !(zx && atoi(zx) == 0);  // partitions too: the first pack reads zx (PackZX)
+      const char* ov = getenv("MMX_OVERLAP");  // 0: the halo exchange before the whole x-update
+      overlap_ = nranks_ > 1 && !(ov && atoi(ov) == 0);
       const char* fp = getenv("MMX_FUSE_PRED");  // 0: k_predict runs in every step (DeviceMesh::predBar)
       fusePred_ = !(fp && atoi(fp) == 0);
       if (tslotOn_) tslot_.alloc(std::max<size_t>((size_t)nF_ * K, 1));
@@ -206,24 +213,39 @@ class Engine final : public EngineBase {
           if (plan_.incSrc[t] >= 0) k = std::min<long long>(k, plan_.incSrc[t] / K);
         key[v] = k;
       }
-      std::vector<int32_t> ord(nl);
-      for (int v = 0; v < nl; ++v) ord[v] = v;
-      const char* xo = getenv("MMX_XUP_ORDER");  // 3D default: y slabs (C4 x-update 0.174 -> 0.152 ms with the sweep)
-      if (xo ? atoi(xo) == 1 : D == 3) {
-        // eight slabs across the y axis (2D: opt-in), one per XCD group of the node order (the x-update's
-        // XCD-contiguous blocks), each by first incident simplex: an XCD's share of every z
-        // layer is one slab, so its live slot terms are an eighth of a layer
-        const int n8 = ((nl + 255) / 256 + 7) / 8 * 256;
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return Vl[(size_t)a * D + 1] < Vl[(size_t)b * D + 1]; });
-        for (int c = 0; c < 8; ++c) {
-          const int lo = std::min(nl, c * n8), hi = std::min(nl, (c + 1) * n8);
-          std::stable_sort(ord.begin() + lo, ord.begin() + hi, [&](int a, int b) { return key[a] < key[b]; });
-        }
-      } else {
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key[a] < key[b]; });
+      // an element partition orders its interior nodes (no slot of another rank) first: their
+      // x-update runs while the halo exchange is in flight (overlap_), the rest after it
+      std::vector<int32_t> inner, bound;
+      for (int v = 0; v < nl; ++v) {
+        bool remote = false;
+        for (int t = plan_.incPtr[v]; t < plan_.incPtr[v + 1]; ++t) remote |= plan_.incSrc[t] < 0;
+        (remote && overlap_ ? bound : inner).push_back(v);
       }
+      nInner_ = (int)inner.size();
+      const char* xo = getenv("MMX_XUP_ORDER");  // 3D default: y slabs (C4 x-update 0.174 -> 0.152 ms with the sweep)
+      const bool slabs = xo ? atoi(xo) == 1 : D == 3;
+      auto order = [&](std::vector<int32_t>& ord) {
+        const int n = (int)ord.size();
+        if (slabs) {
+          // eight slabs across the y axis (2D: opt-in), one per XCD group of the node order (the x-update's
+          // XCD-contiguous blocks), each by first incident simplex: an XCD's share of every z
+          // layer is one slab, so its live slot terms are an eighth of a layer
+          const int n8 = ((n + 255) / 256 + 7) / 8 * 256;
+          std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return Vl[(size_t)a * D + 1] < Vl[(size_t)b * D + 1]; });
+          for (int c = 0; c < 8; ++c) {
+            const int lo = std::min(n, c * n8), hi = std::min(n, (c + 1) * n8);
+            std::stable_sort(ord.begin() + lo, ord.begin() + hi, [&](int a, int b) { return key[a] < key[b]; });
+          }
+        } else {
+          std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key[a] < key[b]; });
+        }
+      };
+      order(inner);
+      order(bound);
+      std::vector<int32_t> ord(inner);
+      ord.insert(ord.end(), bound.begin(), bound.end());
       nodeOrder_.upload(ord.data(), std::max<size_t>(ord.size(), 1), st_);
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
     }
     invdiag_.upload(invdiag.data(), invdiag.size(), st_);
     if (compMesh_) Vc_.upload(Vcl.data(), Vcl.size(), st_);
@@ -266,7 +288,7 @@ class Engine final : public EngineBase {
     }
     // prox workgroups take 16 (3D quad) to 256 simplices; node kernels pad their grid to a multiple of 8 (XCD map)
     // (k_prox_quad: 16 tets per workgroup)
-    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 15) / 16, (nP_ + 255) / 256 + 8));
+    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 15) / 16, (nP_ + 255) / 256 + 16));
     maxBlocks_ = maxBlocks;
     partA_.alloc(maxBlocks * kNumPartials);
     partB_.alloc(maxBlocks * kNumPartials);
@@ -276,7 +298,7 @@ class Engine final : public EngineBase {
     ensureResults(64);
     m_ = makeView();
     launch_gather_z<D>(m_, x_.p, z_.p, st_);  // z = D x
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     MMX_HIP(hipGetLastError());
   }
 
@@ -287,6 +309,9 @@ class Engine final : public EngineBase {
     for (auto& e : evPool_) (void)hipEventDestroy(e);
     if (evSync_) (void)hipEventDestroy(evSync_);
     if (resH_) (void)hipHostFree(resH_);
+    if (evProx_) (void)hipEventDestroy(evProx_);
+    if (evEx_) (void)hipEventDestroy(evEx_);
+    if (st2_) (void)hipStreamDestroy(st2_);
     if (st_) (void)hipStreamDestroy(st_);
   }
 
@@ -329,12 +354,20 @@ class Engine final : public EngineBase {
     if (!zFromX) m_.zx = nullptr;
     StepScalars sc{prm_.tau, prm_.dt * prm_.dt, w_, dtOverTau};
     int nbx = 0, nbp = 0;
-    exchange(0);
     if (fusePred) {
       m_.predPrev = xPrev_.p;
       m_.predBar = xBar_.p;
     }
-    launch_xupdate<D>(m_, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p, &nbx, false, st_);
+    PackZX pz;  // a partition's first pack: z = D zx (predicted: 2 x - xPrev) for the exported slots
+    if (zFromX) {
+      pz.F = F_.p;
+      pz.zx = zsrc;
+      if (fusePred) {
+        pz.x = x_.p;
+        pz.xPrev = xPrev_.p;
+      }
+    }
+    xupdateHalo(sc, &nbx, false, false, pz);
     m_.predPrev = m_.predBar = nullptr;
     const bool early = tol >= 0;
     int done = 0;
@@ -368,11 +401,10 @@ class Engine final : public EngineBase {
       }
       hessComputed_ = true;
       stepTaken_ = true;
-      exchange(0);
       // the primal residual ||D x - z|| (src/MeshIntegrator.cpp:162) only feeds the early-exit test
       // and the reported last residual: without the early exit it is formed on the last iteration
       const bool resid = early || i == nIters - 1;
-      launch_xupdate<D>(m_, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p, &nbx, resid, st_, true);
+      xupdateHalo(sc, &nbx, resid, true, PackZX{});
       if (timing) {
         b1 = nextEvent();
         MMX_HIP(hipEventRecord(b1, st_));
@@ -494,7 +526,7 @@ class Engine final : public EngineBase {
         buildJacobian(dtBE);
         beStepTaken_ = true;
       }
-      MMX_HIP(hipStreamSynchronize(st_));  // rhs and the Jacobian values are ready for the solver stream
+      streamWait();  // rhs and the Jacobian values are ready for the solver stream
       const auto tSolve = Clock::now();
       MMX_SP(mmx_matrix_set_rhs_device(jac_, rhs_.p));
       int cgIter = 0;
@@ -508,7 +540,7 @@ class Engine final : public EngineBase {
       nIter++;
       normPrev = norm;
     } while (nIter < MAX_ITERS);
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     st_stats_.steps += 1;
     st_stats_.newton_iters += nIter;
     st_stats_.t_be_ms += msSince(tStep);
@@ -545,7 +577,7 @@ class Engine final : public EngineBase {
       if (rv[4] > 0) throwBad("in backward Euler");
       std::vector<double> r((size_t)n);
       MMX_HIP(hipMemcpyAsync(r.data(), rhs_.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
       for (int i = 0; i < n; ++i) out[i] = -r[i];  // rhs = -F on the device: the negation is exact
       if (sc) {
         sc[0] = rv[0];
@@ -559,11 +591,11 @@ class Engine final : public EngineBase {
       if (jraw_.n != jja_.n) jraw_.alloc(std::max<size_t>(jja_.n, 1));
       launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, 1.0, jraw_.p, st_, false);
       MMX_HIP(hipMemcpyAsync(out, jraw_.p, jja_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
     } else if (op == 3) {
       MMX_HIP(hipMemcpyAsync(dx_.p, in, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st_));
       launch_add_inplace(n, x_.p, dx_.p, st_);
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
     } else {
       throw Error(MMADMM_ERR_INVALID, "newtonOp: unknown op");
     }
@@ -575,7 +607,7 @@ class Engine final : public EngineBase {
     if (ia) MMX_HIP(hipMemcpyAsync(ia, jia_.p, jia_.n * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
     if (ja) MMX_HIP(hipMemcpyAsync(ja, jja_.p, jja_.n * sizeof(int32_t), hipMemcpyDeviceToHost, st_));
     if (a) MMX_HIP(hipMemcpyAsync(a, jval_.p, jval_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
   }
 
   // Mesh::computeEnergy on Vp (src/Mesh.cpp:496-530)
@@ -592,7 +624,7 @@ class Engine final : public EngineBase {
   void done() override {
     MMX_HIP(hipMemcpyAsync(Vp_.p, x_.p, (size_t)nP_ * D * sizeof(double), hipMemcpyDeviceToDevice, st_));
     vpVersion_++;
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
   }
 
   void get(const std::string& what, double* out) override {
@@ -606,7 +638,7 @@ class Engine final : public EngineBase {
       } else {  // de-interleave: slot i of simplex s at s 2K + (i / D) 2D + i % D (+ D for u)
         std::vector<double> h(z_.n);
         MMX_HIP(hipMemcpyAsync(h.data(), z_.p, z_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
-        MMX_HIP(hipStreamSynchronize(st_));
+        streamWait();
         const int sh = what == "u" ? D : 0;
         for (int s = 0; s < nF_; ++s)
           for (int i = 0; i < K; ++i) out[(size_t)s * K + i] = h[(size_t)s * 2 * K + (i / D) * 2 * D + i % D + sh];
@@ -619,7 +651,7 @@ class Engine final : public EngineBase {
     else if (what == "grid") {
       if (gridOnDevice_) {
         MMX_HIP(hipMemcpyAsync(out, gvals_.p, gvals_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
-        MMX_HIP(hipStreamSynchronize(st_));
+        streamWait();
       } else {
         std::memcpy(out, grid_.vals.data(), grid_.vals.size() * sizeof(double));
       }
@@ -633,13 +665,13 @@ class Engine final : public EngineBase {
     if (b == &B_) {  // wave-interleaved on the device: return simplex-major
       std::vector<double> h(b->n);
       MMX_HIP(hipMemcpyAsync(h.data(), b->p, b->n * sizeof(double), hipMemcpyDeviceToHost, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
       for (int s = 0; s < nF_; ++s)
         for (int ij = 0; ij < K * K; ++ij) out[(size_t)s * K * K + ij] = h[bIndex(s, ij)];
       return;
     }
     MMX_HIP(hipMemcpyAsync(out, b->p, b->n * sizeof(double), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
   }
 
   // host mirror of bidx<D> (admm_kernels.hip)
@@ -682,6 +714,10 @@ class Engine final : public EngineBase {
                     nP * 8.0 * D;
     s->xupdate_bytes = 4.0 * (nP + 1) + 4.0 * (D + 1) * nF + (16.0 - 8.0 * ts) * K * nF + 8.0 * D * nP * 2 + 8.0 * nP;
     s->monitor_iso = iso_ ? 1 : 0;
+    s->halo_send_bytes = 8.0 * D * (double)plan_.sendOff.size();
+    s->halo_recv_bytes = nranks_ > 1 ? 8.0 * D * (double)plan_.recvRows : 0.0;
+    s->interior_nodes = nInner_;
+    s->overlap = overlap_ ? 1 : 0;
   }
 
   void resetStats() override {
@@ -693,14 +729,21 @@ class Engine final : public EngineBase {
   // the timed steps' HIP events -> the timers (every step ends with a stream synchronisation, so
   // its events have completed); the pool is then reused
   void resolveTimed() {
-    if (stepEv_.empty() && timed_.empty()) return;
-    MMX_HIP(hipStreamSynchronize(st_));
+    if (stepEv_.empty() && timed_.empty() && exEv_.empty()) return;
+    streamWait();
     float ms = 0;
     for (auto& p : stepEv_) {
       MMX_HIP(hipEventElapsedTime(&ms, p.first, p.second));
       st_stats_.t_step_ms += ms;
       st_stats_.n_steps_timed += 1;
     }
+    if (st2_) MMX_HIP(hipStreamSynchronize(st2_));
+    for (auto& p : exEv_) {
+      MMX_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+      st_stats_.t_exchange_ms += ms;
+      st_stats_.n_exchange += 1;
+    }
+    exEv_.clear();
     for (auto& t : timed_) {
       MMX_HIP(hipEventElapsedTime(&ms, t.a0, t.a1));
       st_stats_.t_prox_ms += ms;
@@ -714,7 +757,7 @@ class Engine final : public EngineBase {
     evUsed_ = 0;
   }
 
-  void sync() override { MMX_HIP(hipStreamSynchronize(st_)); }
+  void sync() override { streamWait(); }
 
   void debugBlockGrad(int s, const double* z, const double* dx, int flags, double* out) override {
     if (s < 0 || s >= nF_) throw Error(MMADMM_ERR_INVALID, "debug_blockgrad: simplex out of range");
@@ -724,7 +767,7 @@ class Engine final : public EngineBase {
     dout.alloc(K + 2);
     launch_debug_blockgrad<D>(m_, s, dz.p, ddx.p, dout.p, flags, st_);
     MMX_HIP(hipMemcpyAsync(out, dout.p, (K + 2) * sizeof(double), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
   }
 
  private:
@@ -761,7 +804,7 @@ class Engine final : public EngineBase {
     xn_.alloc((size_t)n);
     rhs_.alloc((size_t)n);
     dx_.alloc((size_t)n);
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
   }
 
   // buildEulerJac (src/Mesh.cpp:1112-1136); sfac after the first build (src/Mesh.cpp:1287-1290).
@@ -777,13 +820,13 @@ class Engine final : public EngineBase {
     launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
     clearInvFlag();
     launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, dtBE / prm_.tau, jval_.p, st_);
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     MMX_SP(mmx_matrix_set_values_device(jac_, jval_.p));
     if (!jacFactored_) {
       MMX_SP(mmx_matrix_sfac(jac_, &jprm_));
       jacFactored_ = true;
     }
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     st_stats_.jacobians += 1;
     st_stats_.t_jac_ms += msSince(t0);
   }
@@ -802,10 +845,49 @@ class Engine final : public EngineBase {
 
   // halo exchange of interface-slot values with the neighbouring ranks: mode 0 x-update terms,
   // 1 simplex gradients
-  void exchange(int mode) {
+  void exchange(int mode, const PackZX& pz = {}, hipStream_t st = nullptr) {
     if (nranks_ == 1) return;
-    launch_pack_export<D>(mode, (int)plan_.sendOff.size(), expOff_.p, z_.p, uPtr(), gs_.p, w_, export_.p, st_);
-    comm_->exchange(rank_, export_.p, remote_.p, plan_.peers, D, st_);
+    if (!st) st = st_;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing_ && mode == 0) {
+      e0 = nextEvent();
+      MMX_HIP(hipEventRecord(e0, st));
+    }
+    launch_pack_export<D>(mode, (int)plan_.sendOff.size(), expOff_.p, z_.p, uPtr(), gs_.p, w_, export_.p, st, pz);
+    comm_->exchange(rank_, export_.p, remote_.p, plan_.peers, D, st);
+    if (e0) {
+      e1 = nextEvent();
+      MMX_HIP(hipEventRecord(e1, st));
+      exEv_.push_back({e0, e1});
+    }
+  }
+
+  // the x-update of every node with the halo exchange (mode 0) before it.  On an element partition
+  // (overlap_) the interior nodes -- no slot of another rank, first in the node order -- are updated
+  // on the step's stream while the pack and the send/recv run on a second stream; the interface
+  // nodes follow once the exchange is in.  Each node's sum is the same either way (ascending
+  // global simplex id), so the positions are bit-identical; only the residual partials come as two
+  // consecutive sets.  (src/MeshIntegrator.cpp:146-160: the consensus the exchange feeds.)
+  void xupdateHalo(const StepScalars& sc, int* nbx, bool resid, bool useTs, const PackZX& pz) {
+    if (!overlap_) {
+      exchange(0, pz);
+      launch_xupdate<D>(m_, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p, nbx, resid, st_, useTs);
+      return;
+    }
+    MMX_HIP(hipEventRecord(evProx_, st_));
+    DeviceMesh<D> mi = m_;
+    mi.xupHi = nInner_;
+    int nb1 = 0, nb2 = 0;
+    launch_xupdate<D>(mi, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p, &nb1, resid, st_, useTs);
+    MMX_HIP(hipStreamWaitEvent(st2_, evProx_, 0));
+    exchange(0, pz, st2_);
+    MMX_HIP(hipEventRecord(evEx_, st2_));
+    MMX_HIP(hipStreamWaitEvent(st_, evEx_, 0));
+    DeviceMesh<D> mb = m_;
+    mb.xupLo = nInner_;
+    launch_xupdate<D>(mb, sc, xBar_.p, z_.p, uPtr(), x_.p, partB_.p + (size_t)nb1 * kNumPartials, &nb2, resid, st_,
+                      useTs);
+    *nbx = nb1 + nb2;
   }
 
   // rows x 2*kNumPartials scalar records on the device -> combined over ranks on the host
@@ -814,7 +896,7 @@ class Engine final : public EngineBase {
   // blocking stream wait costs tens of microseconds per step), or the stream wait (MMX_SPIN=0)
   void waitStream() {
     if (!spinWait_) {
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
       return;
     }
     if (!evSync_) MMX_HIP(hipEventCreateWithFlags(&evSync_, hipEventDisableTiming));
@@ -822,6 +904,15 @@ class Engine final : public EngineBase {
     hipError_t r;
     while ((r = hipEventQuery(evSync_)) == hipErrorNotReady) __builtin_ia32_pause();
     MMX_HIP(r);
+  }
+
+  // hipStreamSynchronize, on an element partition bounded by the communicator's deadline (a peer
+  // that never sends its halo ends the step with MMADMM_ERR_RCCL, comm_poll.h)
+  void streamWait() {
+    if (nranks_ > 1 && comm_)
+      comm_->wait(st_);
+    else
+      MMX_HIP(hipStreamSynchronize(st_));
   }
 
   void fetchResults(const double* dev, int rows, std::vector<double>& out) {
@@ -834,14 +925,14 @@ class Engine final : public EngineBase {
     }
     if (nranks_ == 1) {
       MMX_HIP(hipMemcpyAsync(out.data(), dev, cnt * sizeof(double), hipMemcpyDeviceToHost, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
       return;
     }
     if (resAll_.n < cnt * nranks_) resAll_.alloc(cnt * nranks_);
     comm_->allgather(rank_, dev, resAll_.p, cnt, st_);
     std::vector<double> all(cnt * nranks_);
     MMX_HIP(hipMemcpyAsync(all.data(), resAll_.p, all.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     for (size_t i = 0; i < cnt; ++i) {
       const bool isMax = (i % kNumPartials) == 5;
       double v = all[i];
@@ -904,7 +995,7 @@ class Engine final : public EngineBase {
     MMX_HIP(hipMemcpyAsync(H0, rgnPart_.p, sizeof(double) * nbl * 2 * D, hipMemcpyDeviceToHost, st_));
     MMX_HIP(hipMemcpyAsync(H0 + (size_t)256 * 2 * D, rgnPart_.p + (size_t)256 * 2 * D, sizeof(double) * nbe * D,
                            hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int b = 0; b < nbl; ++b)
       for (int d = 0; d < D; ++d) {
@@ -921,7 +1012,7 @@ class Engine final : public EngineBase {
       MMX_HIP(hipMemcpyAsync(rgnSmallS_.p, in, sizeof(double) * n, hipMemcpyHostToDevice, st_));
       comm_->allgather(rank_, rgnSmallS_.p, rgnSmallR_.p, (size_t)n, st_);
       MMX_HIP(hipMemcpyAsync(hr, rgnSmallR_.p, sizeof(double) * n * nranks_, hipMemcpyDeviceToHost, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
     };
     for (int d = 0; d < D; ++d) {
       hs[d] = llo[d];
@@ -970,7 +1061,7 @@ class Engine final : public EngineBase {
                            rgnSend_.p, maxOwned_, st_);
     std::vector<int> cnt(nranks_ + 1);
     MMX_HIP(hipMemcpyAsync(cnt.data(), rgnCnt_.p, sizeof(int) * nranks_, hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     for (int q = 0; q < nranks_; ++q) hs[q] = (double)cnt[q];
     smallGather(hs, nranks_);
     std::vector<HaloPeer> peers;
@@ -1017,7 +1108,7 @@ class Engine final : public EngineBase {
                       grid_.ny, grid_.nz, rgnMon_.p, rgTmp_.p, H, st_, nc);
     int fail = 0;
     MMX_HIP(hipMemcpyAsync(&fail, rgnCnt_.p + nranks_, sizeof(int), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     hs[0] = (double)fail;
     smallGather(hs, 1);
     for (int q = 0; q < nranks_; ++q)
@@ -1052,7 +1143,7 @@ class Engine final : public EngineBase {
     launch_iso_compact<D>(gvals_.p, np, giso_.p, isoFlag_.p, st_);
     int notIso = 1;
     MMX_HIP(hipMemcpyAsync(&notIso, isoFlag_.p, sizeof(int), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     iso_ = (notIso == 0);
   }
   // the grid coordinates and, in 3D, each axis's cell table {g_i, h_i = g_{i+1} - g_i, RN(1/h_i), 0}
@@ -1142,7 +1233,7 @@ class Engine final : public EngineBase {
     } else {  // a host plugin: evaluated on the host at the current vertices, as the reference does
       std::vector<double> Xh((size_t)n * D), mv((size_t)n * DD);
       MMX_HIP(hipMemcpyAsync(Xh.data(), X, Xh.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
       for (int v = 0; v < n; ++v) {
         double M[9];
         for (int i = 0; i < DD; ++i) M[i] = 0.0;
@@ -1150,7 +1241,7 @@ class Engine final : public EngineBase {
         std::memcpy(&mv[(size_t)v * DD], M, DD * sizeof(double));
       }
       MMX_HIP(hipMemcpyAsync(mon, mv.data(), mv.size() * sizeof(double), hipMemcpyHostToDevice, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
     }
   }
   // smoothing passes over the box (shrinking halo) and the commit: the rows of R (NaN elsewhere)
@@ -1212,7 +1303,7 @@ class Engine final : public EngineBase {
       MMX_HIP(hipMemcpyAsync(rgHost_ + (size_t)512 * 2 * D, extPart, sizeof(double) * nbe * D, hipMemcpyDeviceToHost,
                              st_));
     }
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int b = 0; b < nb; ++b)
@@ -1262,7 +1353,7 @@ class Engine final : public EngineBase {
     } else {  // a host plugin: evaluated on the host at the current vertices, as the reference does
       std::vector<double> Xh((size_t)nG * D), mv((size_t)nG * DD);
       MMX_HIP(hipMemcpyAsync(Xh.data(), X, Xh.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
       for (int v = 0; v < nG; ++v) {
         double M[9];
         for (int i = 0; i < DD; ++i) M[i] = 0.0;
@@ -1270,7 +1361,7 @@ class Engine final : public EngineBase {
         std::memcpy(&mv[(size_t)v * DD], M, DD * sizeof(double));
       }
       MMX_HIP(hipMemcpyAsync(rgMon_.p, mv.data(), mv.size() * sizeof(double), hipMemcpyHostToDevice, st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
     }
     // the grid rows to rebuild: all of them on one rank; on an element partition the box of rows
     // this rank's monitor evaluations can reach (its vertices' bounding box, widened by two
@@ -1340,6 +1431,8 @@ class Engine final : public EngineBase {
     m.tieStale = tieCount_.p + (tiePar_ ^ 1);
     m.invFlag = tieCount_.p + 2;
     m.nodeOrder = nodeOrder_.p;
+    m.xupLo = 0;
+    m.xupHi = nP_;
     m.prox2dWave = wave2d_ ? 1 : 0;
     {
       const char* xs = getenv("MMX_XUP_SWEEP");  // 3D default: one workgroup per CU (profiles/r03/xupdate)
@@ -1418,10 +1511,10 @@ class Engine final : public EngineBase {
   [[noreturn]] void throwBad(const char* where) {
     unsigned flag = 0;
     MMX_HIP(hipMemcpyAsync(&flag, tieCount_.p + 2, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
-    MMX_HIP(hipStreamSynchronize(st_));
+    streamWait();
     if (flag) {
       MMX_HIP(hipMemsetAsync(tieCount_.p + 2, 0, sizeof(unsigned), st_));
-      MMX_HIP(hipStreamSynchronize(st_));
+      streamWait();
       throw Error(MMADMM_ERR_INVERTED, std::string("inverted element ") + where + " (reference: assert(Edet > 0))");
     }
     if (nranks_ > 1 && regridEachStep_)
@@ -1468,6 +1561,13 @@ class Engine final : public EngineBase {
   size_t rgScanBytes_ = 0;
   double* rgHost_ = nullptr;
   hipStream_t st_ = nullptr;
+  // element partition: the halo exchange's stream, its ordering events, the interior nodes' count
+  // (the first nInner_ positions of the node order), the exchange timers
+  hipStream_t st2_ = nullptr;
+  hipEvent_t evProx_ = nullptr, evEx_ = nullptr;
+  bool overlap_ = false;
+  int nInner_ = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> exEv_;
   DevBuf<int32_t> F_, incPtr_, incOff_;
   DevBuf<double> tslot_;
   bool tslotOn_ = false;
@@ -1565,6 +1665,7 @@ int mmadmm_create(int dim, int nP, const double* Xp, const double* Xc, int nF, c
     if (!(p->dt > 0) || !(p->tau > 0) || !(p->rho > 0))
       throw Error(MMADMM_ERR_INVALID, "mmadmm_create: dt, tau, rho must be positive");
     if (p->nranks > 1) throw Error(MMADMM_ERR_INVALID, "mmadmm_create: use mmadmm_create_partitioned for nranks > 1");
+    mmx::check_kernel_layout(mmx::kLayoutWord);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
       throw Error(MMADMM_ERR_HIP, "mmadmm_create: no HIP device (the engine has no CPU fallback)");
@@ -1597,6 +1698,7 @@ int mmadmm_create_partitioned(int dim, int nP, const double* Xp, const double* X
     mmx::Comm* c = mmx::comm_of(comm);
     if (p->nranks > 1 && (!c || c->nranks != p->nranks))
       throw Error(MMADMM_ERR_INVALID, "mmadmm_create_partitioned: communicator missing or of another size");
+    mmx::check_kernel_layout(mmx::kLayoutWord);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
       throw Error(MMADMM_ERR_HIP, "mmadmm_create_partitioned: no HIP device (the engine has no CPU fallback)");

@@ -612,7 +612,7 @@ struct SparseMatrix {
       launch_chain_factor(chfac.args, d_af.p, chfac.gU.p, fepoch, tickets(), errw(), st);
     } else if (facWave) {
       launch_ilu_factor_wave(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_dg.p, d_piv.p, d_jaf.p, d_toff.p, d_tgt.p, d_permw.p, n,
-                             d_af.p, d_flags.p, d_gF.n ? d_gF.p : nullptr, fepoch, errw(), st);
+                             d_af.p, d_flags.p, d_gF.n ? d_gF.p : nullptr, fepoch, tickets(), errw(), st);
     } else if (facLds)
       launch_ilu_factor_lds(d_ia.p, d_a.p, d_amap.p, d_iaf.p, d_jaf.p, d_dg.p, d_piv.p, d_toff.p, d_tgt.p, d_permf.p, nchf,
                             d_af.p, d_flags.p, fepoch, tickets(), errw(), st);
@@ -894,6 +894,7 @@ int mmx_struc_destroy(mmx_struc s) {
 
 int mmx_matrix_create(int device, int n, const int32_t* ia, const int32_t* ja, mmx_matrix* out) {
   return guarded([&] {
+    mmx::check_kernel_layout(mmx::kLayoutWord);
     if (!out || !ia || (n > 0 && !ja && ia[n] > 0)) throw Error(MMADMM_ERR_INVALID, "mmx_matrix_create: bad arguments");
     *out = nullptr;
     auto* h = new mmx_matrix_s;
@@ -909,6 +910,7 @@ int mmx_matrix_create(int device, int n, const int32_t* ia, const int32_t* ja, m
 
 int mmx_matrix_create_from_struc(int device, mmx_struc s, mmx_matrix* out) {
   return guarded([&] {
+    mmx::check_kernel_layout(mmx::kLayoutWord);
     if (!s || !out) throw Error(MMADMM_ERR_INVALID, "bad arguments");
     if (!s->s.packed) s->s.pack();
     *out = nullptr;
@@ -1218,6 +1220,29 @@ int mmx_stream_copy(int device, const double* d_src, double* d_dst, long long n,
     MMX_HIP(hipEventElapsedTime(&el, t.a, t.b));
     MMX_HIP(hipStreamDestroy(st));
     *ms = (double)el / reps;
+  });
+}
+
+// test hook: a kernel on a stream of its own that holds `blocks` workgroups' CUs for ms milliseconds
+// (asynchronous; mmx_occupy_wait joins it) -- e.g. the wave factor must complete beside it
+static hipStream_t g_occSt = nullptr;
+static mmx::DevBuf<double>* g_occSink = nullptr;
+int mmx_occupy(int device, int blocks, double ms) {
+  return guarded([&] {
+    if (blocks < 1 || blocks > 65536 || !(ms > 0) || ms > 10000) throw Error(MMADMM_ERR_INVALID, "mmx_occupy: bad arguments");
+    MMX_HIP(hipSetDevice(device));
+    if (!g_occSt) MMX_HIP(hipStreamCreateWithFlags(&g_occSt, hipStreamNonBlocking));
+    if (!g_occSink) {
+      g_occSink = new mmx::DevBuf<double>();
+      g_occSink->alloc(1024);
+    }
+    mmx::launch_occupy(blocks, ms, g_occSink->p, g_occSt);
+    MMX_HIP(hipGetLastError());
+  });
+}
+int mmx_occupy_wait(void) {
+  return guarded([&] {
+    if (g_occSt) MMX_HIP(hipStreamSynchronize(g_occSt));
   });
 }
 

@@ -3,18 +3,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "layout.h"
+
 namespace mmx {
 
 // Slot partial-sum record written by one workgroup; reduced in a fixed order.
 // v[0] = sum Ih (BFGS entry energies), v[1] = sum |z_new - z_old|^2, v[2] = sum |Dx - z|^2,
 // v[3] = BFGS iterations, v[4] = error flags (inverted element), v[5] = max BFGS iters.
-constexpr int kNumPartials = 6;
+constexpr int kNumPartials = kLayoutPartials;
 
-// 2D z / u layout: 1 = interleaved per vertex slot (admm_kernels.hip zu_*), 0 = two arrays (kept:
-// interleaved measured slower, C3 x-update 0.063 -> 0.068 ms, prox 0.325 -> 0.330 ms; profiles/r05/ab/)
-#ifndef MMX_ZU_INTER
-#define MMX_ZU_INTER 0
-#endif
 template <int D>
 struct DeviceMesh {
   int nP, nF;
@@ -46,6 +43,9 @@ struct DeviceMesh {
   int xupSweep;           // 3D slot-term x-update as a per-XCD sweep: workgroups per CU (0: one node per lane)
   int forceTie;           // test hook (MMX_FORCE_TIE=n): every n-th prox block takes the exact path
   const int* nodeOrder;   // x-update processing order (nodes by first incident simplex) or nullptr
+  // the x-update's share of that order: positions [xupLo, xupHi) (an element partition launches its
+  // interior nodes, which need no remote slot, while the halo exchange runs, then the rest)
+  int xupLo, xupHi;
   const double* invdiag;  // per node 1 / t_ii (block-diagonal t = tau I + dt^2 WD^T WD)
   const double* Vc;       // nP x D reference positions (CompMesh) or nullptr
   // monitor grid
@@ -128,9 +128,18 @@ void launch_reduce_partials2(const double* partials, int nblocks, double* out, c
                              double* out2, hipStream_t st, const RedWork& w = {});
 // interface-slot values a rank contributes to the exchange: mode 0 the x-update term
 // w (w (z - u)) per slot, mode 1 the simplex gradient gs per slot (D values each)
+// zx (mode 0, a step's first exchange on a partition with DeviceMesh::zx): z of a slot of node v is
+// zx_v (predicted: 2 x_v - xPrev_v, the fused predictX of the x-update that has not run yet), F
+// gives the slot's node
+struct PackZX {
+  const int* F = nullptr;
+  const double* zx = nullptr;
+  const double* x = nullptr;      // predicted: x and xPrev before the step's first x-update
+  const double* xPrev = nullptr;
+};
 template <int D>
 void launch_pack_export(int mode, int nExp, const int* expOff, const double* z, const double* u, const double* gs,
-                        double w, double* out, hipStream_t st);
+                        double w, double* out, hipStream_t st, const PackZX& zx = {});
 
 // ---- backward Euler (Mesh::backwardsEulerStep, src/Mesh.cpp:1263-1341) ----
 // FD derivative blocks of FSubJac (src/Mesh.cpp:1173-1230) at positions Vp: one D x K block per

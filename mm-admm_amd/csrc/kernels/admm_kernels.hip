@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <stdexcept>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -262,7 +263,7 @@ __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, c
 // A node's incident slots are taken 8 at a time: their offsets, then all their z and u values
 // are requested before the first is added (branch-free: lanes past the end re-read the last
 // slot, a slot of another rank reads its gathered row), then summed in ascending order.
-template <int D, bool RESID, bool TS, int CH = 8, bool ZX = false, bool PRED = false>
+template <int D, bool RESID, bool TS, int CH = 8, bool ZX = false, bool PRED = false, bool REM = false>
 __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepScalars& sc,
                                              const double* __restrict__ xBar, const double* __restrict__ z,
                                              const double* __restrict__ u, double* __restrict__ x, int idx,
@@ -292,7 +293,8 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
       for (int c = 0; c < D; ++c) xb[c] = xBar[(size_t)v * D + c];
     }
     // ZX: a step's first x-update without z (DeviceMesh::zx): every local slot of node v holds z = zx_v
-    // (with PRED, zx is this step's xBar: the node's own xb)
+    // (with PRED, zx is this step's xBar: the node's own xb); REM: an element partition, whose
+    // remote slots still come from the exchange (their terms formed by launch_pack_export)
     constexpr bool zv0 = ZX && !TS;
     if constexpr (zv0) {
       if constexpr (PRED) {
@@ -321,7 +323,9 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
           const double* pu = loc ? u + zu_off<D>(off[j]) : pz;
 #pragma unroll
           for (int c = 0; c < D; ++c) {
-            if constexpr (zv0)  // (one rank only: no slot of another rank)
+            if constexpr (zv0 && REM)
+              zv[j][c] = loc ? zn[c] : pz[c];
+            else if constexpr (zv0)  // (one rank only: no slot of another rank)
               zv[j][c] = zn[c];
             else
               zv[j][c] = pz[c];
@@ -379,16 +383,17 @@ __device__ __forceinline__ void xupdate_node(const DeviceMesh<D>& m, const StepS
 #ifndef MMX_XU_CH2D
 #define MMX_XU_CH2D 6  // 2D: incident slots requested at once per node (C3: 8 0.066 ms, 6 0.0645, 4 0.079)
 #endif
-template <int D, bool RESID, bool TS, bool ZX = false, bool PRED = false>
+template <int D, bool RESID, bool TS, bool ZX = false, bool PRED = false, bool REM = false>
 __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars sc,
                                                      const double* __restrict__ xBar,
                                                      const double* __restrict__ z,
                                                      const double* __restrict__ u, double* __restrict__ x,
                                                      double* __restrict__ partials, int xcd) {
   const int lb = logical_block(xcd);
-  const int idx = lb * kBlock + threadIdx.x;
+  const int idx = m.xupLo + lb * kBlock + threadIdx.x;
   double pv[3] = {0, 0, 0};
-  if (idx < m.nP) xupdate_node<D, RESID, TS, (D == 2 ? MMX_XU_CH2D : 8), ZX, PRED>(m, sc, xBar, z, u, x, idx, pv);
+  if (idx < m.xupHi)
+    xupdate_node<D, RESID, TS, (D == 2 ? MMX_XU_CH2D : 8), ZX, PRED, REM>(m, sc, xBar, z, u, x, idx, pv);
   if constexpr (RESID) block_partials<3>(pv, partials, lb);
 }
 // The slot-term x-update (no residual) as a sweep: XCD c (= blockIdx % 8) takes the node-order
@@ -402,7 +407,7 @@ __global__ void __launch_bounds__(kBlock) k_xupdate_sweep(DeviceMesh<D> m, StepS
                                                            const double* __restrict__ z, const double* __restrict__ u,
                                                            double* __restrict__ x, int n8) {
   const int c = (int)(blockIdx.x % 8), w = (int)(blockIdx.x / 8), per = (int)(gridDim.x / 8);
-  const int lo = c * n8, hi = min(lo + n8, m.nP);
+  const int lo = m.xupLo + c * n8, hi = min(lo + n8, m.xupHi);
   double pv[3];
   for (int idx = lo + w * kBlock + (int)threadIdx.x; idx < hi; idx += per * kBlock)
     xupdate_node<D, false, TS, CH>(m, sc, xBar, z, u, x, idx, pv);
@@ -2012,13 +2017,24 @@ template <int D>
 __global__ void __launch_bounds__(kBlock) k_pack_export(int mode, int nExp, const int* __restrict__ expOff,
                                                          const double* __restrict__ z, const double* __restrict__ u,
                                                          const double* __restrict__ gs, double w,
-                                                         double* __restrict__ out) {
+                                                         double* __restrict__ out, PackZX zx) {
+  constexpr int K = D * (D + 1);
   const int e = blockIdx.x * kBlock + threadIdx.x;
   if (e >= nExp) return;
   const size_t off = (size_t)expOff[e], zo = zu_off<D>(expOff[e]);
+  double zv[D];
+  if (mode == 0 && zx.zx) {  // z of the slot = zx of its node (DeviceMesh::zx); predicted: 2 x - xPrev
+    const int s = expOff[e] / K, n = (expOff[e] % K) / D;
+    const size_t v = (size_t)zx.F[(size_t)s * (D + 1) + n];
+#pragma unroll
+    for (int c = 0; c < D; ++c) zv[c] = zx.x ? 2 * zx.x[v * D + c] - zx.xPrev[v * D + c] : zx.zx[v * D + c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < D; ++c) zv[c] = z[zo + c];
+  }
 #pragma unroll
   for (int c = 0; c < D; ++c)
-    out[(size_t)e * D + c] = (mode == 0) ? w * (w * (z[zo + c] - u[zo + c])) : gs[off + c];
+    out[(size_t)e * D + c] = (mode == 0) ? w * (w * (zv[c] - u[zo + c])) : gs[off + c];
 }
 
 constexpr int kRed = 1024;
@@ -2244,20 +2260,35 @@ template <int D>
 void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar, const double* z,
                     const double* u, double* x, double* partials, int* nblocks, bool resid, hipStream_t st,
                     bool useTslot) {
-  *nblocks = nblk_xcd(m.nP);
-  if (m.nP == 0) return;
-  const bool ts = useTslot && m.tslot;
-  if (D == 2 && m.zx && !resid && !ts) {  // a step's first x-update: z from DeviceMesh::zx
-    if (m.predBar)  // ... and predictX's extrapolation fused in
-      hipLaunchKernelGGL((k_xupdate<D, false, false, true, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z,
-                         u, x, partials, xcd_map());
-    else
-      hipLaunchKernelGGL((k_xupdate<D, false, false, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, u,
-                         x, partials, xcd_map());
+  const int nsub = m.xupHi - m.xupLo;  // the launch's share of the node order
+  *nblocks = nblk_xcd(nsub);
+  if (nsub <= 0) {
+    *nblocks = 0;
     return;
   }
+  const bool ts = useTslot && m.tslot;
+  const bool rem = m.remote != nullptr;
+  if (D == 2 && m.zx && !resid && !ts) {  // a step's first x-update: z from DeviceMesh::zx
+#define MMX_XU_ZX(P, R)                                                                                        \
+  hipLaunchKernelGGL((k_xupdate<D, false, false, true, P, R>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, \
+                     u, x, partials, xcd_map())
+    if (m.predBar && rem)  // ... and predictX's extrapolation fused in
+      MMX_XU_ZX(true, true);
+    else if (m.predBar)
+      MMX_XU_ZX(true, false);
+    else if (rem)
+      MMX_XU_ZX(false, true);
+    else
+      MMX_XU_ZX(false, false);
+#undef MMX_XU_ZX
+    return;
+  }
+  // the fused extrapolation exists only in the form above: a caller that set it for another form
+  // would lose predictX silently
+  if (m.predBar || m.predPrev)
+    throw std::logic_error("launch_xupdate: predBar set for an x-update that cannot fuse predictX");
   if (!resid && m.xupSweep > 0) {  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU
-    const int n8 = ((m.nP + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
+    const int n8 = ((nsub + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
     const dim3 g(256 * m.xupSweep);
     if (ts && m.xupCh >= 24)
       hipLaunchKernelGGL((k_xupdate_sweep<D, true, 24>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
@@ -2480,7 +2511,11 @@ void launch_euler_apply(const DeviceMesh<D>& m, const double* gs, double* x, dou
 }
 // one workgroup per set reads its partials at ~0.1 TB/s (C3: 10 sets of 31 k prox partials took 45 us
 // per step); the split form spreads each set over kRedSplit workgroups
-static bool split_ok(const RedWork& w, int nblocks) { return w.scratch && nblocks >= kRedSplitMin; }
+// MMX_RED_SPLIT_MIN overrides kRedSplitMin (tests force the split form on small meshes)
+static bool split_ok(const RedWork& w, int nblocks) {
+  const char* e = getenv("MMX_RED_SPLIT_MIN");
+  return w.scratch && nblocks >= (e ? atoi(e) : kRedSplitMin);
+}
 static void reduce_split(const double* partA, size_t stride, int nbA, int nA, double* outA, size_t outStride,
                          const double* partB, int nbB, double* outB, const RedWork& w, hipStream_t st) {
   const int sets = nA + (nbB >= 0 ? 1 : 0);
@@ -2521,15 +2556,15 @@ template void launch_debug_blockgrad<3>(const DeviceMesh<3>&, int, const double*
                                         hipStream_t);
 template <int D>
 void launch_pack_export(int mode, int nExp, const int* expOff, const double* z, const double* u, const double* gs,
-                        double w, double* out, hipStream_t st) {
+                        double w, double* out, hipStream_t st, const PackZX& zx) {
   if (nExp <= 0) return;
   hipLaunchKernelGGL(k_pack_export<D>, dim3((nExp + kBlock - 1) / kBlock), dim3(kBlock), 0, st, mode, nExp, expOff, z, u,
-                     gs, w, out);
+                     gs, w, out, zx);
 }
 template void launch_pack_export<2>(int, int, const int*, const double*, const double*, const double*, double, double*,
-                                    hipStream_t);
+                                    hipStream_t, const PackZX&);
 template void launch_pack_export<3>(int, int, const int*, const double*, const double*, const double*, double, double*,
-                                    hipStream_t);
+                                    hipStream_t, const PackZX&);
 
 void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st) {
   if (n == 0) return;
@@ -2605,3 +2640,6 @@ extern "C" int mmx_wprof_dump(const char* path) {
   return (int)(h.size() / 8);
 }
 #endif
+
+// the layout word this kernel object was compiled with (layout.h; checked by the host at create)
+extern "C" unsigned mmx_layout_admm(void) { return mmx::kLayoutWord; }

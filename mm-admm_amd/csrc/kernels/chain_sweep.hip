@@ -646,3 +646,6 @@ void launch_chain_fill(long long n, const int* srcIdx, const double* af, double*
 }
 
 }  // namespace mmx
+
+// the layout word this kernel object was compiled with (layout.h; checked by the host at create)
+extern "C" unsigned mmx_layout_chain(void) { return mmx::kLayoutWord; }

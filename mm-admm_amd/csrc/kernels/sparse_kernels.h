@@ -5,15 +5,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "layout.h"  // MMX_SPMV_*, MMX_CHAIN_VEC / CODE16
+
 namespace mmx {
 
-// Products staged in LDS per SpMV workgroup (16 KB of fp64).
-#ifndef MMX_SPMV_TILE
-#define MMX_SPMV_TILE 2048
-#endif
-#ifndef MMX_SPMV_BLOCK
-#define MMX_SPMV_BLOCK 256
-#endif
+// Products staged in LDS per SpMV workgroup (16 KB of fp64; layout.h).
 constexpr int kSpmvTile = MMX_SPMV_TILE;
 constexpr int kSpmvBlock = MMX_SPMV_BLOCK;
 // Rows per chunk of the level-scheduled factor/sweeps (one wavefront per chunk) and the size of
@@ -68,8 +64,10 @@ void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, cons
 constexpr int kFacWaveNL = 32;
 void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, const int* iaf, const int* dg,
                             const int2* piv, const int* jaf, const int* toff, const signed char* tgt, const int* perm,
-                            int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* err,
-                            hipStream_t st);
+                            int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* ticket,
+                            unsigned* err, hipStream_t st);
+// test hook: blocks x 1024 lanes (64 KB LDS each) holding their CUs for ms milliseconds
+void launch_occupy(int blocks, double ms, double* sink, hipStream_t st);
 
 // Sweep over the rows of perm (forward or backward level order).  Forward: unit L into granules
 // gout, right-hand side per pro (0: src; 1: p = res + beta (p - omega avbar); 2: s = res - alpha
@@ -81,15 +79,6 @@ void launch_sweep(bool fwd, int pro, const int* iaf, const int* jaf, const int* 
 
 // Band/chain-scheduled sweeps (chain_sweep.hip, schedule host/chain_sched.h): the same rows and
 // arithmetic as launch_sweep, with intra-band dependencies resolved in LDS.
-// chain-sweep stage images (chain_sweep.hip, host/sparse.cpp upload_chain): entries lane-interleaved
-// for 16-byte LDS reads (MMX_CHAIN_VEC), entry codes 16-bit (MMX_CHAIN_CODE16; 32-bit otherwise,
-// except the 48-entry stages, always 16-bit)
-#ifndef MMX_CHAIN_VEC
-#define MMX_CHAIN_VEC 1
-#endif
-#ifndef MMX_CHAIN_CODE16
-#define MMX_CHAIN_CODE16 1
-#endif
 inline constexpr bool chain_code16(int ee) { return MMX_CHAIN_CODE16 || ee > 32; }
 
 struct ChainArgs {

@@ -505,9 +505,11 @@ __global__ void __launch_bounds__(kSweepRows) k_ilu_factor_lds(const int* __rest
 }
 
 // The same factor with one wavefront per row (rows wider than a lane can take in reasonable time:
-// 3D mesh rows have up to 26 lower and 71 entries).  The rows are dealt round-robin in forward
-// level order to a grid that is resident at once (sized by the occupancy query), so a row only
-// waits for rows earlier in that order.  Per row: its image in LDS (entry e at w[e]); lane q polls
+// 3D mesh rows have up to 26 lower and 71 entries).  Each wavefront takes rows by ticket in
+// forward level order, and requests its next ticket while the current row runs: the smallest
+// ticket not yet finished is always some running wave's current row, whose pivots all carry
+// smaller tickets, so the factor progresses with any number of resident waves (round 5 dealt rows
+// round-robin to a grid assumed resident at once, which a concurrent kernel could break).  Per row: its image in LDS (entry e at w[e]); lane q polls
 // the flag of lower entry q's pivot row until all are published; then, for every lower entry q,
 // lane u holds U(j_q, .)'s u-th upper value and its position tgt[] in row i (-1: not held),
 // requested together.  The eliminations run in ascending q: mult = w[q] / U(j_q, j_q), w[q] = mult,
@@ -520,13 +522,17 @@ __global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__
                                                          const int* __restrict__ dg, const int2* __restrict__ piv,
                                                          const int* __restrict__ jaf, const int* __restrict__ toff,
                                                          const signed char* __restrict__ tgt, const int* __restrict__ perm,
-                                                         int nrows, int nwaves, double* af, unsigned* flags, uint64_t* gF,
-                                                         unsigned epoch, unsigned* err) {
+                                                         int nrows, unsigned* ticket, double* af, unsigned* flags,
+                                                         uint64_t* gF, unsigned epoch, unsigned* err) {
   __shared__ double s_row[4][kFacW + 1];
   const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
   double* w = s_row[wv];
-  const int gw = (int)blockIdx.x * 4 + wv;
-  for (int x = gw; x < nrows; x += nwaves) {
+  // lane 0 takes the wave's tickets (the value is read only where it is needed: the next ticket's
+  // round trip overlaps the current row)
+  auto take = [&]() -> unsigned { return lane == 0 ? atomicAdd(ticket, 1u) : 0u; };
+  unsigned tk = take();
+  for (int x = (int)__shfl(tk, 0); x < nrows; x = (int)__shfl(tk, 0)) {
+    tk = take();  // the next row's ticket
     const int i = perm[x];
     const int kb = iaf[i], kd = dg[i], ke = iaf[i + 1];
     const int W = ke - kb, nl = kd - kb;
@@ -849,6 +855,7 @@ void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, cons
                      tgt, perm, nchunks, af, flags, epoch, ticket, err);
 }
 
+// (the grid's size is a throughput choice only: the tickets need no co-residency)
 int ilu_factor_wave_grid() {
   static int g = [] {
     int dev = 0, cus = 0, nb = 0;
@@ -866,17 +873,37 @@ int ilu_factor_wave_grid() {
 
 void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, const int* iaf, const int* dg,
                             const int2* piv, const int* jaf, const int* toff, const signed char* tgt, const int* perm,
-                            int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* err,
-                            hipStream_t st) {
+                            int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* ticket,
+                            unsigned* err, hipStream_t st) {
   if (nrows <= 0) return;
-  // every workgroup resident at once: a row waits only for rows dealt before it
+  // one CU's worth of waves per CU and occupancy slot; rows by ticket (*ticket zeroed by the caller)
   const int blocks = std::min(ilu_factor_wave_grid(), (nrows + 3) / 4);
   if (gF)
     hipLaunchKernelGGL((k_ilu_factor_wave<kFacWaveNL, true>), dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv,
-                       jaf, toff, tgt, perm, nrows, blocks * 4, af, flags, gF, epoch, err);
+                       jaf, toff, tgt, perm, nrows, ticket, af, flags, gF, epoch, err);
   else
     hipLaunchKernelGGL((k_ilu_factor_wave<kFacWaveNL, false>), dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv,
-                       jaf, toff, tgt, perm, nrows, blocks * 4, af, flags, gF, epoch, err);
+                       jaf, toff, tgt, perm, nrows, ticket, af, flags, gF, epoch, err);
+}
+
+// Test hook (mmx_occupy): `blocks` workgroups of 1024 lanes with 64 KB of LDS each that hold their
+// CUs for `ms` milliseconds (the 100 MHz real-time counter; every wave leaves at the deadline) --
+// a concurrent kernel that keeps part of the chip away from the solver's kernels.
+__global__ void __launch_bounds__(1024) k_occupy(unsigned long long ticks, double* sink) {
+  extern __shared__ double lds[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  lds[threadIdx.x] = (double)threadIdx.x;
+  double acc = 0.0;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(8);
+    acc += lds[(threadIdx.x * 7) & 1023];
+  }
+  if (acc < 0.0) sink[threadIdx.x] = acc;  // never true: keeps the loop's reads
+}
+void launch_occupy(int blocks, double ms, double* sink, hipStream_t st) {
+  if (blocks <= 0 || !(ms > 0)) return;
+  const unsigned long long ticks = (unsigned long long)(ms * 1e5);  // 100 MHz
+  hipLaunchKernelGGL(k_occupy, dim3(blocks), dim3(1024), 64 * 1024, st, ticks, sink);
 }
 
 void launch_ilu_factor(const int* ia, const int* ja, const double* a, const int* amap, const int* iaf, const int* jaf,
@@ -1015,3 +1042,6 @@ void launch_stream_copy(int variant, long long n2, const double* src, double* ds
 }
 
 }  // namespace mmx
+
+// the layout word this kernel object was compiled with (layout.h; checked by the host at create)
+extern "C" unsigned mmx_layout_sparse(void) { return mmx::kLayoutWord; }

@@ -92,6 +92,8 @@ def lib():
     L.mmx_matrix_stats_reset.argtypes = [vp]
     L.mmx_matrix_destroy.argtypes = [vp]
     L.mmx_stream_copy.argtypes = [i, vp, vp, ll, i, i, ctypes.POINTER(ctypes.c_double)]
+    L.mmx_occupy.argtypes = [i, i, ctypes.c_double]
+    L.mmx_occupy_wait.argtypes = []
     L.mmx_ilu_symbolic.argtypes = [i, c_int_p, c_int_p, i, ctypes.POINTER(ll), c_int_p, c_int_p, c_int_p]
     _cfg = True
     return L
@@ -304,3 +306,13 @@ def matmult(A, x):
 
 
 __all__ = ["ParamIter", "MatrixStruc", "MatrixIter", "matmult", "ilu_symbolic", "stream_copy_ms", "MMADMMError"]
+
+
+def occupy(blocks, ms, device=0):
+    """test hook: hold `blocks` workgroups' CUs for ms milliseconds on a stream of the library's own
+    (asynchronous; occupy_wait() joins it)"""
+    _check(lib().mmx_occupy(int(device), int(blocks), float(ms)))
+
+
+def occupy_wait():
+    _check(lib().mmx_occupy_wait())

@@ -51,7 +51,10 @@ class mmadmm_stats(ctypes.Structure):
                 ("cg_iters", ctypes.c_longlong), ("t_jac_ms", ctypes.c_double), ("t_solve_ms", ctypes.c_double),
                 ("t_be_ms", ctypes.c_double), ("regrids", ctypes.c_longlong), ("regrid_rows", ctypes.c_longlong),
                 ("regrid_gather_bytes", ctypes.c_double), ("regrid_cand", ctypes.c_longlong),
-                ("regrid_fallbacks", ctypes.c_longlong), ("monitor_iso", ctypes.c_int)]
+                ("regrid_fallbacks", ctypes.c_longlong), ("monitor_iso", ctypes.c_int),
+                ("t_exchange_ms", ctypes.c_double), ("n_exchange", ctypes.c_longlong),
+                ("halo_send_bytes", ctypes.c_double), ("halo_recv_bytes", ctypes.c_double),
+                ("interior_nodes", ctypes.c_int), ("overlap", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -132,6 +135,8 @@ def lib():
     vp = ctypes.c_void_p
     L.mmadmm_comm_unique_id.argtypes = [vp, ctypes.c_int]
     L.mmadmm_comm_create_rccl.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.mmadmm_comm_create_rccl_timeout.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_double,
+                                                  ctypes.POINTER(vp)]
     L.mmadmm_comm_create_loopback.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.mmadmm_comm_destroy.argtypes = [vp]
     L.mmadmm_comm_nranks.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
@@ -347,10 +352,17 @@ class Comm:
         return buf.raw
 
     @staticmethod
-    def rccl(nranks, rank, uid, device):
+    def rccl(nranks, rank, uid, device, timeout_s=None):
+        """RCCL communicator (collective over the ranks).  timeout_s bounds its creation and every
+        wait of a partitioned step (default: MMX_COMM_TIMEOUT_S, else 300 s; <= 0: none): a rank
+        that never joins or stops makes the others fail with MMADMM_ERR_RCCL, not hang."""
         h = ctypes.c_void_p()
         buf = ctypes.create_string_buffer(bytes(uid), UNIQUE_ID_BYTES)
-        _check(lib().mmadmm_comm_create_rccl(int(nranks), int(rank), buf, int(device), ctypes.byref(h)))
+        if timeout_s is None:
+            _check(lib().mmadmm_comm_create_rccl(int(nranks), int(rank), buf, int(device), ctypes.byref(h)))
+        else:
+            _check(lib().mmadmm_comm_create_rccl_timeout(int(nranks), int(rank), buf, int(device),
+                                                         ctypes.c_double(float(timeout_s)), ctypes.byref(h)))
         return Comm(h)
 
     @staticmethod

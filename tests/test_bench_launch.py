@@ -114,6 +114,61 @@ def test_bench_two_ranks_host_transport_rehearsal():
     assert d["ranks"] == 2 and d["n_gpus"] >= 1 and d["steps"] == 3
     cfg = d["config"]
     assert cfg["parallelism"].startswith("element-partition x2") and cfg["comm"] == "host"
-    assert cfg["rccl_nranks"] == 2 and len(cfg["nodes_per_rank"]) == 2
+    assert cfg["comm_nranks"] == 2 and cfg["rccl_nranks"] is None and len(cfg["nodes_per_rank"]) == 2
     assert sum(cfg["simplices_per_rank"]) == cfg["global_simplices"]
     assert d["value"] > 0 and d["early_exit"]["admm_iters_per_step"] > 0
+
+
+def _env_no_launcher(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MMX_BENCH_PROGRESS",
+                                                            "MMX_BENCH_TEST_STALL_RANK")}
+    env.update(extra)
+    return env
+
+
+def test_rendezvous_two_ranks():
+    """--gpus 2 --rendezvous-only: the re-launch, both ranks' phase lines and the gloo rendezvous, no GPU"""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rendezvous-only",
+                        "--budget-s", "120"], capture_output=True, text=True, timeout=400, env=_env_no_launcher())
+    assert r.returncode == 0, r.stderr[-3000:]
+    for rk in (0, 1):
+        for ph in ("start", "rendezvous", "setup", "done"):
+            assert "rank %d/2: phase %s" % (rk, ph) in r.stderr, r.stderr[-3000:]
+
+
+def test_stalled_rank_fails_within_budget_and_is_named():
+    """one of two ranks never joins the rendezvous.  The job must end non-zero
+    within its budget (each rank's watchdog, and the parent's process-group kill behind it) and name
+    the rank that never got there -- a driver time-out with no diagnosis is the failure this prevents."""
+    import time
+    budget = 20
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rendezvous-only",
+                        "--budget-s", str(budget)], capture_output=True, text=True, timeout=budget + 240,
+                       env=_env_no_launcher(MMX_BENCH_TEST_STALL_RANK="1"))
+    el = time.time() - t0
+    assert r.returncode != 0, r.stderr[-3000:]
+    assert el < budget + 90, el  # the watchdogs fire at the budget; the parent's kill is at budget + 60
+    assert "ranks that never reached the rendezvous: 1" in r.stderr, r.stderr[-3000:]
+    assert "rank 1: last phase start" in r.stderr
+    assert "exceeded in phase" in r.stderr  # a watchdog's message
+    assert r.stdout.strip() == ""
+
+
+def test_relaunch_kills_group_after_budget(monkeypatch, tmp_path):
+    """the parent's own budget: a launcher that outlives budget + 60 s is killed as a process group
+    and the call returns 124 (here with a fake launcher and the grace shortened)"""
+    import time
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    real_popen = subprocess.Popen
+
+    def fake_popen(cmd, **kw):  # a 'launcher' that sleeps, with a child of its own in the group
+        return real_popen([sys.executable, "-c", "import subprocess,sys,time; "
+                           "subprocess.Popen([sys.executable,'-c','import time; time.sleep(600)']); time.sleep(600)"],
+                          **kw)
+
+    monkeypatch.setattr(subprocess, "Popen", fake_popen)
+    t0 = time.time()
+    rc = bench.relaunch(2, budget_s=-58.0)  # kill after 2 s
+    assert rc == 124
+    assert time.time() - t0 < 60

@@ -396,3 +396,36 @@ def test_wave_factor_equals_level_factor(la, mesh, gran, monkeypatch):
     assert _bit(af_w, af_l)
     if N < 20000:
         assert _bit(af_w, L.ilu0(ia, ja, a))
+
+
+def test_wave_factor_completes_beside_a_kernel_holding_cus(la, monkeypatch):
+    """the wave factor takes rows by ticket, so it needs no co-resident grid.  A
+    kernel on another stream of this process holds every CU's first 16 waves and 64 KB of LDS for
+    4 s; the factor (3D pattern, rect 3 16) must finish well before that kernel ends -- round 5's
+    static dealing left rows on non-resident waves, and the resident ones spun until the ~1 s
+    give-up (MMADMM_ERR_HIP) -- and stay bit-identical to the level factor."""
+    import time
+    m = oracle_py.Mesh.rect(3, 16)
+    ia, ja = L.mesh_pattern(3, m.nP, m.F)
+    N = len(ia) - 1
+    rng = np.random.default_rng(21)
+    a = rng.uniform(-1, 1, len(ja))
+    rows = np.repeat(np.arange(N), np.diff(ia))
+    d = np.nonzero(ja == rows)[0]
+    a[d] = np.add.reduceat(np.abs(a), ia[:-1]) * 0.3 + 1.0
+    af_l, _ = _factor_run(la, ia, ja, a, "level", monkeypatch)
+    monkeypatch.delenv("MMX_FACTOR", raising=False)
+    A = _matrix(la, ia, ja, a, np.ones(N))
+    A.sfac(la.ParamIter.mesh())
+    A.factor()  # warm-up (first launches)
+    la.occupy(256, 4000.0)
+    t0 = time.time()
+    A.factor()
+    af_w = A.get_factor()[2]
+    el = time.time() - t0
+    fm = A.stats()["factor_mode"]
+    la.occupy_wait()
+    A.close()
+    assert fm == 2
+    assert _bit(af_w, af_l)
+    assert el < 3.0, el

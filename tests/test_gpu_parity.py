@@ -126,12 +126,14 @@ def test_steps_bitwise(name):
     mk, mon, dt, tau, rho, comp = cases()[name]
     mesh = mk()
     O, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
-    nsteps = 4 if mesh.dim == 2 else 3
+    # 2D: 6 steps, so the predictor fused into the first x-update (steps after the third) runs three
+    # times and its xPrev / xBar writes are read by later steps' extrapolations
+    nsteps = 6 if mesh.dim == 2 else 3
     for s in range(nsteps):
         ih_o = O.step(5, -1.0)[0]
         ih_g = G.step(5, -1.0)[0]
         assert abs(ih_o - ih_g) <= 1e-12 * abs(ih_o)
-        for f in ("x", "z", "u", "xBar"):
+        for f in ("x", "z", "u", "xBar", "xPrev"):
             np.testing.assert_array_equal(G.get(f), O.get(f), err_msg=f"{f} step {s}")
     np.testing.assert_array_equal(G.get("hess"), O.get("hess"))
     assert G.stats()["bfgs_iters"] == O.bfgs_iters()
@@ -428,3 +430,46 @@ def test_isotropic_grid_path_bitwise(name, monkeypatch):
     assert out["0"][0] == 0 and out["1"][0] == iso
     for a, b in zip(out["0"][1:], out["1"][1:]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("knob", ["MMX_ZX", "MMX_FUSE_PRED"])
+@pytest.mark.parametrize("name", ["hexdisc12_mex1", "rect16_mex2"])
+def test_step_start_fusions_ab_bitwise(name, knob, monkeypatch):
+    """The 2D step start (ADVICE r5): z taken from the positions (DeviceMesh::zx, no k_gather_z) and
+    predictX fused into the first x-update, against new engines with each turned off -- x, xPrev,
+    xBar, z, u bit-identical over 6 steps (the fused predictor runs from the fourth)."""
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    _, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    monkeypatch.setenv(knob, "0")
+    _, Gk = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    monkeypatch.delenv(knob)
+    for s in range(6):
+        assert G.step(5, -1.0)[0] == Gk.step(5, -1.0)[0]
+        for f in ("x", "xPrev", "xBar", "z", "u"):
+            np.testing.assert_array_equal(G.get(f), Gk.get(f), err_msg=f"{knob}=0: {f} step {s}")
+
+
+@pytest.mark.parametrize("name", ["hexdisc12_mex1", "rect3d_3_mex1"])
+def test_split_reductions_small_mesh(name, monkeypatch):
+    """The two-launch reductions (k_reduce_split + k_reduce_combine into the mapped pinned results)
+    normally run only at >= 4096 partial rows, i.e. at the at-size meshes.
+    MMX_RED_SPLIT_MIN=1 forces them on a small mesh: the energies and BFGS totals must equal the
+    oracle's and the one-workgroup path's, and repeated runs must be bit-identical."""
+    mk, mon, dt, tau, rho, comp = cases()[name]
+    mesh = mk()
+    O, G = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    monkeypatch.setenv("MMX_RED_SPLIT_MIN", "1")
+    _, Gs = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    _, Gs2 = make_pair(mesh, mon, dt, tau, rho, comp, 1, 1)
+    for s in range(3):
+        for tol in (-1.0, 1e-3):  # the deferred whole-step reduction and the per-iteration one
+            ih_o, it_o = O.step(5, tol)[:2]
+            ih_g, it_g = G.step(5, tol)
+            ih_s, it_s = Gs.step(5, tol)
+            ih_s2, it_s2 = Gs2.step(5, tol)
+            assert it_s == it_g == it_o and ih_s == ih_s2
+            assert abs(ih_s - ih_o) <= 1e-12 * abs(ih_o) and abs(ih_s - ih_g) <= 1e-12 * abs(ih_g)
+    np.testing.assert_array_equal(Gs.get("x"), O.get("x"))
+    assert Gs.stats()["bfgs_iters"] == O.bfgs_iters() == Gs2.stats()["bfgs_iters"]
+    assert Gs.stats()["last_primal"] == Gs2.stats()["last_primal"]

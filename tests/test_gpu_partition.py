@@ -57,7 +57,9 @@ def test_partitioned_equals_single(mx, name, gen, dim, mon, rho, tau, dt, nranks
     ref = mx.Engine(M, dt)
     comm = mx.Comm.loopback(nranks)
     parts = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm, partition=method) for r in range(nranks)]
-    steps, iters = 4, 6
+    # 5 steps: 2D partitions take z from the positions and fuse predictX into the first x-update
+    # from the fourth step on (round 6), and overlap every x-update's interior nodes with the exchange
+    steps, iters = 5, 6
     ih_ref = [ref.step(iters, -1.0)[0] for _ in range(steps)]
     ih = [[None] * steps for _ in range(nranks)]
 
@@ -314,3 +316,45 @@ def test_partitioned_early_exit_equals_single(mx):
     for e in parts:
         assert np.array_equal(e.get("x").reshape(-1, 2), xr[e.local_nodes()])
         assert e.stats()["n_prox"] == n_ref
+
+
+@pytest.mark.parametrize("knob", ["MMX_OVERLAP", "MMX_ZX", "MMX_FUSE_PRED"])
+@pytest.mark.parametrize("dim,nranks", [(2, 3), (3, 2)])
+def test_partition_step_variants_bitwise(mx, dim, nranks, knob, monkeypatch):
+    """Round 6: the partitioned step overlaps the interior x-update with the
+    halo exchange and, in 2D, keeps the one-rank step start (z from the positions, predictX fused).
+    Each against engines with it turned off: node positions, xPrev, xBar, z, u bit-identical; the
+    exchange is timed on its stream and its bytes reported."""
+    mesh = mx.MeshData.hexdisc(14, 0.5, 0.5, 0.5) if dim == 2 else mx.MeshData.rect(3, 4)
+    mon, rho, dt = (1, 50.0, 0.055) if dim == 2 else (6, 2000.0, 0.025)
+    M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, mon), rho=rho, tau=0.5, device=0)
+    comm_a, comm_b = mx.Comm.loopback(nranks), mx.Comm.loopback(nranks)
+    A = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm_a) for r in range(nranks)]
+    monkeypatch.setenv(knob, "0")
+    B = [mx.Engine(M, dt, rank=r, nranks=nranks, comm=comm_b) for r in range(nranks)]
+    monkeypatch.delenv(knob)
+    for e in A + B:
+        e.set_timing(True)
+    steps = 5
+
+    def run(es, r):
+        def f():
+            for _ in range(steps):
+                es[r].step(6, -1.0)
+        return f
+
+    _run_parallel([run(A, r) for r in range(nranks)] + [run(B, r) for r in range(nranks)])
+    for r in range(nranks):
+        for f in ("x", "xPrev", "xBar", "z", "u"):
+            assert np.array_equal(A[r].get(f), B[r].get(f)), f"{knob}=0, rank {r}: {f} differs"
+        st = A[r].stats()
+        assert st["overlap"] == 1 and 0 < st["interior_nodes"] < A[r].nP
+        assert st["n_exchange"] == steps * 7 and st["t_exchange_ms"] > 0
+        assert st["halo_send_bytes"] > 0 and st["halo_recv_bytes"] > 0
+        if knob == "MMX_OVERLAP":
+            sb = B[r].stats()
+            assert sb["overlap"] == 0 and sb["interior_nodes"] == B[r].nP
+    for e in A + B:
+        e.close()
+    comm_a.close()
+    comm_b.close()
