@@ -2,7 +2,9 @@
 #include "chain_sched.h"
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <queue>
 #include <unordered_map>
@@ -11,6 +13,19 @@
 namespace mmx {
 
 namespace {
+// MMX_SCHED_PROF=1: the builders' phase times on stderr (host set-up of the first backward-Euler step)
+struct PhaseClock {
+  bool on;
+  const char* who;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseClock(const char* w) : on(getenv("MMX_SCHED_PROF") != nullptr), who(w), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[sched] %s %s %.3f s\n", who, what, std::chrono::duration<double>(n - t).count());
+    t = n;
+  }
+};
 constexpr int kChainLenCap = 1 << 20;  // longest chain (positions fit the schedule's ints)
 // iterations a global value takes to reach another band (model; MMX_CHAIN_LAT overrides)
 static int import_latency() {
@@ -64,10 +79,19 @@ bool assign_import_slots(const std::vector<int>& first, const std::vector<int>& 
 }
 }  // namespace
 
+void big_fill(BigVec& v, size_t n, int x) {
+  BigVec().swap(v);
+  v.resize(n);  // uninitialised (NoInitAlloc)
+  int* p = v.data();
+#pragma omp parallel for schedule(static)
+  for (size_t i = 0; i < n; ++i) p[i] = x;
+}
+
 ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std::vector<int>& jaf,
-                                   const std::vector<int>& dg, bool fwd, int forceG) {
+                                   const std::vector<int>& dg, bool fwd, int forceG, bool codes) {
   ChainSchedule S;
   S.fwd = fwd;
+  PhaseClock pc(fwd ? "fwd" : "bwd");
   auto rb = [&](int i) { return fwd ? iaf[i] : dg[i] + 1; };
   auto re = [&](int i) { return fwd ? dg[i] : iaf[i + 1]; };
   int emax = 0;
@@ -111,6 +135,7 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
     rowIdx[i] = cRows.back()++;
   }
   const int C = (int)cStart.size();
+  pc.mark("chains");
   // positions: a row's value is final at posOf (its last segment / its pair's position); ringOf
   // is the row's sequence number in its lane's LDS ring
   std::vector<int> cLen(C), posOf(n), ringOf(n);
@@ -155,9 +180,19 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   // band's own dependencies (the band then waits for late imports); aligned skews also delay each
   // lane until its imports are due (3D: a band's chains span planes whose imports arrive at very
   // different times).  MMX_CHAIN_ALIGN=0/1 forces one; by default the shorter modelled path wins.
-  std::vector<long long> doneAt(n, -1), offset(S.nbands, 0);
-  auto pass1 = [&](bool align) {
-    std::fill(doneAt.begin(), doneAt.end(), -1);
+  struct Pass1 {  // one modelled schedule: lane skews, band lengths and offsets
+    std::vector<int> laneSkew, bandT;
+    std::vector<long long> doneAt, offset;
+    long long est = 0;
+  };
+  auto pass1 = [&](bool align, Pass1& P) {
+    P.laneSkew.assign((size_t)S.nbands * L, 0);
+    P.bandT.assign(S.nbands, 0);
+    P.doneAt.assign(n, -1);
+    P.offset.assign(S.nbands, 0);
+    std::vector<int>& laneSkew = P.laneSkew;
+    std::vector<long long>& doneAt = P.doneAt;
+    std::vector<long long>& offset = P.offset;
     long long est = 0;
     for (int b = 0; b < S.nbands; ++b) {
       const int c0 = b * L, nl = std::min(L, C - c0);
@@ -174,22 +209,22 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
             for (int k = kb; k < ke; ++k) {
               const int j = jaf[k], cj = chainOf[j];
               if (cj >= c0 && cj < c) {
-                sk = std::max<long long>(sk, S.laneSkew[(size_t)b * L + (cj - c0)] + posOf[j] - p + 1);
+                sk = std::max<long long>(sk, laneSkew[(size_t)b * L + (cj - c0)] + posOf[j] - p + 1);
               } else if (align && cj < c0 && doneAt[j] >= 0) {
                 sk = std::max<long long>(sk, doneAt[j] + import_latency() - off0 - p);
               }
             }
           }
         if (sk > kChainLenCap) sk = kChainLenCap;
-        S.laneSkew[(size_t)b * L + l] = (int)sk;
+        laneSkew[(size_t)b * L + l] = (int)sk;
         minSk = std::min(minSk, (int)sk);
       }
       if (align && nl > 0 && minSk > 0) {  // start the band later rather than idle its lanes
-        for (int l = 0; l < nl; ++l) S.laneSkew[(size_t)b * L + l] -= minSk;
+        for (int l = 0; l < nl; ++l) laneSkew[(size_t)b * L + l] -= minSk;
         off += minSk;
       }
       for (int l = 0; l < nl; ++l) {
-        const int c = c0 + l, sk = S.laneSkew[(size_t)b * L + l];
+        const int c = c0 + l, sk = laneSkew[(size_t)b * L + l];
         T = std::max(T, sk + cLen[c]);
         if (!align)  // the band waits for its late imports
           for (int p = 0; p < cLen[c]; ++p)
@@ -204,31 +239,42 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
       }
       offset[b] = off;
       for (int l = 0; l < nl; ++l) {
-        const int c = c0 + l, sk = S.laneSkew[(size_t)b * L + l];
+        const int c = c0 + l, sk = laneSkew[(size_t)b * L + l];
         for (int r = 0; r < cRows[c]; ++r) {
           const int i = fwd ? cStart[c] + r : cStart[c] - r;
           doneAt[i] = off + posOf[i] + sk + 1;
         }
       }
-      S.bandT[b] = T;
+      P.bandT[b] = T;
       est = std::max(est, off + T);
     }
-    return est;
+    P.est = est;
   };
   {
+    // MMX_CHAIN_ALIGN=0/1 forces one; by default both are modelled (concurrently) and the shorter
+    // critical path wins
     const char* ae = getenv("MMX_CHAIN_ALIGN");
     const int mode = ae ? atoi(ae) : -1;
-    long long est;
+    Pass1 P0, P1;
     if (mode >= 0) {
-      est = pass1(mode != 0);
+      pass1(mode != 0, P0);
       S.aligned = mode != 0;
     } else {
-      const long long e0 = pass1(false), e1 = pass1(true);
-      S.aligned = e1 < e0;
-      est = S.aligned ? e1 : pass1(false);
+#pragma omp parallel sections num_threads(2)
+      {
+#pragma omp section
+        pass1(false, P0);
+#pragma omp section
+        pass1(true, P1);
+      }
+      S.aligned = P1.est < P0.est;
+      if (S.aligned) std::swap(P0, P1);
     }
-    S.estIters = est;
+    S.estIters = P0.est;
+    S.laneSkew.swap(P0.laneSkew);
+    S.bandT.swap(P0.bandT);
   }
+  pc.mark("pass1");
   // lane arrays, slots, ring distances (a ring slot of a lane is written again R / G positions
   // after it is written); a value further back than the ring holds is imported
   int maxDist = 1;
@@ -267,109 +313,135 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   }
   S.R = std::max(2 * G, pow2_at_least(maxDist));
   const int R = S.R;
+  pc.mark("ring");
 
   // pass 2: codes, value sources, imports
-  const size_t ne = (size_t)S.slots * L * EE;
-  S.code.assign(ne, kChainPad);
-  S.impNeed.assign((size_t)S.slots, -1);
+  const size_t ne = codes ? (size_t)S.slots * L * EE : 0;
+  big_fill(S.code, ne, kChainPad);
+  S.impNeed.assign(codes ? (size_t)S.slots : 0, -1);
   S.bandE.assign(S.nbands, 4);
-  S.src.assign(ne, -1);
-  if (!fwd) S.dsrc.assign((size_t)S.slots * G * L, -1);
-  std::vector<int> impOf(n, -1), first, last, rows;
+  big_fill(S.src, ne, -1);
+  if (!fwd && codes) S.dsrc.assign((size_t)S.slots * G * L, -1);
+  pc.mark("alloc");
   std::vector<std::vector<int>> srcBands(S.nbands);  // bands each band imports from
   // the importer runs at most RI imports ahead of the compute wave: it takes the whole ring (a
   // band importing hundreds of values per iteration needs many iterations of run-ahead)
   const int RI = kChainImpMax;
-  for (int b = 0; b < S.nbands; ++b) {
-    const int c0 = b * L, nl = std::min(L, C - c0);
-    first.clear();
-    last.clear();
-    rows.clear();
-    struct Use {
-      size_t slot;
-      int row;
-    };
-    std::vector<Use> impUses;
-    for (int l = 0; l < nl; ++l) {
-      const int c = c0 + l, skl = S.laneSkew[(size_t)b * L + l];
-      for (int p = 0; p < cLen[c]; ++p)
-        for (int g = 0; g < G; ++g) {
-          int q, kb, ke;
-          const int i = part(c, p, g, q, kb, ke);
-          if (i < 0) continue;
-          const int t = p + skl;
-          const size_t base = ((size_t)(S.bandSlot[b] + t) * EE + (size_t)g * E) * L + l;  // [slot][g][e][lane]
-          if (!fwd && q == cNs[c] - 1) S.dsrc[((size_t)(S.bandSlot[b] + t) * G + g) * L + l] = dg[i];
-          int e = 0;
-          S.bandE[b] = std::max(S.bandE[b], (std::max(ke - kb, 0) + 3) / 4 * 4);
-          for (int k = kb; k < ke; ++k, ++e) {
-            const int j = jaf[k], cj = chainOf[j];
-            const size_t x = base + (size_t)e * L;
-            S.src[x] = k;
-            bool ring = false;
-            if (cj == c && posOf[j] == p) {  // the pair's first row, taken from the register
-              S.code[x] = kChainFwd;
-              ring = true;
-            } else if (cj >= c0 && cj <= c) {
-              const int lj = cj - c0;
-              const int d = t - (posOf[j] + S.laneSkew[(size_t)b * L + lj]);
-              if (d * G <= R) {
-                S.code[x] = lj * (R + 1) + (ringOf[j] & (R - 1));
+  struct BandOut {  // per band: its imports in order of first use, or why it failed
+    std::vector<int> row, free, slot, wait;
+    int used = 0;
+    bool bad = false;
+  };
+  std::vector<BandOut> bout(S.nbands);
+  // bands are independent here (disjoint slots of the code / source arrays, their own imports):
+  // in parallel, each thread with its own row -> import map; the imports are listed in band order
+  // after the loop, exactly as a sequential walk lists them
+#pragma omp parallel
+  {
+    std::vector<int> impOf(n, -1), first, last, rows;
+#pragma omp for schedule(dynamic, 8)
+    for (int b = 0; b < S.nbands; ++b) {
+      const int c0 = b * L, nl = std::min(L, C - c0);
+      first.clear();
+      last.clear();
+      rows.clear();
+      struct Use {
+        size_t slot;
+        int row;
+      };
+      std::vector<Use> impUses;
+      for (int l = 0; l < nl; ++l) {
+        const int c = c0 + l, skl = S.laneSkew[(size_t)b * L + l];
+        for (int p = 0; p < cLen[c]; ++p)
+          for (int g = 0; g < G; ++g) {
+            int q, kb, ke;
+            const int i = part(c, p, g, q, kb, ke);
+            if (i < 0) continue;
+            const int t = p + skl;
+            const size_t base = ((size_t)(S.bandSlot[b] + t) * EE + (size_t)g * E) * L + l;  // [slot][g][e][lane]
+            if (codes && !fwd && q == cNs[c] - 1) S.dsrc[((size_t)(S.bandSlot[b] + t) * G + g) * L + l] = dg[i];
+            int e = 0;
+            S.bandE[b] = std::max(S.bandE[b], (std::max(ke - kb, 0) + 3) / 4 * 4);
+            for (int k = kb; k < ke; ++k, ++e) {
+              const int j = jaf[k], cj = chainOf[j];
+              const size_t x = base + (size_t)e * L;
+              if (codes) S.src[x] = k;
+              bool ring = false;
+              if (cj == c && posOf[j] == p) {  // the pair's first row, taken from the register
+                if (codes) S.code[x] = kChainFwd;
                 ring = true;
+              } else if (cj >= c0 && cj <= c) {
+                const int lj = cj - c0;
+                const int d = t - (posOf[j] + S.laneSkew[(size_t)b * L + lj]);
+                if (d * G <= R) {
+                  if (codes) S.code[x] = lj * (R + 1) + (ringOf[j] & (R - 1));
+                  ring = true;
+                }
               }
-            }
-            if (!ring) {
-              int& id = impOf[j];
-              if (id < 0) {
-                id = (int)rows.size();
-                rows.push_back(j);
-                first.push_back(t);
-                last.push_back(t);
+              if (!ring) {
+                int& id = impOf[j];
+                if (id < 0) {
+                  id = (int)rows.size();
+                  rows.push_back(j);
+                  first.push_back(t);
+                  last.push_back(t);
+                }
+                first[id] = std::min(first[id], t);
+                last[id] = std::max(last[id], t);
+                if (codes) impUses.push_back({x, j});
               }
-              first[id] = std::min(first[id], t);
-              last[id] = std::max(last[id], t);
-              impUses.push_back({x, j});
             }
           }
+      }
+      // imports in order of first use
+      std::vector<int> ord(rows.size());
+      for (size_t q = 0; q < ord.size(); ++q) ord[q] = (int)q;
+      std::sort(ord.begin(), ord.end(), [&](int a, int c) {
+        return first[a] != first[c] ? first[a] < first[c] : rows[a] < rows[c];
+      });
+      std::vector<int> rank(rows.size());
+      for (size_t q = 0; q < ord.size(); ++q) rank[ord[q]] = (int)q;
+      std::vector<int> slotOf, waitOf;
+      BandOut& bo = bout[b];
+      bo.bad = !assign_import_slots(first, last, ord, RI, slotOf, waitOf, bo.used);
+      if (!bo.bad) {
+        for (const Use& u : impUses) {
+          const int k = rank[impOf[u.row]];
+          S.code[u.slot] = -(slotOf[k] + 1);
+          const size_t it = u.slot / ((size_t)EE * L);  // slot (iteration) of the use
+          S.impNeed[it] = std::max(S.impNeed[it], k);
         }
+        for (int j : rows) srcBands[b].push_back(chainOf[j] / L);
+        std::sort(srcBands[b].begin(), srcBands[b].end());
+        srcBands[b].erase(std::unique(srcBands[b].begin(), srcBands[b].end()), srcBands[b].end());
+        for (size_t q = 0; q < ord.size(); ++q) {
+          const int id = ord[q];
+          bo.row.push_back(rows[id]);
+          bo.free.push_back(last[id]);
+          bo.slot.push_back(slotOf[q]);
+          bo.wait.push_back(waitOf[q]);
+        }
+      }
+      for (int j : rows) impOf[j] = -1;
     }
-    // imports in order of first use
-    std::vector<int> ord(rows.size());
-    for (size_t q = 0; q < ord.size(); ++q) ord[q] = (int)q;
-    std::sort(ord.begin(), ord.end(), [&](int a, int c) {
-      return first[a] != first[c] ? first[a] < first[c] : rows[a] < rows[c];
-    });
-    std::vector<int> rank(rows.size());
-    for (size_t q = 0; q < ord.size(); ++q) rank[ord[q]] = (int)q;
-    std::vector<int> slotOf, waitOf;
-    int used = 0;
-    if (!assign_import_slots(first, last, ord, RI, slotOf, waitOf, used)) {
+  }
+  for (int b = 0; b < S.nbands; ++b) {
+    const BandOut& bo = bout[b];
+    if (bo.bad) {
       S.why = "import ring too small for band " + std::to_string(b);
       return S;
     }
-    S.maxImpSlots = std::max(S.maxImpSlots, used);
-    for (const Use& u : impUses) {
-      const int k = rank[impOf[u.row]];
-      S.code[u.slot] = -(slotOf[k] + 1);
-      const size_t it = u.slot / ((size_t)EE * L);  // slot (iteration) of the use
-      S.impNeed[it] = std::max(S.impNeed[it], k);
-    }
+    S.maxImpSlots = std::max(S.maxImpSlots, bo.used);
     S.bandImp[b] = (int)S.impRow.size();
-    S.bandNImp[b] = (int)ord.size();
-    for (int j : rows) srcBands[b].push_back(chainOf[j] / L);
-    std::sort(srcBands[b].begin(), srcBands[b].end());
-    srcBands[b].erase(std::unique(srcBands[b].begin(), srcBands[b].end()), srcBands[b].end());
-    for (size_t q = 0; q < ord.size(); ++q) {
-      const int id = ord[q];
-      S.impRow.push_back(rows[id]);
-      S.impFree.push_back(last[id]);
-      S.impSlot.push_back(slotOf[q]);
-      S.impWait.push_back(waitOf[q]);
-    }
-    for (int j : rows) impOf[j] = -1;
+    S.bandNImp[b] = (int)bo.row.size();
+    S.impRow.insert(S.impRow.end(), bo.row.begin(), bo.row.end());
+    S.impFree.insert(S.impFree.end(), bo.free.begin(), bo.free.end());
+    S.impSlot.insert(S.impSlot.end(), bo.slot.begin(), bo.slot.end());
+    S.impWait.insert(S.impWait.end(), bo.wait.begin(), bo.wait.end());
   }
   S.RI = RI;
   S.nImports = (long long)S.impRow.size();
+  pc.mark("pass2");
   // ticket order: a band becomes available once every band it imports from has a ticket; among the
   // available bands the longest (most iterations) goes first, then the lowest index.  The long
   // bands carry the critical path (in the backward sweep they come last by index, behind thousands
@@ -403,8 +475,12 @@ ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std
   // codes -> LDS indices: 0 zero cell, 1 + ring index, 1 + 64 (R + 1) + import slot; the pair's
   // forwarded entry: the cell after the import slots (never read: the kernel takes the register)
   const int impBase = 1 + L * (R + 1);
-  for (int& c : S.code)
+#pragma omp parallel for schedule(static)
+  for (size_t x = 0; x < S.code.size(); ++x) {
+    int& c = S.code[x];
     c = (c == kChainPad) ? 0 : (c == kChainFwd) ? impBase + RI : (c >= 0 ? 1 + c : impBase + (-c - 1));
+  }
+  pc.mark("order+codes");
   S.ok = true;
   return S;
 }
@@ -551,7 +627,9 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
       return F;
     }
   }
-  F.geo = build_chain_schedule(n, iaf, jaf, dg, true, 1);
+  PhaseClock pc("factor");
+  F.geo = build_chain_schedule(n, iaf, jaf, dg, true, 1, false);  // its geometry (no stage codes)
+  pc.mark("geometry");
   ChainSchedule& S = F.geo;
   if (!S.ok) {
     F.why = "forward chain schedule: " + S.why;
@@ -561,10 +639,6 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
     F.why = "segmented schedule";
     return F;
   }
-  S.code.clear();
-  S.code.shrink_to_fit();
-  S.src.clear();
-  S.src.shrink_to_fit();
   const int L = kChainLanes;
   const char* fr = getenv("MMX_FAC_R");
   const int R = std::min(std::min(S.R, kFacRMax), fr ? atoi(fr) : kFacRMax);  // ring slots per lane (rows)
@@ -587,8 +661,15 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
       }
     }
   const size_t nslot = (size_t)S.slots;
-  F.code.assign(nslot * kFacNSC * L, 0);
-  F.vsrc.assign(nslot * kFacWF * L, -1);
+  pc.mark("positions");
+  {
+    const size_t nc = nslot * kFacNSC * L;
+    F.code.resize(nc);  // uninitialised, then zeroed in parallel
+    uint16_t* cp = F.code.data();
+#pragma omp parallel for schedule(static)
+    for (size_t x = 0; x < nc; ++x) cp[x] = 0;
+  }
+  big_fill(F.vsrc, nslot * kFacWF * L, -1);
   F.meta.assign(nslot * L, 0);
   F.rowStart.assign(nslot * L, 0);
   F.impNeed.assign(nslot, -1);
@@ -608,10 +689,13 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
     bool bad = false;
   };
   std::vector<BandOut> out(S.nbands);
+  pc.mark("alloc");
   // bands are independent (disjoint slots of the code arrays; imports per band): in parallel
-#pragma omp parallel for schedule(dynamic, 16)
+#pragma omp parallel
+  {
+  std::vector<int> impOf(n, -1);  // imported row -> import id (this thread's current band)
+#pragma omp for schedule(dynamic, 16)
   for (int b = 0; b < S.nbands; ++b) {
-    std::unordered_map<int, int> impOf;  // imported row -> import id (this band)
     std::vector<int> rows, first, last;  // per import id: row, first and last use
     std::vector<Use> uses;
     BandOut& bo = out[b];
@@ -625,12 +709,9 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
         F.meta[slot * L + l] = W | (nl << 8) | (1 << 16);
         F.rowStart[slot * L + l] = kb;
         for (int e = 0; e < W; ++e) F.vsrc[fac_vidx(slot, e, l)] = kb + e;
-        // the LDS index of U(j, c) for the row at iteration t
-        auto value = [&](int j, int c, size_t cell) {
-          const int* ub = jaf.data() + dg[j];
-          const int* ue = jaf.data() + iaf[j + 1];
-          const int* f = std::lower_bound(ub, ue, c);
-          const int pos = (int)(f - jaf.data());  // the caller checked that the entry exists
+        // the LDS index of U(j, .) at factor position pos (the caller found it) for the row at
+        // iteration t
+        auto value = [&](int j, int pos, size_t cell) {
           if (bandOf[j] == b && laneOf[j] <= l) {
             const size_t gj = (size_t)b * L + laneOf[j];
             const int d = t - (posOf[j] + S.laneSkew[gj]);
@@ -639,16 +720,12 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
               return;
             }
           }
-          auto it = impOf.find(j);
-          int id;
-          if (it == impOf.end()) {
+          int& id = impOf[j];
+          if (id < 0) {
             id = (int)rows.size();
-            impOf.emplace(j, id);
             rows.push_back(j);
             first.push_back(t);
             last.push_back(t);
-          } else {
-            id = it->second;
           }
           first[id] = std::min(first[id], t);
           last[id] = std::max(last[id], t);
@@ -656,15 +733,16 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
         };
         for (int q = 0; q < nl; ++q) {
           const int j = jaf[kb + q];
-          value(j, j, fac_cidx(slot, kFacNUpd + q, l));  // the pivot U(j, j)
-          // the targets of pivot q: entries e > q whose column lies in row j's upper part
-          const int* ub = jaf.data() + dg[j] + 1;
+          value(j, dg[j], fac_cidx(slot, kFacNUpd + q, l));  // the pivot U(j, j)
+          // the targets of pivot q: entries e > q whose column lies in row j's upper part (both
+          // column lists ascending: one merge walk)
+          const int* f = jaf.data() + dg[j] + 1;
           const int* ue = jaf.data() + iaf[j + 1];
-          for (int e = q + 1; e < W; ++e) {
+          for (int e = q + 1; e < W && f != ue; ++e) {
             const int c = jaf[kb + e];
             if (c <= j) continue;
-            const int* f = std::lower_bound(ub, ue, c);
-            if (f != ue && *f == c) value(j, c, fac_cidx(slot, fac_slot(e, q), l));
+            while (f != ue && *f < c) ++f;
+            if (f != ue && *f == c) value(j, (int)(f - jaf.data()), fac_cidx(slot, fac_slot(e, q), l));
           }
         }
       }
@@ -677,7 +755,10 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
     for (size_t q = 0; q < ord.size(); ++q) rank[ord[q]] = (int)q;
     int used = 0;
     bo.bad = !assign_import_slots(first, last, ord, RI, slotOf, waitOf, used);
-    if (bo.bad) continue;
+    if (bo.bad) {
+      for (int j : rows) impOf[j] = -1;
+      continue;
+    }
     bo.slots = used;
     for (const Use& u : uses) {
       const int k = rank[u.id];
@@ -691,7 +772,10 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
       bo.slot.push_back(slotOf[q]);
       bo.wait.push_back(waitOf[q]);
     }
+    for (int j : rows) impOf[j] = -1;
   }
+  }
+  pc.mark("bands");
   for (int b = 0; b < S.nbands; ++b) {
     const BandOut& bo = out[b];
     if (bo.bad) {
@@ -739,6 +823,7 @@ FactorSchedule build_factor_schedule(int n, const std::vector<int>& iaf, const s
         }
       }
   }
+  pc.mark("exports");
   F.ok = true;
   return F;
 }

@@ -23,10 +23,35 @@
 // Every row is computed by exactly the arithmetic of the level sweep (same entries, same order).
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace mmx {
+
+// an allocator whose resize() leaves ints uninitialised: the schedule's entry arrays (GBs at C4)
+// are then first touched by the parallel fills that set them, not by one thread's zeroing
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    if constexpr (sizeof...(A) == 0)
+      ::new ((void*)p) U;
+    else
+      ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+using BigVec = std::vector<int, NoInitAlloc<int>>;
+// v = n copies of x, filled in parallel
+void big_fill(BigVec& v, size_t n, int x);
 
 constexpr int kChainLanes = 64;
 constexpr int kChainRingMax = 32;    // LDS ring slots per lane (doubles) -- chain_sweep.hip kRingMax
@@ -57,8 +82,8 @@ struct ChainSchedule {
   std::vector<int> bandSlot, bandT, bandImp, bandNImp;  // per band
   std::vector<int> laneStart, laneLen, laneSkew;        // per band * 64 + lane (laneLen: rows if G = 2, else positions)
   std::vector<int> laneNs;                              // per band * 64 + lane: segments per row
-  std::vector<int> code;   // per ((slot * G + g) * E + e) * 64 + lane: LDS index of the value (0 for pads)
-  std::vector<int> src;    // same shape: index of the value in the factor (af), -1 for pads
+  BigVec code;   // per ((slot * G + g) * E + e) * 64 + lane: LDS index of the value (0 for pads)
+  BigVec src;    // same shape: index of the value in the factor (af), -1 for pads
   std::vector<int> dsrc;   // backward: per (slot * G + g) * 64 + lane, index of the diagonal in af (-1 idle)
   std::vector<int> impRow, impFree;  // per import: producer row; last iteration it is read
   std::vector<int> impSlot, impWait; // per import: LDS slot; iterations to complete before it is
@@ -71,9 +96,11 @@ struct ChainSchedule {
 };
 
 // fwd: unit-lower sweep over the entries [iaf[i], dg[i]); !fwd: upper sweep over (dg[i], iaf[i+1]).
-// forceG: rows per position (0: automatic).
+// forceG: rows per position (0: automatic).  codes = false: the geometry only (bands, lanes, skews,
+// slots, ring size, ticket order) -- no entry codes, sources or import tables (the factor schedule's
+// use: it lays its own stages over the forward geometry).
 ChainSchedule build_chain_schedule(int n, const std::vector<int>& iaf, const std::vector<int>& jaf,
-                                   const std::vector<int>& dg, bool fwd, int forceG = 0);
+                                   const std::vector<int>& dg, bool fwd, int forceG = 0, bool codes = true);
 
 // ---- the numeric ILU(0) factor on the same chain/band schedule (chain_factor.hip) ----------------
 // Row i of the factor (scaler_ILU::factor, ILU_class.cpp:300-527, IKJ order) restated target by
@@ -102,8 +129,8 @@ struct FactorSchedule {
   ChainSchedule geo;               // bands, lanes, skews, ticket order (forward, one row per position)
   int R = 0, RI = 0;
   long long slots = 0;
-  std::vector<uint16_t> code;      // [slot][kFacNSC][lane]: LDS index of each (e, q) value / pivot (0: none)
-  std::vector<int> vsrc;           // [slot][kFacWF][lane]: factor position of the row's entry e (-1: pad)
+  std::vector<uint16_t, NoInitAlloc<uint16_t>> code;  // [slot][kFacNSC][lane]: LDS index of each (e, q) value / pivot (0: none)
+  BigVec vsrc;                     // [slot][kFacWF][lane]: factor position of the row's entry e (-1: pad)
   std::vector<int> meta;           // [slot][lane]: W | nlow << 8 | 1 << 16 for a row (| 1 << 17 when
                                    // another band imports it: it publishes granules), 0 idle
   std::vector<int> rowStart;       // [slot][lane]: factor position of the row's first entry

@@ -4,6 +4,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -25,8 +31,27 @@ namespace {
 // (comm_poll.h), and so is every stream wait of a partitioned step (wait()), so a rank that never
 // joins or stops half-way ends the job with MMADMM_ERR_RCCL and a message naming the call, after
 // ncclCommAbort -- not with a hang.
+// The communicator's initialisation on a helper thread (RcclComm's constructor).  The helper owns
+// the non-blocking group: it polls ncclCommGetAsyncError until the initialisation is complete
+// before it exits (RCCL's asynchronous group job refers to the calling thread's thread-local group
+// state: a helper that returned early left it dangling -- measured, a segfault at one rank).  The
+// constructor, past its deadline, aborts the communicator itself while the helper is still
+// blocked in ncclGroupEnd, or asks the polling helper to abort it; `mu` orders the two.
+struct InitJob {
+  std::mutex mu;
+  int stage = 0;          // 1: handle known, 2: finished (res final)
+  bool polling = false;   // the helper is past ncclGroupEnd
+  bool aborted = false;   // ncclCommAbort was called (by either thread)
+  bool abortReq = false;  // the constructor asks the polling helper to abort
+  ncclComm_t comm = nullptr;
+  ncclResult_t res = ncclSuccess;
+  ncclUniqueId id;
+  ncclConfig_t cfg;
+};
+
 struct RcclComm final : Comm {
   ncclComm_t comm = nullptr;
+  std::shared_ptr<InitJob> initJob_;
   int rank = 0;
   double timeout = 300.0;
   hipEvent_t ev = nullptr;
@@ -39,8 +64,108 @@ struct RcclComm final : Comm {
     std::memcpy(&id, uid, sizeof(id));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
-    ncclResult_t r0 = ncclCommInitRankConfig(&comm, n, id, r, &cfg);
-    check(r0, "ncclCommInitRankConfig (every rank must create its communicator)");
+    // RCCL 2.27 blocks in the initialisation until every rank has joined even for a non-blocking
+    // communicator (measured on the box with a rank that never comes: ncclCommInitRankConfig alone,
+    // and ncclGroupEnd around it, never returned).  So it runs on a helper thread that hands over the
+    // communicator's handle first; this thread waits for it against the deadline and, past it,
+    // aborts the communicator (which ends the helper's wait) and reports MMADMM_ERR_RCCL.
+    // the job (with the id and the config RCCL may still read after the call returns) lives as
+    // long as this communicator, or as the helper thread if that outlives it
+    auto job = std::make_shared<InitJob>();
+    job->id = id;
+    job->cfg = cfg;
+    initJob_ = job;
+    std::thread th([job, n, r, device]() {
+      (void)hipSetDevice(device);
+      ncclResult_t a = ncclGroupStart();
+      ncclComm_t c = nullptr;
+      if (a == ncclSuccess) a = ncclCommInitRankConfig(&c, n, job->id, r, &job->cfg);
+      {
+        std::lock_guard<std::mutex> lk(job->mu);
+        job->comm = c;
+        job->stage = 1;
+      }
+      const ncclResult_t b = ncclGroupEnd();
+      ncclResult_t res = (a == ncclSuccess || a == ncclInProgress) ? b : a;
+      {
+        std::lock_guard<std::mutex> lk(job->mu);
+        job->polling = true;
+        if (job->aborted) {  // the constructor aborted while this thread was in ncclGroupEnd
+          job->res = ncclInternalError;
+          job->stage = 2;
+          return;
+        }
+      }
+      while (res == ncclInProgress) {
+        {
+          std::lock_guard<std::mutex> lk(job->mu);
+          if (job->abortReq) {
+            if (c) (void)ncclCommAbort(c);
+            job->aborted = true;
+            job->res = ncclInProgress;
+            job->stage = 2;
+            return;
+          }
+          ncclResult_t st = ncclInProgress;
+          if (ncclCommGetAsyncError(c, &st) != ncclSuccess) st = ncclInternalError;
+          res = st;
+        }
+        if (res == ncclInProgress) short_sleep();
+      }
+      std::lock_guard<std::mutex> lk(job->mu);
+      job->res = res;
+      job->stage = 2;
+    });
+    auto stage = [&] {
+      std::lock_guard<std::mutex> lk(job->mu);
+      return job->stage;
+    };
+    const int pr = poll_bounded([&] { return stage() == 2 ? kPollReady : kPollBusy; }, timeout, steady_seconds,
+                                short_sleep, 100);
+    if (pr == kPollOk) {
+      th.join();
+      if (dbg()) fprintf(stderr, "[mmx comm] rank %d: initialisation returned %d\n", rank, (int)job->res);
+      if (job->res != ncclSuccess) {
+        if (job->comm && !job->aborted) (void)ncclCommAbort(job->comm);
+        throw Error(MMADMM_ERR_RCCL, "rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                                         ": ncclCommInitRankConfig: " + ncclGetErrorString(job->res));
+      }
+      comm = job->comm;
+      return;
+    }
+    // past the deadline: abort -- here if the helper is blocked in ncclGroupEnd (the abort ends that
+    // wait), else through the helper -- give it a little while to return, then report; a helper that
+    // still does not return is left detached
+    if (dbg()) fprintf(stderr, "[mmx comm] rank %d: initialisation past its deadline\n", rank);
+    while (stage() < 1) short_sleep();  // the handle comes at once (the call queues in the group)
+    {
+      bool here = false;
+      ncclComm_t c = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(job->mu);
+        if (job->stage < 2) {
+          if (job->polling) {
+            job->abortReq = true;
+          } else {
+            job->aborted = true;
+            here = true;
+            c = job->comm;
+          }
+        }
+      }
+      if (here && c) (void)ncclCommAbort(c);
+    }
+    const int pr2 = poll_bounded([&] { return stage() == 2 ? kPollReady : kPollBusy; }, 20.0, steady_seconds,
+                                 short_sleep, 100);
+    if (pr2 == kPollOk)
+      th.join();
+    else
+      th.detach();
+    comm = nullptr;
+    throw Error(MMADMM_ERR_RCCL, "rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                                     ": ncclCommInitRankConfig (every rank must create its communicator): not complete "
+                                     "after " + std::to_string(timeout) +
+                                     " s (MMX_COMM_TIMEOUT_S) -- a peer rank is missing or stuck; communicator aborted");
   }
   ~RcclComm() override {
     if (ev) (void)hipEventDestroy(ev);
@@ -67,8 +192,14 @@ struct RcclComm final : Comm {
         timeout, steady_seconds, short_sleep);
     return pr == kPollTimeout ? ncclInProgress : last;
   }
+  static bool dbg() {
+    static const bool on = getenv("MMX_COMM_DEBUG") != nullptr;
+    return on;
+  }
   [[noreturn]] void fail(const std::string& msg) {
+    if (dbg()) fprintf(stderr, "[mmx comm] rank %d: %s -- aborting the communicator\n", rank, msg.c_str());
     if (comm) (void)ncclCommAbort(comm);
+    if (dbg()) fprintf(stderr, "[mmx comm] rank %d: ncclCommAbort returned\n", rank);
     comm = nullptr;
     throw Error(MMADMM_ERR_RCCL, "rank " + std::to_string(rank) + " of " + std::to_string(nranks) + ": " + msg);
   }

@@ -777,8 +777,17 @@ class Engine final : public EngineBase {
 
   // buildMatrix (src/Mesh.cpp:262-382): the Jacobian's pattern over the D*nP unknowns, the
   // ParamIter of the reference and the symbolic ILU (sfac, done once as the reference does).
+  // MMX_SCHED_PROF=1: the first backward-Euler step's host set-up phases on stderr
+  static void profMark(const char* what, std::chrono::steady_clock::time_point& t) {
+    static const bool on = getenv("MMX_SCHED_PROF") != nullptr;
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[sched] engine %s %.3f s\n", what, std::chrono::duration<double>(now - t).count());
+    t = now;
+  }
   void ensureJacobian() {
     if (jac_) return;
+    auto tp = std::chrono::steady_clock::now();
     const int n = nP_ * D;
     mmx_struc sp = nullptr;
     MMX_SP(mmx_struc_create(n, 0, &sp));
@@ -791,10 +800,12 @@ class Engine final : public EngineBase {
       ja.resize(nnz);
       rc = mmx_struc_get(sp, nullptr, &nnz, ia.data(), ja.data());
     }
+    profMark("pattern", tp);
     int dev = prm_.device;
     if (dev < 0) MMX_HIP(hipGetDevice(&dev));
     if (rc == MMADMM_OK) rc = mmx_matrix_create_from_struc(dev, sp, &jac_);
     (void)mmx_struc_destroy(sp);
+    profMark("matrix create", tp);
     if (rc != MMADMM_OK) throw Error(rc, std::string("backward Euler Jacobian: ") + mmadmm_last_error());
     mmx_param_iter_mesh(&jprm_);
     jia_.upload(ia.data(), ia.size(), st_);
@@ -816,15 +827,18 @@ class Engine final : public EngineBase {
     jacVp_ = vpVersion_;
     jacDt_ = dtBE;
     const auto t0 = Clock::now();
+    auto tp = t0;
     const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
     launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
     clearInvFlag();
     launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, dtBE / prm_.tau, jval_.p, st_);
     streamWait();
+    profMark("FD Jacobian + assembly", tp);
     MMX_SP(mmx_matrix_set_values_device(jac_, jval_.p));
     if (!jacFactored_) {
       MMX_SP(mmx_matrix_sfac(jac_, &jprm_));
       jacFactored_ = true;
+      profMark("sfac", tp);
     }
     streamWait();
     st_stats_.jacobians += 1;

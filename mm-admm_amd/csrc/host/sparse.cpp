@@ -1,10 +1,16 @@
 // sparse.cpp -- host side of the LASolver replacement (include/mmx_sparse.h): MatrixStruc
 // packing, the symbolic ILU (level of fill, natural order) and the device-resident MatrixIter
 // whose numeric factor, sweeps, SpMV and CG-STAB run as HIP kernels (kernels/sparse_kernels.hip).
+#include <omp.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/mmx_sparse.h"
@@ -17,6 +23,20 @@ namespace {
 
 // MatrixStruc (lib/LASolver/MatrixIter.cpp:88-257): per-row column lists; pack() sorts each row
 // ascending and removes duplicates; the diagonal is present unless no_diag.
+// MMX_SCHED_PROF=1: phase times of the host set-up on stderr
+struct PhaseTimer {
+  bool on;
+  const char* who;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseTimer(const char* w) : on(getenv("MMX_SCHED_PROF") != nullptr), who(w), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[sched] %s %s %.3f s\n", who, what, std::chrono::duration<double>(now - t).count());
+    t = now;
+  }
+};
+
 struct Struc {
   int n = 0;
   bool packed = false;
@@ -26,13 +46,15 @@ struct Struc {
   void pack() {
     if (packed) throw Error(MMADMM_ERR_INVALID, "error: data structure already packed");
     ia.assign(n + 1, 0);
+#pragma omp parallel for schedule(dynamic, 4096)
     for (int i = 0; i < n; ++i) {
       auto& r = rows[i];
       if (!std::is_sorted(r.begin(), r.end())) std::sort(r.begin(), r.end());
       r.erase(std::unique(r.begin(), r.end()), r.end());
-      ia[i + 1] = ia[i] + (int)r.size();
     }
+    for (int i = 0; i < n; ++i) ia[i + 1] = ia[i] + (int)rows[i].size();
     ja.resize(ia[n]);
+#pragma omp parallel for schedule(dynamic, 4096)
     for (int i = 0; i < n; ++i) {
       std::copy(rows[i].begin(), rows[i].end(), ja.begin() + ia[i]);
       std::vector<int>().swap(rows[i]);
@@ -51,16 +73,35 @@ void symbolic_ilu(int n, const std::vector<int>& ia, const std::vector<int>& ja,
     iaf.assign(ia.begin(), ia.begin() + n + 1);
     jaf.assign(ja.begin(), ja.begin() + ia[n]);
     dgRel.assign(n, -1);
+    // rows in parallel; the first bad row (lowest index) is reported, as the sequential loop would
+    int bad = n, why = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(min : bad)
     for (int i = 0; i < n; ++i) {
       int* b = jaf.data() + iaf[i];
       int* e = jaf.data() + iaf[i + 1];
-      if (b == e) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " is empty (no diagonal)");
+      if (b == e) {
+        bad = std::min(bad, i);
+        continue;
+      }
       std::sort(b, e);
-      for (int* q = b + 1; q < e; ++q)
-        if (*q == q[-1]) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has duplicate columns");
+      bool dup = false;
+      for (int* q = b + 1; q < e; ++q) dup |= (*q == q[-1]);
       int* d = std::lower_bound(b, e, i);
-      if (d == e || *d != i) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has no diagonal entry");
+      if (dup || d == e || *d != i) {
+        bad = std::min(bad, i);
+        continue;
+      }
       dgRel[i] = (int)(d - b);
+    }
+    if (bad < n) {
+      const int* b = jaf.data() + iaf[bad];
+      const int* e = jaf.data() + iaf[bad + 1];
+      bool dup = false;
+      for (const int* q = b + 1; q < e; ++q) dup |= (*q == q[-1]);
+      why = (b == e) ? 0 : dup ? 1 : 2;
+      throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(bad) +
+                                          (why == 0 ? " is empty (no diagonal)" : why == 1 ? " has duplicate columns"
+                                                                                           : " has no diagonal entry"));
     }
     return;
   }
@@ -291,11 +332,46 @@ struct SparseMatrix {
 
   void sfac(const mmx_param_iter& p) {
     check_params(p);
+    PhaseTimer pt("sfac");
     symbolic_ilu(n, ia, ja, p.level, iaf, jaf, dgRel);
+    pt.mark("symbolic");
     level = p.level;
     std::vector<int> dg(n), amap(nnz);
+    for (int i = 0; i < n; ++i) dg[i] = iaf[i] + dgRel[i];
+    // the sweep and factor schedules (the bulk of the host set-up: DESIGN.md §7b) depend only on the
+    // factor's pattern: built on helper threads while this one prepares the rest
+    const char* smode = getenv("MMX_SWEEP");
+    const bool tryChain = !(smode && std::strcmp(smode, "level") == 0);
+    const char* fmode = getenv("MMX_FACTOR");
+    const bool tryChainFactor = !(fmode && (std::strcmp(fmode, "level") == 0 || std::strcmp(fmode, "global") == 0));
+    ChainSchedule Fs, Bs;
+    FactorSchedule FS;
+    std::vector<std::thread> helpers;
+    std::exception_ptr helperErr[2];
+    const int nt = std::max(1, omp_get_max_threads());
+    auto helper = [&](int slot, auto fn) {
+      helpers.emplace_back([&, slot, fn, nt] {
+        try {
+          omp_set_num_threads(std::max(1, nt / 2));
+          fn();
+        } catch (...) {
+          helperErr[slot] = std::current_exception();
+        }
+      });
+    };
+    if (tryChain) {
+      helper(0, [&] { Bs = build_chain_schedule(n, iaf, jaf, dg, false); });
+      if (tryChainFactor) helper(1, [&] { FS = build_factor_schedule(n, iaf, jaf, dg); });
+    }
+    struct Joiner {  // the helpers reference this frame: joined on every way out of it
+      std::vector<std::thread>& h;
+      ~Joiner() {
+        for (auto& t : h)
+          if (t.joinable()) t.join();
+      }
+    } joiner{helpers};
+#pragma omp parallel for schedule(dynamic, 4096)
     for (int i = 0; i < n; ++i) {
-      dg[i] = iaf[i] + dgRel[i];
       const int* b = jaf.data() + iaf[i];
       const int* e = jaf.data() + iaf[i + 1];
       for (int k = ia[i]; k < ia[i + 1]; ++k) amap[k] = (int)(std::lower_bound(b, e, ja[k]) - jaf.data());
@@ -306,6 +382,7 @@ struct SparseMatrix {
     d_amap.upload(amap.data(), std::max<size_t>(amap.size(), 1), st);
     d_af.alloc(std::max<size_t>(jaf.size(), 1));
     factVersion = -1;
+    pt.mark("amap + uploads");
     {  // pivot-row upper ranges of every lower entry (the factor's dependent loads, precomputed)
       std::vector<int2> pv(std::max<size_t>(jaf.size(), 1), make_int2(0, 0));
       for (int i = 0; i < n; ++i)
@@ -324,9 +401,12 @@ struct SparseMatrix {
         }
       const char* fm = getenv("MMX_FACTOR");
       facLds = maxW <= kFacW && tot < (1ll << 31) && !(fm && std::strcmp(fm, "global") == 0);
+      pt.mark("pivot ranges");
       if (facLds) {
+        // every target cell is written once below: no initialisation pass over the (C4: ~0.5 GB) array
         std::vector<int> toff(off.size());
-        std::vector<signed char> tg(std::max<long long>(tot, 1), -1);
+        std::vector<signed char, NoInitAlloc<signed char>> tg(std::max<long long>(tot, 1));
+        if (tot == 0) tg[0] = -1;
 #pragma omp parallel for schedule(dynamic, 4096)
         for (int i = 0; i < n; ++i) {
           const int* rb = jaf.data() + iaf[i];
@@ -334,19 +414,27 @@ struct SparseMatrix {
           for (int k = iaf[i]; k < dg[i]; ++k) {
             toff[k] = (int)off[k];
             const int id = jaf[k];
+            signed char* out = tg.data() + off[k] - (dg[id] + 1);
+            const int* f = rb;  // both column lists ascending: one merge walk
             for (int pp = dg[id] + 1; pp < iaf[id + 1]; ++pp) {
-              const int* f = std::lower_bound(rb, re, jaf[pp]);
-              tg[off[k] + (pp - dg[id] - 1)] = (f != re && *f == jaf[pp]) ? (signed char)(f - rb) : (signed char)-1;
+              const int c = jaf[pp];
+              while (f != re && *f < c) ++f;
+              out[pp] = (f != re && *f == c) ? (signed char)(f - rb) : (signed char)-1;
             }
           }
         }
+        pt.mark("update targets");
         d_toff.upload(toff.data(), toff.size(), st);
         d_tgt.upload(tg.data(), tg.size(), st);
+        MMX_HIP(hipStreamSynchronize(st));  // (the host images go out of scope)
+        pt.mark("update targets upload");
       }
     }
-    // level schedules of the lower (forward sweep, factor) and upper (backward sweep) factor
-    std::vector<int> lev(n);
+    // level schedules of the lower (forward sweep, factor) and upper (backward sweep) factor: the
+    // two concurrently; the forward levels are kept for the wave factor's row order
+    std::vector<int> levF(n), levB(n);
     auto schedule = [&](bool fwd, DevBuf<int>& out, int& nch, int& nlev) {
+      std::vector<int>& lev = fwd ? levF : levB;
       int maxl = 0;
       for (int t = 0; t < n; ++t) {
         const int i = fwd ? t : n - 1 - t;
@@ -367,20 +455,33 @@ struct SparseMatrix {
         perm[fill[lev[i]]++] = i;
       }
       nch = start[nlev] / kSweepRows;
-      out.upload(perm.data(), perm.size(), st);
+      return perm;
     };
-    schedule(true, d_permf, nchf, nlevf);
-    schedule(false, d_permb, nchb, nlevb);
+    std::vector<int> permF, permB;
+#pragma omp parallel sections num_threads(2)
+    {
+#pragma omp section
+      permF = schedule(true, d_permf, nchf, nlevf);
+#pragma omp section
+      permB = schedule(false, d_permb, nchb, nlevb);
+    }
+    d_permf.upload(permF.data(), permF.size(), st);
+    d_permb.upload(permB.data(), permB.size(), st);
+    pt.mark("level schedules");
     useChain = false;
-    const char* mode = getenv("MMX_SWEEP");
-    if (!(mode && std::strcmp(mode, "level") == 0)) {
-      const ChainSchedule F = build_chain_schedule(n, iaf, jaf, dg, true);
-      const ChainSchedule B = F.ok ? build_chain_schedule(n, iaf, jaf, dg, false) : ChainSchedule();
-      if (F.ok && B.ok) {
-        upload_chain(F, chf);
-        upload_chain(B, chb);
+    if (tryChain) {
+      Fs = build_chain_schedule(n, iaf, jaf, dg, true);
+      pt.mark("forward chain schedule");
+      for (auto& h : helpers) h.join();
+      for (auto& e : helperErr)
+        if (e) std::rethrow_exception(e);
+      pt.mark("backward + factor schedules (joined)");
+      if (Fs.ok && Bs.ok) {
+        upload_chain(Fs, chf);
+        upload_chain(Bs, chb);
         useChain = true;
       }
+      pt.mark("chain uploads");
     }
     useChainFactor = false;
     facWave = false;
@@ -388,9 +489,8 @@ struct SparseMatrix {
       // default where the rows fit its layout (2D): bit-identical to the level schedule and
       // 12.3 ms against 25.0 ms at n = 2 M (profiles/r03/chain_factor/);
       // MMX_FACTOR=level (or global) keeps the level-scheduled factor
-      const char* fm = getenv("MMX_FACTOR");
-      if (useChain && !(fm && (std::strcmp(fm, "level") == 0 || std::strcmp(fm, "global") == 0))) {
-        const FactorSchedule FS = build_factor_schedule(n, iaf, jaf, dg);
+      const char* fm = fmode;
+      if (useChain && tryChainFactor) {
         if (FS.ok && !(fm && std::strcmp(fm, "wave") == 0)) {
           upload_factor(FS, dg);
           useChainFactor = true;
@@ -409,15 +509,10 @@ struct SparseMatrix {
             stamp[amap[k]] = i;
           }
         }
-        if (fits) {  // every row once, in forward level order
-          std::vector<int> lv(n, 0), cnt;
-          int nl = 0;
-          for (int i = 0; i < n; ++i) {
-            int l = 0;
-            for (int k = iaf[i]; k < dg[i]; ++k) l = std::max(l, lv[jaf[k]] + 1);
-            lv[i] = l;
-            nl = std::max(nl, l + 1);
-          }
+        if (fits) {  // every row once, in forward level order (the forward sweep's levels)
+          const std::vector<int>& lv = levF;
+          std::vector<int> cnt;
+          const int nl = nlevf;
           cnt.assign(nl + 1, 0);
           for (int i = 0; i < n; ++i) cnt[lv[i] + 1]++;
           for (int l = 0; l < nl; ++l) cnt[l + 1] += cnt[l];
@@ -439,7 +534,7 @@ struct SparseMatrix {
       }
     }
     MMX_HIP(hipStreamSynchronize(st));
-    MMX_HIP(hipStreamSynchronize(st));
+    pt.mark("factor set-up + uploads");
     symbolic = true;
   }
 
@@ -448,7 +543,7 @@ struct SparseMatrix {
     return (e && atoi(e) == 0) ? 0 : 1;
   }
   void upload_chain(const ChainSchedule& S, ChainDir& c) {
-    auto up = [&](DevBuf<int>& d, const std::vector<int>& h) {
+    auto up = [&](DevBuf<int>& d, const auto& h) {
       if (h.empty()) {
         const int z = 0;
         d.upload(&z, 1, st);
@@ -470,12 +565,13 @@ struct SparseMatrix {
     // same entry ranges either way
     const int EEs = S.E * S.G;
     const size_t blocks = S.code.size() / ((size_t)S.E * kChainLanes);
-    auto permute = [&](const std::vector<int>& lg, int W) {
-      std::vector<int> ph(lg.size());
+    auto permute = [&](const BigVec& lg, int W) {
+      BigVec ph;
       if (!MMX_CHAIN_VEC) {
         ph = lg;
         return ph;
       }
+      ph.resize(lg.size());  // uninitialised: every element is written below
       const int E = S.E, L = kChainLanes;
 #pragma omp parallel for schedule(static)
       for (long long bk = 0; bk < (long long)blocks; ++bk) {
@@ -488,12 +584,14 @@ struct SparseMatrix {
     (void)EEs;
     const void* codePtr;
     const bool c16on = chain_code16(S.E * S.G);
-    const std::vector<int> pcode = permute(S.code, c16on ? 8 : 4), psrc = permute(S.src, 2);
+    const BigVec pcode = permute(S.code, c16on ? 8 : 4), psrc = permute(S.src, 2);
     std::vector<uint16_t> c16;
     if (S.E > 32 && (S.seg || S.G != 1 || S.R > kChainRingWide))
       throw Error(MMADMM_ERR_INVALID, "wide chain stage layout");
     if (c16on) {  // 16-bit codes (validate_chain_schedule: every index fits)
-      c16.assign(pcode.begin(), pcode.end());
+      c16.resize(pcode.size());
+#pragma omp parallel for schedule(static)
+      for (size_t x = 0; x < pcode.size(); ++x) c16[x] = (uint16_t)pcode[x];
       c.code16.upload(c16.data(), std::max<size_t>(c16.size(), 1), st);
       codePtr = c.code16.p;
     } else {
@@ -527,7 +625,7 @@ struct SparseMatrix {
   }
 
   void upload_factor(const FactorSchedule& F, const std::vector<int>& dg) {
-    auto up = [&](DevBuf<int>& d, const std::vector<int>& h) {
+    auto up = [&](DevBuf<int>& d, const auto& h) {
       if (h.empty()) {
         const int z = 0;
         d.upload(&z, 1, st);
@@ -856,6 +954,7 @@ int mmx_struc_mesh_pattern(mmx_struc s, int dim, int nF, const int32_t* F) {
         const int va = F[(size_t)t * (D + 1) + a];
         for (int b = 0; b <= D; ++b) nb[fill[va]++] = F[(size_t)t * (D + 1) + b];
       }
+#pragma omp parallel for schedule(dynamic, 4096)
     for (int v = 0; v < nP; ++v) {
       int* b = nb.data() + cnt[v];
       int* e = std::unique(b, (std::sort(b, nb.data() + cnt[v + 1]), nb.data() + cnt[v + 1]));

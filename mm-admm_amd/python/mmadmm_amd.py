@@ -434,7 +434,10 @@ class Comm:
             self.h = None
 
     def __del__(self):
-        _close_at_exit(self)
+        try:
+            _close_at_exit(self)
+        except TypeError:  # interpreter shutdown: the module's globals are gone
+            pass
 
 
 def _abort(transport):
@@ -556,7 +559,10 @@ class Engine:
             self.h = None
 
     def __del__(self):
-        _close_at_exit(self)
+        try:
+            _close_at_exit(self)
+        except TypeError:  # interpreter shutdown: the module's globals are gone
+            pass
 
     def step(self, nIters, tol=1e-3):
         Ih = ctypes.c_double()

@@ -80,7 +80,12 @@ def test_mismatched_objects_fail_at_create():
     if not os.path.exists(os.path.join(BUILD, "engine.o")):
         pytest.skip("library objects not built (run __graft_entry__.build())")
     lib = _mismatched_lib()
-    out = _run_create(lib)
+    try:
+        out = _run_create(lib)
+    finally:  # a test artefact: not left in the tree (it would travel with every GPU call)
+        for f in (lib, os.path.join(OUT, "engine_zuinter.o")):
+            if os.path.exists(f):
+                os.remove(f)
     # the LASolver side (sparse.cpp) was built with the kernels' flags: its check passes
     assert out["LAYOUT"].split()[0] == "0"
     rc, msg = out["CREATE"].split(" ", 1)
