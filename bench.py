@@ -906,10 +906,14 @@ def main():
     if world > 1:
         phase("report")
     st = eng.stats()
-    per_rank = [(eng.nP, eng.nF)]
+    # per rank: local nodes and simplices, the halo exchange's device time per ADMM iteration (pack +
+    # send/recv on its stream, overlapped with the interior x-update), its bytes, the interior nodes
+    mine = (eng.nP, eng.nF, (st["t_exchange_ms"] * 1e3 / st["n_exchange"]) if st["n_exchange"] else None,
+            st["halo_send_bytes"], st["halo_recv_bytes"], st["interior_nodes"], st["overlap"])
+    per_rank = [mine]
     if world > 1:
         per_rank = [None] * world
-        dist.all_gather_object(per_rank, (eng.nP, eng.nF))
+        dist.all_gather_object(per_rank, mine)
     # a second run with the early exit enabled reports the iterations actually executed
     eng.reset_stats()
     for _ in range(3):
@@ -957,6 +961,14 @@ def main():
                    "simplices_rank0": eng.nF, "nodes_per_rank": [p[0] for p in per_rank],
                    "simplices_per_rank": [p[1] for p in per_rank], "rccl_nranks": rccl_nranks,
                    "comm_nranks": (comm_nranks if world > 1 else None),
+                   "exchange_us_per_iter": ([None if p[2] is None else round(p[2], 2) for p in per_rank]
+                                            if world > 1 else None),
+                   "halo_bytes_per_iter": ([{"send": int(p[3]), "recv": int(p[4])} for p in per_rank]
+                                           if world > 1 else None),
+                   "interior_nodes_per_rank": ([p[5] for p in per_rank] if world > 1 else None),
+                   "halo_overlap": (bool(per_rank[0][6]) if world > 1 else None),
+                   "imbalance": (round(max(p[1] for p in per_rank) / (sum(p[1] for p in per_rank) / world), 4)
+                                 if world > 1 else None),
                    "admm_iter": args.admm_iter, "parallelism": parallelism,
                    "comm": (args.comm if world > 1 else None),
                    "value_unit_note": "ADMM it/s x global nodes / %d" % base_nodes},

@@ -116,6 +116,10 @@ def test_bench_two_ranks_host_transport_rehearsal():
     assert cfg["parallelism"].startswith("element-partition x2") and cfg["comm"] == "host"
     assert cfg["comm_nranks"] == 2 and cfg["rccl_nranks"] is None and len(cfg["nodes_per_rank"]) == 2
     assert sum(cfg["simplices_per_rank"]) == cfg["global_simplices"]
+    # the halo exchange per rank (round 6): device time per ADMM iteration, bytes, overlap, balance
+    assert len(cfg["exchange_us_per_iter"]) == 2 and all(v and v > 0 for v in cfg["exchange_us_per_iter"])
+    assert all(h["send"] > 0 and h["recv"] > 0 for h in cfg["halo_bytes_per_iter"])
+    assert cfg["halo_overlap"] is True and 1.0 <= cfg["imbalance"] < 1.01
     assert d["value"] > 0 and d["early_exit"]["admm_iters_per_step"] > 0
 
 
