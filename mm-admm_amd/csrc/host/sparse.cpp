@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -40,26 +41,58 @@ struct PhaseTimer {
 struct Struc {
   int n = 0;
   bool packed = false;
-  std::vector<std::vector<int>> rows;
+  bool diag = false;  // every row holds its diagonal (MatrixStruc(n), no_diag = 0): implicit until pack
+  std::vector<std::vector<int>> rows;  // entries set one at a time (set_entry)
+  // entries of mesh_pattern in bulk, as a CSR whose rows are sorted and duplicate-free (no
+  // per-row allocations: 1.5 M rows at C4)
+  std::vector<int> bia, bja;
   std::vector<int> ia, ja;
 
   void pack() {
     if (packed) throw Error(MMADMM_ERR_INVALID, "error: data structure already packed");
     ia.assign(n + 1, 0);
-#pragma omp parallel for schedule(dynamic, 4096)
-    for (int i = 0; i < n; ++i) {
-      auto& r = rows[i];
+    const bool bulk = !bia.empty();
+    // row i = sorted union of {i} (diag), rows[i] and bulk row i: sizes first, then the entries
+    std::vector<int> cnt(n, 0);
+    auto merged = [&](int i, int* out) {  // writes the row (out != nullptr) and returns its length
+      std::vector<int>& r = rows[i];
       if (!std::is_sorted(r.begin(), r.end())) std::sort(r.begin(), r.end());
       r.erase(std::unique(r.begin(), r.end()), r.end());
-    }
-    for (int i = 0; i < n; ++i) ia[i + 1] = ia[i] + (int)rows[i].size();
+      const int* b = bulk ? bja.data() + bia[i] : nullptr;
+      const int* be = bulk ? bja.data() + bia[i + 1] : nullptr;
+      const int* a = r.data();
+      const int* ae = r.data() + r.size();
+      bool dpend = diag;
+      int len = 0, last = -1;
+      while (true) {
+        int v = INT32_MAX;
+        if (a != ae) v = std::min(v, *a);
+        if (b != be) v = std::min(v, *b);
+        if (dpend) v = std::min(v, i);
+        if (v == INT32_MAX) break;
+        if (a != ae && *a == v) ++a;
+        if (b != be && *b == v) ++b;
+        if (dpend && v == i) dpend = false;
+        if (v != last) {
+          if (out) out[len] = v;
+          ++len;
+          last = v;
+        }
+      }
+      return len;
+    };
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int i = 0; i < n; ++i) cnt[i] = merged(i, nullptr);
+    for (int i = 0; i < n; ++i) ia[i + 1] = ia[i] + cnt[i];
     ja.resize(ia[n]);
 #pragma omp parallel for schedule(dynamic, 4096)
     for (int i = 0; i < n; ++i) {
-      std::copy(rows[i].begin(), rows[i].end(), ja.begin() + ia[i]);
+      merged(i, ja.data() + ia[i]);
       std::vector<int>().swap(rows[i]);
     }
     rows.clear();
+    std::vector<int>().swap(bia);
+    std::vector<int>().swap(bja);
     packed = true;
   }
 };
@@ -384,21 +417,34 @@ struct SparseMatrix {
     factVersion = -1;
     pt.mark("amap + uploads");
     {  // pivot-row upper ranges of every lower entry (the factor's dependent loads, precomputed)
-      std::vector<int2> pv(std::max<size_t>(jaf.size(), 1), make_int2(0, 0));
-      for (int i = 0; i < n; ++i)
+      std::vector<int2> pv(std::max<size_t>(jaf.size(), 1));
+#pragma omp parallel for schedule(dynamic, 4096)
+      for (int i = 0; i < n; ++i) {
         for (int k = iaf[i]; k < dg[i]; ++k) pv[k] = make_int2(dg[jaf[k]], iaf[jaf[k] + 1]);
+        for (int k = dg[i]; k < iaf[i + 1]; ++k) pv[k] = make_int2(0, 0);
+      }
       d_piv.upload(pv.data(), pv.size(), st);
+      MMX_HIP(hipStreamSynchronize(st));  // (pv goes out of scope)
     }
     {  // update positions for the LDS-row factor (rows of at most kFacW entries)
       int maxW = 0;
-      for (int i = 0; i < n; ++i) maxW = std::max(maxW, iaf[i + 1] - iaf[i]);
-      std::vector<long long> off(std::max<size_t>(jaf.size(), 1), 0);
-      long long tot = 0;
-      for (int i = 0; i < n; ++i)
+      std::vector<long long> off(std::max<size_t>(jaf.size(), 1), 0), rowTot(n + 1, 0);
+      // per row: its lower entries' pivot upper lengths (prefix within the row), then a scan of rows
+#pragma omp parallel for schedule(dynamic, 4096) reduction(max : maxW)
+      for (int i = 0; i < n; ++i) {
+        maxW = std::max(maxW, iaf[i + 1] - iaf[i]);
+        long long t = 0;
         for (int k = iaf[i]; k < dg[i]; ++k) {
-          off[k] = tot;
-          tot += iaf[jaf[k] + 1] - dg[jaf[k]] - 1;
+          off[k] = t;
+          t += iaf[jaf[k] + 1] - dg[jaf[k]] - 1;
         }
+        rowTot[i + 1] = t;
+      }
+      for (int i = 0; i < n; ++i) rowTot[i + 1] += rowTot[i];
+      const long long tot = rowTot[n];
+#pragma omp parallel for schedule(dynamic, 4096)
+      for (int i = 0; i < n; ++i)
+        for (int k = iaf[i]; k < dg[i]; ++k) off[k] += rowTot[i];
       const char* fm = getenv("MMX_FACTOR");
       facLds = maxW <= kFacW && tot < (1ll << 31) && !(fm && std::strcmp(fm, "global") == 0);
       pt.mark("pivot ranges");
@@ -906,8 +952,7 @@ int mmx_struc_create(int n, int no_diag, mmx_struc* out) {
     auto* h = new mmx_struc_s;
     h->s.n = n;
     h->s.rows.resize(n);
-    if (no_diag == 0)
-      for (int i = 0; i < n; ++i) h->s.rows[i].push_back(i);
+    h->s.diag = (no_diag == 0);  // (implicit until pack: no n one-entry allocations)
     *out = h;
   });
 }
@@ -954,17 +999,36 @@ int mmx_struc_mesh_pattern(mmx_struc s, int dim, int nF, const int32_t* F) {
         const int va = F[(size_t)t * (D + 1) + a];
         for (int b = 0; b <= D; ++b) nb[fill[va]++] = F[(size_t)t * (D + 1) + b];
       }
+    std::vector<int> nu(nP);  // distinct neighbours (itself included) of every node
 #pragma omp parallel for schedule(dynamic, 4096)
     for (int v = 0; v < nP; ++v) {
       int* b = nb.data() + cnt[v];
-      int* e = std::unique(b, (std::sort(b, nb.data() + cnt[v + 1]), nb.data() + cnt[v + 1]));
-      for (int d = 0; d < D; ++d) {
-        auto& r = s->s.rows[v * D + d];
-        r.reserve(r.size() + (size_t)(e - b) * D);
-        for (const int* u = b; u < e; ++u)
-          for (int c = 0; c < D; ++c) r.push_back(*u * D + c);
-      }
+      std::sort(b, nb.data() + cnt[v + 1]);
+      nu[v] = (int)(std::unique(b, nb.data() + cnt[v + 1]) - b);
     }
+    auto& S = s->s;
+    if (!S.bia.empty()) {  // a second mesh pattern (rare): into the per-row lists
+      for (int v = 0; v < nP; ++v)
+        for (int d = 0; d < D; ++d) {
+          auto& r = S.rows[v * D + d];
+          for (int q = 0; q < nu[v]; ++q)
+            for (int c = 0; c < D; ++c) r.push_back(nb[cnt[v] + q] * D + c);
+        }
+      return;
+    }
+    // the bulk CSR: row v D + d holds (u D + c) for the neighbours u (ascending) and c < D
+    S.bia.assign((size_t)S.n + 1, 0);
+    for (int v = 0; v < nP; ++v)
+      for (int d = 0; d < D; ++d) S.bia[(size_t)v * D + d + 1] = nu[v] * D;
+    for (int i = 0; i < S.n; ++i) S.bia[i + 1] += S.bia[i];
+    S.bja.resize(S.bia[S.n]);
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int v = 0; v < nP; ++v)
+      for (int d = 0; d < D; ++d) {
+        int* o = S.bja.data() + S.bia[(size_t)v * D + d];
+        for (int q = 0; q < nu[v]; ++q)
+          for (int c = 0; c < D; ++c) *o++ = nb[cnt[v] + q] * D + c;
+      }
   });
 }
 
