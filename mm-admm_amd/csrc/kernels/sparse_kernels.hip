@@ -516,23 +516,23 @@ __global__ void __launch_bounds__(kSweepRows) k_ilu_factor_lds(const int* __rest
 // and every lane with a target subtracts mult * U at once (distinct targets; LDS in order within
 // the wavefront) -- the operations of k_ilu_factor in the same order, so bit-identical.  NL: lower
 // entries per row, at most; upper parts of at most 64 entries (host-checked).
-template <int NL, bool GR>
-__global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__ ia, const double* __restrict__ a,
+template <int NL, bool GR, int WG = 4>
+__global__ void __launch_bounds__(64 * WG) k_ilu_factor_wave(const int* __restrict__ ia, const double* __restrict__ a,
                                                          const int* __restrict__ amap, const int* __restrict__ iaf,
                                                          const int* __restrict__ dg, const int2* __restrict__ piv,
                                                          const int* __restrict__ jaf, const int* __restrict__ toff,
                                                          const signed char* __restrict__ tgt, const int* __restrict__ perm,
-                                                         int nrows, unsigned* ticket, double* af, unsigned* flags,
-                                                         uint64_t* gF, unsigned epoch, unsigned* err) {
-  __shared__ double s_row[4][kFacW + 1];
+                                                         int nrows, int chunk, unsigned* ticket, double* af,
+                                                         unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* err) {
+  __shared__ double s_row[WG][kFacW + 1];
   const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
   double* w = s_row[wv];
   // lane 0 takes the wave's tickets (the value is read only where it is needed: the next ticket's
-  // round trip overlaps the current row)
-  auto take = [&]() -> unsigned { return lane == 0 ? atomicAdd(ticket, 1u) : 0u; };
-  unsigned tk = take();
-  for (int x = (int)__shfl(tk, 0); x < nrows; x = (int)__shfl(tk, 0)) {
-    tk = take();  // the next row's ticket
+  // round trip overlaps the current chunk).  A ticket is a chunk of `chunk` consecutive rows of the
+  // order, done in order by the wave: one ticket per row made the single counter's device-scope
+  // atomics (~7 ns each, serialised) the factor's bottleneck -- C4 11.2 -> 20.9 ms
+  // one row: false when a dependency wait gave up
+  auto row = [&](int x) -> bool {
     const int i = perm[x];
     const int kb = iaf[i], kd = dg[i], ke = iaf[i + 1];
     const int W = ke - kb, nl = kd - kb;
@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__
       backoff(spins, false, err, 4u, give_up);
       if (give_up) break;
     }
-    if (give_up) return;
+    if (give_up) return false;
     if constexpr (!GR) pvt = low ? ld_agent(&af[pv.x]) : 1.0;
     double uu[NL];
     int tg[NL];
@@ -594,7 +594,7 @@ __global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__
       bool gu = false;
       while (!__all(okU)) {
         backoff(sp, false, err, 4u, gu);
-        if (gu) return;
+        if (gu) return false;
         if (!okU) {
           okU = true;
           fetch_upper(false);
@@ -617,6 +617,41 @@ __global__ void __launch_bounds__(256) k_ilu_factor_wave(const int* __restrict__
       for (int e = lane; e < W; e += 64) st_agent(&af[kb + e], w[e]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(&flags[i], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return true;
+  };
+  if (chunk > 0) {
+    // per wave: lane 0 takes the wave's tickets (read only where needed: the next ticket's round
+    // trip overlaps the current chunk); a ticket is `chunk` consecutive rows of the order, done in
+    // order by the wave
+    auto take = [&]() -> unsigned { return lane == 0 ? atomicAdd(ticket, 1u) : 0u; };
+    unsigned tk = take();
+    for (int x0 = (int)__shfl(tk, 0) * chunk; x0 < nrows; x0 = (int)__shfl(tk, 0) * chunk) {
+      tk = take();  // the next chunk's ticket
+      const int x1 = min(x0 + chunk, nrows);
+      for (int x = x0; x < x1; ++x)
+        if (!row(x)) return;
+    }
+  } else {
+    // per workgroup (the default): a ticket is 4 consecutive rows of the order, one per wave, taken
+    // by lane 0 of wave 0 one chunk ahead (a quarter of the device-scope atomics on the one counter:
+    // at one per row they were the factor's bottleneck -- C4 20.9 ms against 11.2 ms without
+    // tickets); the waves meet at a barrier per chunk
+    __shared__ unsigned s_tk[2];
+    __shared__ int s_bad;
+    if (threadIdx.x == 0) {
+      s_tk[0] = atomicAdd(ticket, 1u);
+      s_bad = 0;
+    }
+    __syncthreads();
+    int par = 0;
+    for (unsigned t = s_tk[0]; (long long)t * WG < nrows; t = s_tk[par]) {
+      if (threadIdx.x == 0) s_tk[par ^ 1] = atomicAdd(ticket, 1u);
+      const int x = (int)t * WG + wv;
+      if (x < nrows && !row(x) && lane == 0) s_bad = 1;
+      __syncthreads();
+      if (s_bad) return;
+      par ^= 1;
     }
   }
 }
@@ -855,15 +890,29 @@ void launch_ilu_factor_lds(const int* ia, const double* a, const int* amap, cons
                      tgt, perm, nchunks, af, flags, epoch, ticket, err);
 }
 
+// tickets of the wave factor: 0 = per workgroup, 4 rows (one per wave); n > 0 = per wave, n
+// consecutive rows (MMX_FAC_CHUNK overrides)
+constexpr int kFacWaveChunk = 0;
 // (the grid's size is a throughput choice only: the tickets need no co-residency)
+static int factor_wg() {  // waves per workgroup of the wave factor (MMX_FAC_WG: 4 or 8)
+  static const int v = [] {
+    const char* e = getenv("MMX_FAC_WG");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
+  return v;
+}
 int ilu_factor_wave_grid() {
   static int g = [] {
-    int dev = 0, cus = 0, nb = 0;
+    int dev = 0, cus = 0, nb = 0, nb2 = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ilu_factor_wave<kFacWaveNL, true>, 256, 0);
-    int nb2 = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_ilu_factor_wave<kFacWaveNL, false>, 256, 0);
+    if (factor_wg() == 8) {
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ilu_factor_wave<kFacWaveNL, true, 8>, 512, 0);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_ilu_factor_wave<kFacWaveNL, false, 8>, 512, 0);
+    } else {
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ilu_factor_wave<kFacWaveNL, true>, 256, 0);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, k_ilu_factor_wave<kFacWaveNL, false>, 256, 0);
+    }
     nb = nb < nb2 ? nb : nb2;
     nb = nb < 1 ? 1 : (nb > 8 ? 8 : nb);
     return (cus > 0 ? cus : 1) * nb;
@@ -876,14 +925,27 @@ void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, con
                             int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* ticket,
                             unsigned* err, hipStream_t st) {
   if (nrows <= 0) return;
-  // one CU's worth of waves per CU and occupancy slot; rows by ticket (*ticket zeroed by the caller)
-  const int blocks = std::min(ilu_factor_wave_grid(), (nrows + 3) / 4);
-  if (gF)
-    hipLaunchKernelGGL((k_ilu_factor_wave<kFacWaveNL, true>), dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv,
-                       jaf, toff, tgt, perm, nrows, ticket, af, flags, gF, epoch, err);
+  // one CU's worth of waves per CU and occupancy slot; rows by ticket (*ticket zeroed by the caller),
+  // MMX_FAC_CHUNK rows per ticket
+  static const int chunk = [] {
+    const char* e = getenv("MMX_FAC_CHUNK");
+    return e ? std::max(0, atoi(e)) : kFacWaveChunk;
+  }();
+  const int wg = chunk > 0 ? 4 : factor_wg();
+  const int per = wg * std::max(chunk, 1);  // rows a workgroup takes per round of tickets
+  const int blocks = std::min(ilu_factor_wave_grid(), (nrows + per - 1) / per);
+#define MMX_FACW(G, W)                                                                                           \
+  hipLaunchKernelGGL((k_ilu_factor_wave<kFacWaveNL, G, W>), dim3(blocks), dim3(64 * W), 0, st, ia, a, amap, iaf, dg, \
+                     piv, jaf, toff, tgt, perm, nrows, chunk, ticket, af, flags, gF, epoch, err)
+  if (gF && wg == 8)
+    MMX_FACW(true, 8);
+  else if (gF)
+    MMX_FACW(true, 4);
+  else if (wg == 8)
+    MMX_FACW(false, 8);
   else
-    hipLaunchKernelGGL((k_ilu_factor_wave<kFacWaveNL, false>), dim3(blocks), dim3(256), 0, st, ia, a, amap, iaf, dg, piv,
-                       jaf, toff, tgt, perm, nrows, ticket, af, flags, gF, epoch, err);
+    MMX_FACW(false, 4);
+#undef MMX_FACW
 }
 
 // Test hook (mmx_occupy): `blocks` workgroups of 1024 lanes with 64 KB of LDS each that hold their
