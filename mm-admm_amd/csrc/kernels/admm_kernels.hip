@@ -229,8 +229,11 @@ template <int D>
 __global__ void __launch_bounds__(kBlock) k_predict(DeviceMesh<D> m, int mode, const double* __restrict__ gs,
                                                      const double* __restrict__ x, double* __restrict__ xPrev,
                                                      double* __restrict__ xBar, double dt_over_tau, int xcd) {
-  const int v = logical_block(xcd) * kBlock + threadIdx.x;
-  if (v >= m.nP) return;
+  const int idx = logical_block(xcd) * kBlock + threadIdx.x;
+  if (idx >= m.nP) return;
+  // mode 0 gathers the incident gradients: in the x-update's order (neighbouring simplices); mode 1
+  // streams x and xPrev in node-id order
+  const int v = (mode == 0 && m.nodeOrder) ? m.nodeOrder[idx] : idx;
   double xv[D], xb[D];
 #pragma unroll
   for (int c = 0; c < D; ++c) xv[c] = x[(size_t)v * D + c];
@@ -1871,8 +1874,11 @@ __global__ void __launch_bounds__(kBlock) k_energy(DeviceMesh<D> m, const double
 template <int D>
 __global__ void __launch_bounds__(kBlock) k_euler_apply(DeviceMesh<D> m, const double* __restrict__ gs,
                                                          double* __restrict__ x, double dt_over_tau, int xcd) {
-  const int v = logical_block(xcd) * kBlock + threadIdx.x;
-  if (v >= m.nP) return;
+  const int idx = logical_block(xcd) * kBlock + threadIdx.x;
+  if (idx >= m.nP) return;
+  // nodes in the x-update's processing order (first incident simplex; 3D: y slabs): a workgroup's
+  // nodes gather from neighbouring simplices (C4: 0.58 ms in node-id order)
+  const int v = m.nodeOrder ? m.nodeOrder[idx] : idx;
   double g[D];
 #pragma unroll
   for (int c = 0; c < D; ++c) g[c] = 0.0;
@@ -1978,13 +1984,17 @@ __global__ void __launch_bounds__(kBlock) k_jac_assemble(DeviceMesh<D> m, const 
 
 // Newton residual of backwardsEulerStep (src/Mesh.cpp:1301-1306): grad from eulerStepMod's
 // INTERIOR-only scatter (ascending simplex id), F = grad * (dt/tau) + (x - xn), rhs = -F.
-template <int D>
+// ORD: the nodes in the x-update's processing order (their gathers from neighbouring simplices; C4
+// 0.58 ms in node-id order) and no partials -- k_abs_partials then forms them from rhs in node-id
+// order with this kernel's blocks, the same sums in the same order (bit-identical)
+template <int D, bool ORD = false>
 __global__ void __launch_bounds__(kBlock) k_be_residual(DeviceMesh<D> m, const double* __restrict__ gs,
                                                          const double* __restrict__ x, const double* __restrict__ xn,
                                                          double dt_over_tau, double* __restrict__ rhs,
                                                          double* __restrict__ partials, int xcd) {
   const int lb = logical_block(xcd);
-  const int v = lb * kBlock + threadIdx.x;
+  const int idx = lb * kBlock + threadIdx.x;
+  const int v = (ORD && idx < m.nP) ? m.nodeOrder[idx] : idx;
   double pv[1] = {0.0};
   if (v < m.nP) {
     double g[D];
@@ -2004,6 +2014,19 @@ __global__ void __launch_bounds__(kBlock) k_be_residual(DeviceMesh<D> m, const d
       pv[0] += __builtin_fabs(F);
       rhs[(size_t)v * D + c] = -F;
     }
+  }
+  if constexpr (!ORD) block_partials<1>(pv, partials, lb);
+}
+// the partials of k_be_residual<D, false> from rhs = -F (|-F| = |F| exactly)
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_abs_partials(int nP, const double* __restrict__ rhs,
+                                                          double* __restrict__ partials, int xcd) {
+  const int lb = logical_block(xcd);
+  const int v = lb * kBlock + threadIdx.x;
+  double pv[1] = {0.0};
+  if (v < nP) {
+#pragma unroll
+    for (int c = 0; c < D; ++c) pv[0] += __builtin_fabs(rhs[(size_t)v * D + c]);
   }
   block_partials<1>(pv, partials, lb);
 }
@@ -2595,6 +2618,12 @@ void launch_be_residual(const DeviceMesh<D>& m, const double* gs, const double* 
                         double dt_over_tau, double* rhs, double* partials, int* nblocks, hipStream_t st) {
   *nblocks = nblk_xcd(m.nP);
   if (m.nP == 0) return;
+  if (m.nodeOrder) {  // the node-ordered residual, then its partials in node-id order
+    hipLaunchKernelGGL((k_be_residual<D, true>), dim3(*nblocks), dim3(kBlock), 0, st, m, gs, x, xn, dt_over_tau, rhs,
+                       partials, xcd_map());
+    hipLaunchKernelGGL(k_abs_partials<D>, dim3(*nblocks), dim3(kBlock), 0, st, m.nP, rhs, partials, xcd_map());
+    return;
+  }
   hipLaunchKernelGGL(k_be_residual<D>, dim3(*nblocks), dim3(kBlock), 0, st, m, gs, x, xn, dt_over_tau, rhs, partials,
                      xcd_map());
 }
