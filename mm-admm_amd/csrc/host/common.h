@@ -45,6 +45,10 @@ int guarded(Fn&& f) {
   }
 }
 
+// dst <- src (bytes) on stream st through pinned staging buffers (staging.cpp); src may be freed
+// when it returns
+void upload_staged(void* dst, const void* src, size_t bytes, hipStream_t st);
+
 // Owning device buffer (hipMalloc / hipFree).
 template <class T>
 struct DevBuf {
@@ -64,7 +68,10 @@ struct DevBuf {
   }
   void upload(const T* h, size_t count, hipStream_t st) {
     alloc(count);
-    if (count) MMX_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
+    if (count * sizeof(T) >= ((size_t)16 << 20))  // large: pinned staging (~5x the pageable rate)
+      upload_staged(p, h, count * sizeof(T), st);
+    else if (count)
+      MMX_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
   }
 };
 

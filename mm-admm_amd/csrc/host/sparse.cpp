@@ -380,7 +380,7 @@ struct SparseMatrix {
     ChainSchedule Fs, Bs;
     FactorSchedule FS;
     std::vector<std::thread> helpers;
-    std::exception_ptr helperErr[2];
+    std::exception_ptr helperErr[3];
     const int nt = std::max(1, omp_get_max_threads());
     auto helper = [&](int slot, auto fn) {
       helpers.emplace_back([&, slot, fn, nt] {
@@ -395,6 +395,7 @@ struct SparseMatrix {
     if (tryChain) {
       helper(0, [&] { Bs = build_chain_schedule(n, iaf, jaf, dg, false); });
       if (tryChainFactor) helper(1, [&] { FS = build_factor_schedule(n, iaf, jaf, dg); });
+      helper(2, [&] { Fs = build_chain_schedule(n, iaf, jaf, dg, true); });
     }
     struct Joiner {  // the helpers reference this frame: joined on every way out of it
       std::vector<std::thread>& h;
@@ -416,65 +417,36 @@ struct SparseMatrix {
     d_af.alloc(std::max<size_t>(jaf.size(), 1));
     factVersion = -1;
     pt.mark("amap + uploads");
-    {  // pivot-row upper ranges of every lower entry (the factor's dependent loads, precomputed)
-      std::vector<int2> pv(std::max<size_t>(jaf.size(), 1));
-#pragma omp parallel for schedule(dynamic, 4096)
-      for (int i = 0; i < n; ++i) {
-        for (int k = iaf[i]; k < dg[i]; ++k) pv[k] = make_int2(dg[jaf[k]], iaf[jaf[k] + 1]);
-        for (int k = dg[i]; k < iaf[i + 1]; ++k) pv[k] = make_int2(0, 0);
-      }
-      d_piv.upload(pv.data(), pv.size(), st);
-      MMX_HIP(hipStreamSynchronize(st));  // (pv goes out of scope)
-    }
-    {  // update positions for the LDS-row factor (rows of at most kFacW entries)
+    {
+      // per row: its width and its lower entries' pivot upper lengths, summed, then a scan of rows --
+      // the offsets into the update-target table.  The pivot ranges, offsets and targets themselves
+      // are formed on the device from the factor pattern just uploaded (launch_fac_prep): at C4 they
+      // are ~1.3 GB that a pageable upload took ~0.4 s to move
       int maxW = 0;
-      std::vector<long long> off(std::max<size_t>(jaf.size(), 1), 0), rowTot(n + 1, 0);
-      // per row: its lower entries' pivot upper lengths (prefix within the row), then a scan of rows
+      std::vector<long long> rowTot(n + 1, 0);
 #pragma omp parallel for schedule(dynamic, 4096) reduction(max : maxW)
       for (int i = 0; i < n; ++i) {
         maxW = std::max(maxW, iaf[i + 1] - iaf[i]);
         long long t = 0;
-        for (int k = iaf[i]; k < dg[i]; ++k) {
-          off[k] = t;
-          t += iaf[jaf[k] + 1] - dg[jaf[k]] - 1;
-        }
+        for (int k = iaf[i]; k < dg[i]; ++k) t += iaf[jaf[k] + 1] - dg[jaf[k]] - 1;
         rowTot[i + 1] = t;
       }
       for (int i = 0; i < n; ++i) rowTot[i + 1] += rowTot[i];
       const long long tot = rowTot[n];
-#pragma omp parallel for schedule(dynamic, 4096)
-      for (int i = 0; i < n; ++i)
-        for (int k = iaf[i]; k < dg[i]; ++k) off[k] += rowTot[i];
       const char* fm = getenv("MMX_FACTOR");
       facLds = maxW <= kFacW && tot < (1ll << 31) && !(fm && std::strcmp(fm, "global") == 0);
-      pt.mark("pivot ranges");
+      DevBuf<long long> d_rowTot;
+      d_rowTot.upload(rowTot.data(), rowTot.size(), st);
+      d_piv.alloc(std::max<size_t>(jaf.size(), 1));
       if (facLds) {
-        // every target cell is written once below: no initialisation pass over the (C4: ~0.5 GB) array
-        std::vector<int> toff(off.size());
-        std::vector<signed char, NoInitAlloc<signed char>> tg(std::max<long long>(tot, 1));
-        if (tot == 0) tg[0] = -1;
-#pragma omp parallel for schedule(dynamic, 4096)
-        for (int i = 0; i < n; ++i) {
-          const int* rb = jaf.data() + iaf[i];
-          const int* re = jaf.data() + iaf[i + 1];
-          for (int k = iaf[i]; k < dg[i]; ++k) {
-            toff[k] = (int)off[k];
-            const int id = jaf[k];
-            signed char* out = tg.data() + off[k] - (dg[id] + 1);
-            const int* f = rb;  // both column lists ascending: one merge walk
-            for (int pp = dg[id] + 1; pp < iaf[id + 1]; ++pp) {
-              const int c = jaf[pp];
-              while (f != re && *f < c) ++f;
-              out[pp] = (f != re && *f == c) ? (signed char)(f - rb) : (signed char)-1;
-            }
-          }
-        }
-        pt.mark("update targets");
-        d_toff.upload(toff.data(), toff.size(), st);
-        d_tgt.upload(tg.data(), tg.size(), st);
-        MMX_HIP(hipStreamSynchronize(st));  // (the host images go out of scope)
-        pt.mark("update targets upload");
+        d_toff.alloc(std::max<size_t>(jaf.size(), 1));
+        d_tgt.alloc((size_t)std::max<long long>(tot, 1));
+        MMX_HIP(hipMemsetAsync(d_tgt.p, 0xFF, d_tgt.n, st));  // (-1: only a zero-size table keeps it)
       }
+      launch_fac_prep(n, d_iaf.p, d_jaf.p, d_dg.p, d_rowTot.p, d_piv.p, facLds ? d_toff.p : nullptr,
+                      facLds ? d_tgt.p : nullptr, st);
+      MMX_HIP(hipStreamSynchronize(st));  // (d_rowTot and rowTot go out of scope)
+      pt.mark("pivot ranges + update targets (device)");
     }
     // level schedules of the lower (forward sweep, factor) and upper (backward sweep) factor: the
     // two concurrently; the forward levels are kept for the wave factor's row order
@@ -516,12 +488,10 @@ struct SparseMatrix {
     pt.mark("level schedules");
     useChain = false;
     if (tryChain) {
-      Fs = build_chain_schedule(n, iaf, jaf, dg, true);
-      pt.mark("forward chain schedule");
       for (auto& h : helpers) h.join();
       for (auto& e : helperErr)
         if (e) std::rethrow_exception(e);
-      pt.mark("backward + factor schedules (joined)");
+      pt.mark("chain + factor schedules (joined)");
       if (Fs.ok && Bs.ok) {
         upload_chain(Fs, chf);
         upload_chain(Bs, chb);

@@ -66,6 +66,12 @@ void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, con
                             const int2* piv, const int* jaf, const int* toff, const signed char* tgt, const int* perm,
                             int nrows, double* af, unsigned* flags, uint64_t* gF, unsigned epoch, unsigned* ticket,
                             unsigned* err, hipStream_t st);
+// the factor's precomputed dependent loads, from the factor pattern (iaf, jaf, dg on the device):
+// per lower entry k of row i, piv[k] = (diag position, end) of its pivot row (0, 0 elsewhere); with
+// toff / tgt: toff[k] = rowTot[i] + the pivot upper lengths of row i's earlier lower entries, and
+// tgt[toff[k] + u] = the position in row i of the pivot row's u-th upper column, or -1
+void launch_fac_prep(int n, const int* iaf, const int* jaf, const int* dg, const long long* rowTot, int2* piv,
+                     int* toff, signed char* tgt, hipStream_t st);
 // test hook: blocks x 1024 lanes (64 KB LDS each) holding their CUs for ms milliseconds
 void launch_occupy(int blocks, double ms, double* sink, hipStream_t st);
 

@@ -948,6 +948,41 @@ void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, con
 #undef MMX_FACW
 }
 
+// one row per lane (sparse.cpp sfac; the host loops this replaces: a merge walk of row i's sorted
+// columns against each pivot row's upper part, as scaler_ILU::factor's target search)
+__global__ void __launch_bounds__(256) k_fac_prep(int n, const int* __restrict__ iaf, const int* __restrict__ jaf,
+                                                  const int* __restrict__ dg, const long long* __restrict__ rowTot,
+                                                  int2* __restrict__ piv, int* __restrict__ toff,
+                                                  signed char* __restrict__ tgt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int rb = iaf[i], re = iaf[i + 1], d = dg[i];
+  long long t = rowTot[i];
+  for (int k = rb; k < re; ++k) {
+    if (k >= d) {
+      piv[k] = make_int2(0, 0);
+      if (toff) toff[k] = 0;
+      continue;
+    }
+    const int j = jaf[k], dj = dg[j], ej = iaf[j + 1];
+    piv[k] = make_int2(dj, ej);
+    if (!toff) continue;
+    toff[k] = (int)t;
+    int f = rb;
+    for (int pp = dj + 1; pp < ej; ++pp) {
+      const int c = jaf[pp];
+      while (f < re && jaf[f] < c) ++f;
+      tgt[t + (pp - dj - 1)] = (f < re && jaf[f] == c) ? (signed char)(f - rb) : (signed char)-1;
+    }
+    t += ej - dj - 1;
+  }
+}
+void launch_fac_prep(int n, const int* iaf, const int* jaf, const int* dg, const long long* rowTot, int2* piv,
+                     int* toff, signed char* tgt, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_fac_prep, dim3((n + 255) / 256), dim3(256), 0, st, n, iaf, jaf, dg, rowTot, piv, toff, tgt);
+}
+
 // Test hook (mmx_occupy): `blocks` workgroups of 1024 lanes with 64 KB of LDS each that hold their
 // CUs for `ms` milliseconds (the 100 MHz real-time counter; every wave leaves at the deadline) --
 // a concurrent kernel that keeps part of the chip away from the solver's kernels.
