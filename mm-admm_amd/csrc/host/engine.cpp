@@ -585,11 +585,11 @@ class Engine final : public EngineBase {
       }
     } else if (op == 2) {
       const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
-      launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
+      launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_, fdWork_.p);
       clearInvFlag();  // the FD blocks report no inversion (their energies are not checked)
       // into a scratch buffer: jval_ keeps the engine's last assembled Jacobian (mmadmm_get_jacobian)
       if (jraw_.n != jja_.n) jraw_.alloc(std::max<size_t>(jja_.n, 1));
-      launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, 1.0, jraw_.p, st_, false);
+      launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, 1.0, jraw_.p, st_, false, maxColNodes_);
       MMX_HIP(hipMemcpyAsync(out, jraw_.p, jja_.n * sizeof(double), hipMemcpyDeviceToHost, st_));
       streamWait();
     } else if (op == 3) {
@@ -808,10 +808,15 @@ class Engine final : public EngineBase {
     profMark("matrix create", tp);
     if (rc != MMADMM_OK) throw Error(rc, std::string("backward Euler Jacobian: ") + mmadmm_last_error());
     mmx_param_iter_mesh(&jprm_);
+    maxColNodes_ = 0;  // the widest row's column nodes (the assembly's wavefront per node needs <= 64)
+    for (int r = 0; r < n; ++r) maxColNodes_ = std::max(maxColNodes_, (ia[r + 1] - ia[r]) / D);
     jia_.upload(ia.data(), ia.size(), st_);
     jja_.upload(ja.data(), ja.size(), st_);
     jval_.alloc(std::max<size_t>(nnz, 1));
     dv_.alloc(std::max<size_t>((size_t)nF_ * (D + 1) * D * K, 1));
+    // the FD blocks' fast pass queues its near-midpoint lanes here (MMX_FDJ_FAST=0: one exact pass)
+    const char* ff = getenv("MMX_FDJ_FAST");
+    if (!(ff && atoi(ff) == 0)) fdWork_.alloc((size_t)nF_ * (D + 1) + 1);
     xn_.alloc((size_t)n);
     rhs_.alloc((size_t)n);
     dx_.alloc((size_t)n);
@@ -829,9 +834,9 @@ class Engine final : public EngineBase {
     const auto t0 = Clock::now();
     auto tp = t0;
     const double h = 10.0 * sqrt(std::numeric_limits<double>::epsilon());
-    launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_);
+    launch_fd_jac<D>(m_, Vp_.p, h, dv_.p, st_, fdWork_.p);
     clearInvFlag();
-    launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, dtBE / prm_.tau, jval_.p, st_);
+    launch_jac_assemble<D>(m_, jia_.p, jja_.p, dv_.p, dtBE / prm_.tau, jval_.p, st_, true, maxColNodes_);
     streamWait();
     profMark("FD Jacobian + assembly", tp);
     MMX_SP(mmx_matrix_set_values_device(jac_, jval_.p));
@@ -1613,6 +1618,8 @@ class Engine final : public EngineBase {
   double jacDt_ = 0.0;
   DevBuf<int32_t> jia_, jja_;
   DevBuf<double> jval_, jraw_, dv_, xn_, rhs_, dx_;
+  DevBuf<unsigned> fdWork_;  // k_fd_jac's tie queue (count + lanes)
+  int maxColNodes_ = 65;
   int stepsTaken_ = 0;
   size_t maxBlocks_ = 1;                 // partial-sum rows per launch (upper bound)
   static constexpr int kDeferMax = 64;   // deferred reductions up to this many ADMM iterations

@@ -145,14 +145,17 @@ void launch_pack_export(int mode, int nExp, const int* expOff, const double* z, 
 // FD derivative blocks of FSubJac (src/Mesh.cpp:1173-1230) at positions Vp: one D x K block per
 // (simplex s, local vertex n), row-major at dv + ((s*(D+1)+n)*D)*K.
 template <int D>
-void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st);
+// work (optional, 1 + nF (D + 1) unsigneds): the fast pass + exact recomputation of its tie lanes
+void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st,
+                   unsigned* work = nullptr);
 // Jacobian values of buildEulerJac (src/Mesh.cpp:1112-1136, 1232-1258) on the buildMatrix CSR
 // pattern (ia, ja over the D*nP unknowns): per entry, the derivative blocks of the node's incident
 // simplices in ascending id (pairsort order, +0.0 adds), scaled by dt/tau, +1 on the diagonal
 // (finish = false: the sums alone, before the scaling and the identity).
 template <int D>
+// maxColNodes: the widest row's column nodes (at most 64: one wavefront per node, else one lane per row)
 void launch_jac_assemble(const DeviceMesh<D>& m, const int* ia, const int* ja, const double* dv,
-                         double dt_over_tau, double* a, hipStream_t st, bool finish = true);
+                         double dt_over_tau, double* a, hipStream_t st, bool finish = true, int maxColNodes = 65);
 // Newton residual F = (dt/tau) grad + (x - xn) with grad the INTERIOR-only scatter of gs
 // (eulerStepMod, src/Mesh.cpp:532-579); rhs = -F; partial record v[0] = sum |F_i|.
 template <int D>

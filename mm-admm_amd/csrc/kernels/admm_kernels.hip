@@ -1901,12 +1901,15 @@ __global__ void __launch_bounds__(kBlock) k_euler_apply(DeviceMesh<D> m, const d
 // moved by h (pass i), and writes derivs(i, :) = (Gkp1 - Gk) / h.  A BOUNDARY_FIXED vertex gets
 // the reference's identity pattern, which is nonzero only for n == 0 (r == c in D*n..D*n+D-1).
 // The node-centric reference evaluates Gk once per (node, simplex); the values are the same.
-template <int D, int ISO = -1>
-__global__ void __launch_bounds__(kBlock) k_fd_jac(DeviceMesh<D> m, const double* __restrict__ Vp, double h,
-                                                    double* __restrict__ dv) {
+// EXACT = false (with `work`): the fast path -- a lane whose powers meet a rounding midpoint (or
+// leave the double-double ranges) writes nothing and queues itself (work[0] counts, work[1 + q]
+// lists), and k_fd_jac_fix recomputes the queued lanes with the exact decision.  On the regular
+// initial meshes the exact path is common, and in the one-kernel form every wave with one such
+// lane ran it, with its expansion arithmetic in 5 KB of scratch per lane (C4: 110 ms)
+template <int D, int ISO, bool EXACT>
+__device__ __forceinline__ void fd_jac_lane(const DeviceMesh<D>& m, const double* __restrict__ Vp, double h,
+                                            double* __restrict__ dv, long long t, unsigned* work) {
   constexpr int K = D * (D + 1);
-  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (t >= (long long)m.nF * (D + 1)) return;
   const int s = (int)(t / (D + 1)), n = (int)(t % (D + 1));
   double* out = dv + (size_t)t * D * K;
   if (m.sbits[s] & (1u << n)) {
@@ -1922,20 +1925,39 @@ __global__ void __launch_bounds__(kBlock) k_fd_jac(DeviceMesh<D> m, const double
   loadXi<D>(m, f, xi);
   const GridView<D> g = gridOf<D, ISO>(m);
   const FunctionalConsts<D> fc = constsOf<D>(m);
+  bool tie = false;
 #pragma unroll 1
   for (int it = -1; it < D; ++it) {
     const int moved = (it < 0) ? -1 : D * n + it;
 #pragma unroll
     for (int c = 0; c < K; ++c) xp[c] = (c == moved) ? xl[c] + h : xl[c];
-    blockGrad<D, true, false>(g, fc, xp, xi, nullptr, g1, Igt);
+    blockGrad<D, true, false, EXACT>(g, fc, xp, xi, nullptr, g1, Igt, nullptr, &tie);
     if (it < 0) {
 #pragma unroll
       for (int c = 0; c < K; ++c) gk[c] = g1[c];
-    } else {
+    } else {  // (a queued lane's rows are all written again by k_fd_jac_fix)
 #pragma unroll
       for (int c = 0; c < K; ++c) out[it * K + c] = (g1[c] - gk[c]) / h;
     }
   }
+  if constexpr (!EXACT) {
+    if (tie) work[1 + atomicAdd(work, 1u)] = (unsigned)t;
+  }
+}
+template <int D, int ISO = -1, bool EXACT = true>
+__global__ void __launch_bounds__(kBlock) k_fd_jac(DeviceMesh<D> m, const double* __restrict__ Vp, double h,
+                                                    double* __restrict__ dv, unsigned* work) {
+  const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (long long)m.nF * (D + 1)) return;
+  fd_jac_lane<D, ISO, EXACT>(m, Vp, h, dv, t, work);
+}
+// the lanes k_fd_jac<.., false> queued, exactly (a fixed grid striding over the queue)
+template <int D, int ISO = -1>
+__global__ void __launch_bounds__(kBlock) k_fd_jac_fix(DeviceMesh<D> m, const double* __restrict__ Vp, double h,
+                                                        double* __restrict__ dv, const unsigned* __restrict__ work) {
+  const unsigned nq = work[0];
+  for (unsigned q = blockIdx.x * kBlock + threadIdx.x; q < nq; q += gridDim.x * kBlock)
+    fd_jac_lane<D, ISO, true>(m, Vp, h, dv, (long long)work[1 + q], nullptr);
 }
 
 // buildEulerJac + FSubJac's scatter (src/Mesh.cpp:1112-1136, 1232-1258), row-centric: row
@@ -1979,6 +2001,108 @@ __global__ void __launch_bounds__(kBlock) k_jac_assemble(DeviceMesh<D> m, const 
       if (col == r) v += 1.0;
     }
     a[i] = v;
+  }
+}
+
+// The same sums simplex-outer: row r walks its node's incident simplices once (ascending id) and
+// adds each simplex's derivative block to the entries of its D + 1 vertices, found by a binary
+// search over the row's node-major columns.  Every entry receives its terms in the same order as
+// above; the +0.0 adds are dropped because they change nothing here -- an entry starts at +0.0, and
+// a sum that starts at +0.0 is never -0.0 under round-to-nearest (+0 + -0 = +0, x + -x = +0), so
+// v + 0.0 = v at every step (bit-identical; C4: 26 ms for the entry-outer form, which loaded the
+// node's incident simplices again for every entry of the row)
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_jac_assemble_s(DeviceMesh<D> m, const int* __restrict__ ia,
+                                                            const int* __restrict__ ja, const double* __restrict__ dv,
+                                                            double dt_over_tau, int finish, double* __restrict__ a) {
+  constexpr int K = D * (D + 1);
+  const int r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= m.nP * D) return;
+  const int pnt = r / D, p = r % D;
+  const int rb = ia[r], re = ia[r + 1], nn = (re - rb) / D;
+  for (int i = rb; i < re; ++i) a[i] = 0.0;
+  const int tb = m.inc_ptr[pnt], te = m.inc_ptr[pnt + 1];
+  for (int t = tb; t < te; ++t) {
+    const int off = m.inc_off[t];
+    const int s = off / K, nl = (off % K) / D;
+    int f[D + 1];
+    loadVerts<D>(m, s, f);
+    const double* d = dv + ((size_t)(s * (D + 1) + nl) * D + p) * K;
+#pragma unroll
+    for (int k = 0; k < D + 1; ++k) {
+      int lo = 0, hi = nn - 1;  // the node f[k] among the row's nodes (ascending; it is there)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ja[rb + mid * D] / D < f[k])
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      double* e = a + rb + lo * D;
+#pragma unroll
+      for (int co = 0; co < D; ++co) e[co] = e[co] + d[D * k + co];
+    }
+  }
+  if (finish) {
+    for (int i = rb; i < re; ++i) {
+      double v = a[i] * dt_over_tau;
+      if (ja[i] == r) v += 1.0;
+      a[i] = v;
+    }
+  }
+}
+
+// The same sums with one wavefront per node: lane q holds the D x D entries (rows p, offsets co)
+// of the node's q-th column node (the node's D rows share their node-major columns) and the wave
+// walks the node's incident simplices once, in ascending id (uniform loads); the lanes of the
+// simplex's vertices add its derivative values -- every entry its terms in the same order
+// (bit-identical; at most 64 column nodes, checked by the launch)
+template <int D>
+__global__ void __launch_bounds__(256) k_jac_assemble_w(DeviceMesh<D> m, const int* __restrict__ ia,
+                                                         const int* __restrict__ ja, const double* __restrict__ dv,
+                                                         double dt_over_tau, int finish, double* __restrict__ a) {
+  constexpr int K = D * (D + 1);
+  const int pnt = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
+  if (pnt >= m.nP) return;
+  const int r0 = pnt * D, rb = ia[r0], nn = (ia[r0 + 1] - rb) / D;
+  const bool act = lane < nn;
+  const int ci = act ? ja[rb + lane * D] / D : -1;
+  double acc[D][D];
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int co = 0; co < D; ++co) acc[p][co] = 0.0;
+  const int tb = m.inc_ptr[pnt], te = m.inc_ptr[pnt + 1];
+  for (int t = tb; t < te; ++t) {
+    const int off = m.inc_off[t];
+    const int s = off / K, nl = (off % K) / D;
+    int f[D + 1];
+    loadVerts<D>(m, s, f);
+    int hit = -1;
+#pragma unroll
+    for (int k = 0; k < D + 1; ++k)
+      if (f[k] == ci) hit = k;
+    if (hit >= 0) {
+      const double* d = dv + ((size_t)(s * (D + 1) + nl) * D) * K + D * hit;
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+#pragma unroll
+        for (int co = 0; co < D; ++co) acc[p][co] = acc[p][co] + d[p * K + co];
+    }
+  }
+  if (!act) return;
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    const int r = r0 + p, i0 = ia[r] + lane * D;
+#pragma unroll
+    for (int co = 0; co < D; ++co) {
+      double v = acc[p][co];
+      if (finish) {  // buildEulerJac's scaling and identity (src/Mesh.cpp:1125-1134)
+        v *= dt_over_tau;
+        if (ja[i0 + co] == r) v += 1.0;
+      }
+      a[i0 + co] = v;
+    }
   }
 }
 
@@ -2595,23 +2719,50 @@ void launch_devmath(int op, int n, const double* in, double* out, hipStream_t st
 }
 
 template <int D>
-void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st) {
+void launch_fd_jac(const DeviceMesh<D>& m, const double* Vp, double h, double* dv, hipStream_t st, unsigned* work) {
   const long long nt = (long long)m.nF * (D + 1);
   if (nt == 0) return;
-  const dim3 gj((unsigned)((nt + kBlock - 1) / kBlock));
+  // the fix pass: one lane per possible queue entry (the queue's length is known on the device only;
+  // lanes past it exit at once) -- the exact path is long, so every queued lane gets its own
+  const dim3 gj((unsigned)((nt + kBlock - 1) / kBlock)), gf = gj;
+  if (work) {  // fast pass + the exact recomputation of its queued lanes
+    if (hipMemsetAsync(work, 0, sizeof(unsigned), st) != hipSuccess) throw std::runtime_error("launch_fd_jac: memset");
+#define MMX_FDJ(I)                                                                                       \
+  do {                                                                                                   \
+    hipLaunchKernelGGL((k_fd_jac<D, I, false>), gj, dim3(kBlock), 0, st, m, Vp, h, dv, work);            \
+    hipLaunchKernelGGL((k_fd_jac_fix<D, I>), gf, dim3(kBlock), 0, st, m, Vp, h, dv, (const unsigned*)work); \
+  } while (0)
+    if (D == 3 && m.giso)
+      MMX_FDJ(1);
+    else if (D == 3)
+      MMX_FDJ(0);
+    else
+      MMX_FDJ(-1);
+#undef MMX_FDJ
+    return;
+  }
   if (D == 3 && m.giso)
-    hipLaunchKernelGGL((k_fd_jac<D, 1>), gj, dim3(kBlock), 0, st, m, Vp, h, dv);
+    hipLaunchKernelGGL((k_fd_jac<D, 1>), gj, dim3(kBlock), 0, st, m, Vp, h, dv, nullptr);
   else if (D == 3)
-    hipLaunchKernelGGL((k_fd_jac<D, 0>), gj, dim3(kBlock), 0, st, m, Vp, h, dv);
+    hipLaunchKernelGGL((k_fd_jac<D, 0>), gj, dim3(kBlock), 0, st, m, Vp, h, dv, nullptr);
   else
-    hipLaunchKernelGGL((k_fd_jac<D, -1>), gj, dim3(kBlock), 0, st, m, Vp, h, dv);
+    hipLaunchKernelGGL((k_fd_jac<D, -1>), gj, dim3(kBlock), 0, st, m, Vp, h, dv, nullptr);
 }
 template <int D>
 void launch_jac_assemble(const DeviceMesh<D>& m, const int* ia, const int* ja, const double* dv, double dt_over_tau,
-                         double* a, hipStream_t st, bool finish) {
+                         double* a, hipStream_t st, bool finish, int maxColNodes) {
   if (m.nP == 0) return;
-  hipLaunchKernelGGL(k_jac_assemble<D>, dim3(nblk(m.nP * D)), dim3(kBlock), 0, st, m, ia, ja, dv, dt_over_tau,
-                     finish ? 1 : 0, a);
+  const char* ev = getenv("MMX_JAC_ASSEMBLE");  // "entry": the entry-outer form (once per assembly)
+  const bool entryOuter = ev && std::string(ev) == "entry";
+  if (entryOuter)
+    hipLaunchKernelGGL(k_jac_assemble<D>, dim3(nblk(m.nP * D)), dim3(kBlock), 0, st, m, ia, ja, dv, dt_over_tau,
+                       finish ? 1 : 0, a);
+  else if (maxColNodes <= 64)
+    hipLaunchKernelGGL(k_jac_assemble_w<D>, dim3((m.nP + 3) / 4), dim3(256), 0, st, m, ia, ja, dv, dt_over_tau,
+                       finish ? 1 : 0, a);
+  else
+    hipLaunchKernelGGL(k_jac_assemble_s<D>, dim3(nblk(m.nP * D)), dim3(kBlock), 0, st, m, ia, ja, dv, dt_over_tau,
+                       finish ? 1 : 0, a);
 }
 template <int D>
 void launch_be_residual(const DeviceMesh<D>& m, const double* gs, const double* x, const double* xn,
@@ -2645,9 +2796,9 @@ void launch_add_inplace(int n, double* x, const double* dx, hipStream_t st) {
                                double*, double*, int*, hipStream_t);                                    \
   template void launch_energy<D>(const DeviceMesh<D>&, const double*, double*, int*, hipStream_t);       \
   template void launch_euler_apply<D>(const DeviceMesh<D>&, const double*, double*, double, hipStream_t);     \
-  template void launch_fd_jac<D>(const DeviceMesh<D>&, const double*, double, double*, hipStream_t);          \
+  template void launch_fd_jac<D>(const DeviceMesh<D>&, const double*, double, double*, hipStream_t, unsigned*);          \
   template void launch_jac_assemble<D>(const DeviceMesh<D>&, const int*, const int*, const double*, double,   \
-                                       double*, hipStream_t, bool);                                                 \
+                                       double*, hipStream_t, bool, int);                                                 \
   template void launch_be_residual<D>(const DeviceMesh<D>&, const double*, const double*, const double*,      \
                                       double, double*, double*, int*, hipStream_t);
 MMX_INST(2)

@@ -197,6 +197,13 @@ MMX_HD_COLD void compress(Ex& e) {
   e.n = top;
 }
 
+// dst = src, its n live components only (a whole-struct copy moves kCap doubles: on the device the
+// expansions live in scratch, and the copies were most of the exact path's traffic)
+MMX_HD void assign(Ex& dst, const Ex& src) {
+  for (int i = 0; i < src.n; ++i) dst.t[i] = src.t[i];
+  dst.n = src.n;
+}
+
 MMX_HD_COLD void mul(const Ex& a, const Ex& b, Ex& out) {
   Ex acc, part, tmp;
   acc.n = 0;
@@ -204,9 +211,9 @@ MMX_HD_COLD void mul(const Ex& a, const Ex& b, Ex& out) {
     scale(a, b.t[j], part);
     sum(acc, part, tmp);
     compress(tmp);
-    acc = tmp;
+    assign(acc, tmp);
   }
-  out = acc;
+  assign(out, acc);
 }
 
 MMX_HD void single(double v, Ex& e) {
@@ -221,15 +228,15 @@ MMX_HD_COLD void ipow(double x, int p, Ex& out) {  // x^p exactly, p >= 1
   while (p) {
     if (p & 1) {
       mul(r, base, t);
-      r = t;
+      assign(r, t);
     }
     p >>= 1;
     if (p) {
       mul(base, base, t);
-      base = t;
+      assign(base, t);
     }
   }
-  out = r;
+  assign(out, r);
 }
 
 MMX_HD int sign(const Ex& e) {  // sign of the largest nonzero component
@@ -264,16 +271,16 @@ MMX_HD_COLD double cr_resolve(double x, int num, int den, double h, int dir) {
     xp::single(mhi, m);
   }
   // m^den
-  mp = m;
+  xp::assign(mp, m);
   for (int i = 1; i < den; ++i) {
     xp::Ex t;
     xp::mul(mp, m, t);
-    mp = t;
+    xp::assign(mp, t);
   }
   int s;
   if (num > 0) {  // sign(x^num - m^den)
     xp::ipow(x, num, lhs);
-    neg = mp;
+    xp::assign(neg, mp);
     for (int i = 0; i < neg.n; ++i) neg.t[i] = -neg.t[i];
     xp::sum(lhs, neg, diff);
     s = xp::sign(diff);

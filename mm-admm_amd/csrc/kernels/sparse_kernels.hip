@@ -948,25 +948,43 @@ void launch_ilu_factor_wave(const int* ia, const double* a, const int* amap, con
 #undef MMX_FACW
 }
 
-// one row per lane (sparse.cpp sfac; the host loops this replaces: a merge walk of row i's sorted
-// columns against each pivot row's upper part, as scaler_ILU::factor's target search)
+// one wavefront per row (sparse.cpp sfac; the host loops this replaces): lane q takes lower entry q
+// (and q + 64, ...): its pivot range; with toff / tgt its offset (rowTot[i] + an exclusive scan of
+// the lower entries' pivot upper lengths across the lanes) and a merge walk of row i's sorted
+// columns against the pivot row's upper part, as scaler_ILU::factor's target search
 __global__ void __launch_bounds__(256) k_fac_prep(int n, const int* __restrict__ iaf, const int* __restrict__ jaf,
                                                   const int* __restrict__ dg, const long long* __restrict__ rowTot,
                                                   int2* __restrict__ piv, int* __restrict__ toff,
                                                   signed char* __restrict__ tgt) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
   if (i >= n) return;
   const int rb = iaf[i], re = iaf[i + 1], d = dg[i];
-  long long t = rowTot[i];
-  for (int k = rb; k < re; ++k) {
-    if (k >= d) {
-      piv[k] = make_int2(0, 0);
-      if (toff) toff[k] = 0;
-      continue;
+  for (int k = d + lane; k < re; k += 64) {  // diagonal and upper entries
+    piv[k] = make_int2(0, 0);
+    if (toff) toff[k] = 0;
+  }
+  long long base = rowTot[i];
+  for (int k0 = rb; k0 < d; k0 += 64) {
+    const int k = k0 + lane;
+    const bool low = k < d;
+    int dj = 0, ej = 0;
+    if (low) {
+      const int j = jaf[k];
+      dj = dg[j];
+      ej = iaf[j + 1];
+      piv[k] = make_int2(dj, ej);
     }
-    const int j = jaf[k], dj = dg[j], ej = iaf[j + 1];
-    piv[k] = make_int2(dj, ej);
     if (!toff) continue;
+    const long long len = low ? (long long)(ej - dj - 1) : 0;
+    long long inc = len;  // inclusive scan over the lanes
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+      const long long o = __shfl_up(inc, sh);
+      if (lane >= sh) inc += o;
+    }
+    const long long t = base + inc - len;
+    base += __shfl(inc, 63);
+    if (!low) continue;
     toff[k] = (int)t;
     int f = rb;
     for (int pp = dj + 1; pp < ej; ++pp) {
@@ -974,13 +992,12 @@ __global__ void __launch_bounds__(256) k_fac_prep(int n, const int* __restrict__
       while (f < re && jaf[f] < c) ++f;
       tgt[t + (pp - dj - 1)] = (f < re && jaf[f] == c) ? (signed char)(f - rb) : (signed char)-1;
     }
-    t += ej - dj - 1;
   }
 }
 void launch_fac_prep(int n, const int* iaf, const int* jaf, const int* dg, const long long* rowTot, int2* piv,
                      int* toff, signed char* tgt, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_fac_prep, dim3((n + 255) / 256), dim3(256), 0, st, n, iaf, jaf, dg, rowTot, piv, toff, tgt);
+  hipLaunchKernelGGL(k_fac_prep, dim3((n + 3) / 4), dim3(256), 0, st, n, iaf, jaf, dg, rowTot, piv, toff, tgt);
 }
 
 // Test hook (mmx_occupy): `blocks` workgroups of 1024 lanes with 64 KB of LDS each that hold their

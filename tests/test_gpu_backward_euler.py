@@ -134,3 +134,31 @@ def test_backward_euler_at_bench_size_bitwise():
         np.testing.assert_array_equal(G.get("x"), O.get("x"), err_msg=f"x step {s}")
     np.testing.assert_array_equal(G.jacobian()[2], O.jacobian()[2])
     G.close()
+
+
+@pytest.mark.parametrize("dim,n,mon", [(2, 60, 3), (3, 14, 6), (3, 12, 7)])
+def test_fd_jac_fast_path_and_assembly_variants_bitwise(dim, n, mon, monkeypatch):
+    """Round 6: the FD derivative blocks as a fast pass (no exact tie decision, no scratch) plus the
+    exact recomputation of the lanes it queues, and the Jacobian assembled simplex-outer, against
+    the one-pass exact kernel (MMX_FDJ_FAST=0) and the entry-outer assembly (MMX_JAC_ASSEMBLE=entry):
+    the Jacobian and two Newton steps bit-identical.  Regular meshes (the exact path is common there)
+    with the anisotropic (6) and isotropic (7) 3D monitors."""
+    mesh = mx.MeshData.rect(dim, n)
+    rho = 2000.0 if dim == 3 else 100.0
+
+    def run():
+        M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, mon), rho=rho, tau=0.5)
+        E = mx.Engine(M, 0.025)
+        E.backwards_euler_step(0.025)
+        jac = E.jacobian()[2].copy()
+        E.backwards_euler_step(0.025)
+        x = E.get("x").copy()
+        E.close()
+        return jac, x
+
+    jac, x = run()
+    monkeypatch.setenv("MMX_FDJ_FAST", "0")
+    monkeypatch.setenv("MMX_JAC_ASSEMBLE", "entry")
+    jac0, x0 = run()
+    np.testing.assert_array_equal(jac, jac0)
+    np.testing.assert_array_equal(x, x0)
