@@ -1192,6 +1192,13 @@ __global__ void __launch_bounds__(BS, 2) k_prox_lds(DeviceMesh<D> m, double tol,
 #ifndef MMX_WAVE_PERSIST
 #define MMX_WAVE_PERSIST 0  // 3D: a persistent grid of this many one-wave workgroups (a multiple of 8), 0: one per block
 #endif
+#ifndef MMX_HELD_DMA_CPOL
+// cache policy of the held rows' DMA: 2 = nontemporal (they are read from global once and kept in
+// LDS, so streaming them leaves L2 to the rows re-read by passes 2 and 3): C4 prox 2.31 -> 2.29 ms.
+// Not kept: the update pass's (last) row reads streamed (no change), u and the cached gradient
+// loaded nontemporal (2.29 -> 2.46 ms); profiles/r06/experiments/c4_streaming_hints.jsonl
+#define MMX_HELD_DMA_CPOL 2
+#endif
 #ifndef MMX_WAVE_XCD
 #define MMX_WAVE_XCD 1  // measured C4: prox 3.42 -> 3.29 ms (neighbouring tets share x and monitor-grid lines in one L2)
 #endif
@@ -1247,7 +1254,7 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
 #pragma unroll
       for (int c = 0; c < WaveB<K>::kHeld * K * 64 * 8 / 1024; ++c)
         __builtin_amdgcn_global_load_lds(src + c * 1024, (__attribute__((address_space(3))) void*)(dst + c * 1024),
-                                         16, 0, 0);
+                                         16, 0, MMX_HELD_DMA_CPOL);
     }
   }
   double pv[6] = {0, 0, 0, 0, 0, 0};
