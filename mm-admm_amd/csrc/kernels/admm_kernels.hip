@@ -2063,7 +2063,10 @@ __global__ void __launch_bounds__(kBlock) k_jac_assemble_s(DeviceMesh<D> m, cons
 // of the node's q-th column node (the node's D rows share their node-major columns) and the wave
 // walks the node's incident simplices once, in ascending id (uniform loads); the lanes of the
 // simplex's vertices add its derivative values -- every entry its terms in the same order
-// (bit-identical; at most 64 column nodes, checked by the launch)
+// (bit-identical; at most 64 column nodes, checked by the launch).  A node that no simplex
+// references (the Shoulder meshes have such nodes) has rows holding only their diagonal entry
+// (mmx_struc_mesh_pattern), not node blocks: its entries are +0.0 (and the identity) as in the
+// other forms.
 template <int D>
 __global__ void __launch_bounds__(256) k_jac_assemble_w(DeviceMesh<D> m, const int* __restrict__ ia,
                                                          const int* __restrict__ ja, const double* __restrict__ dv,
@@ -2071,6 +2074,22 @@ __global__ void __launch_bounds__(256) k_jac_assemble_w(DeviceMesh<D> m, const i
   constexpr int K = D * (D + 1);
   const int pnt = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
   if (pnt >= m.nP) return;
+  const int tb = m.inc_ptr[pnt], te = m.inc_ptr[pnt + 1];
+  if (tb == te) {
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+      const int r = pnt * D + p;
+      for (int i = ia[r] + lane; i < ia[r + 1]; i += 64) {
+        double v = 0.0;
+        if (finish) {
+          v *= dt_over_tau;
+          if (ja[i] == r) v += 1.0;
+        }
+        a[i] = v;
+      }
+    }
+    return;
+  }
   const int r0 = pnt * D, rb = ia[r0], nn = (ia[r0 + 1] - rb) / D;
   const bool act = lane < nn;
   const int ci = act ? ja[rb + lane * D] / D : -1;
@@ -2079,7 +2098,6 @@ __global__ void __launch_bounds__(256) k_jac_assemble_w(DeviceMesh<D> m, const i
   for (int p = 0; p < D; ++p)
 #pragma unroll
     for (int co = 0; co < D; ++co) acc[p][co] = 0.0;
-  const int tb = m.inc_ptr[pnt], te = m.inc_ptr[pnt + 1];
   for (int t = tb; t < te; ++t) {
     const int off = m.inc_off[t];
     const int s = off / K, nl = (off % K) / D;

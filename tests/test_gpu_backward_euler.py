@@ -136,18 +136,26 @@ def test_backward_euler_at_bench_size_bitwise():
     G.close()
 
 
-@pytest.mark.parametrize("dim,n,mon", [(2, 60, 3), (3, 14, 6), (3, 12, 7)])
-def test_fd_jac_fast_path_and_assembly_variants_bitwise(dim, n, mon, monkeypatch):
+@pytest.mark.parametrize("dim,n,mon,loose", [(2, 60, 3, 0), (3, 14, 6, 0), (3, 12, 7, 0), (2, 20, 3, 2), (3, 6, 6, 1)])
+def test_fd_jac_fast_path_and_assembly_variants_bitwise(dim, n, mon, loose, monkeypatch):
     """Round 6: the FD derivative blocks as a fast pass (no exact tie decision, no scratch) plus the
-    exact recomputation of the lanes it queues, and the Jacobian assembled simplex-outer, against
-    the one-pass exact kernel (MMX_FDJ_FAST=0) and the entry-outer assembly (MMX_JAC_ASSEMBLE=entry):
-    the Jacobian and two Newton steps bit-identical.  Regular meshes (the exact path is common there)
-    with the anisotropic (6) and isotropic (7) 3D monitors."""
+    exact recomputation of the lanes it queues, and the Jacobian assembled one wavefront per node,
+    against the one-pass exact kernel (MMX_FDJ_FAST=0) and the entry-outer assembly
+    (MMX_JAC_ASSEMBLE=entry): the Jacobian and two Newton steps bit-identical.  Regular meshes (the
+    exact path is common there) with the anisotropic (6) and isotropic (7) 3D monitors; `loose`
+    nodes that no simplex references (as the Shoulder meshes have: their Jacobian rows hold only the
+    diagonal) inserted at the front of the numbering and appended at its end."""
     mesh = mx.MeshData.rect(dim, n)
+    Xp, F, mask = mesh.Xp, mesh.F, mesh.mask
+    if loose:
+        c = Xp.mean(axis=0, keepdims=True)
+        Xp = np.vstack([c] * loose + [Xp, c])
+        F = F + loose
+        mask = np.concatenate([mask[:1]] * loose + [mask, mask[:1]])
     rho = 2000.0 if dim == 3 else 100.0
 
     def run():
-        M = mx.Mesh(mesh.Xp, mesh.F, mesh.mask, mx.BuiltinMonitor(dim, mon), rho=rho, tau=0.5)
+        M = mx.Mesh(Xp, F, mask, mx.BuiltinMonitor(dim, mon), rho=rho, tau=0.5)
         E = mx.Engine(M, 0.025)
         E.backwards_euler_step(0.025)
         jac = E.jacobian()[2].copy()
