@@ -304,21 +304,27 @@ struct SparseMatrix {
     for (int i = 0; i < n; ++i)
       if (ia_[i + 1] < ia_[i]) throw Error(MMADMM_ERR_INVALID, "ia must be non-decreasing");
     nnz = ia_[n];
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(max : bad)
     for (long long k = 0; k < nnz; ++k)
-      if (ja_[k] < 0 || ja_[k] >= n) throw Error(MMADMM_ERR_INVALID, "column index out of range");
+      if (ja_[k] < 0 || ja_[k] >= n) bad = 1;
+    if (bad) throw Error(MMADMM_ERR_INVALID, "column index out of range");
     ia.assign(ia_, ia_ + n + 1);
-    ja.assign(ja_, ja_ + nnz);
+    ja.resize(nnz);
+#pragma omp parallel for schedule(static)
+    for (long long k = 0; k < nnz; ++k) ja[k] = ja_[k];
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw Error(MMADMM_ERR_HIP, "no HIP device available");
     MMX_HIP(hipSetDevice(device));
     MMX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     d_ia.upload(ia.data(), ia.size(), st);
-    {  // 2 padding entries: launch_spmv2 reads whole aligned pairs
-      std::vector<int> jap(ja);
-      jap.resize(ja.size() + 2, 0);
-      d_ja.upload(jap.data(), jap.size(), st);
-      MMX_HIP(hipStreamSynchronize(st));
-    }
+    // 2 padding entries: launch_spmv2 reads whole aligned pairs
+    d_ja.alloc((size_t)nnz + 2);
+    if (nnz * sizeof(int) >= ((size_t)16 << 20))
+      upload_staged(d_ja.p, ja.data(), (size_t)nnz * sizeof(int), st);
+    else if (nnz)
+      MMX_HIP(hipMemcpyAsync(d_ja.p, ja.data(), (size_t)nnz * sizeof(int), hipMemcpyHostToDevice, st));
+    MMX_HIP(hipMemsetAsync(d_ja.p + nnz, 0, 2 * sizeof(int), st));
     d_a.alloc(nnz + 2);
     MMX_HIP(hipMemsetAsync(d_a.p, 0, sizeof(double) * (nnz + 2), st));
     d_b.alloc(n);
@@ -392,10 +398,32 @@ struct SparseMatrix {
         }
       });
     };
+    // each sweep schedule is uploaded by its helper as soon as it is built (2D: under the factor
+    // schedule, the longest of the three); a failed one leaves useChain off below
+    const char* pe = getenv("MMX_CHAIN_PROF");
+    if (tryChain && pe && atoi(pe) && !d_cprof.p) {
+      d_cprof.alloc(1024);
+      MMX_HIP(hipMemsetAsync(d_cprof.p, 0, 1024 * sizeof(unsigned long long), st));
+    }
+    bool upF = false, upB = false;
     if (tryChain) {
-      helper(0, [&] { Bs = build_chain_schedule(n, iaf, jaf, dg, false); });
+      helper(0, [&] {
+        Bs = build_chain_schedule(n, iaf, jaf, dg, false);
+        if (Bs.ok) {
+          upload_chain(Bs, chb);
+          upB = true;
+          release(Bs);
+        }
+      });
       if (tryChainFactor) helper(1, [&] { FS = build_factor_schedule(n, iaf, jaf, dg); });
-      helper(2, [&] { Fs = build_chain_schedule(n, iaf, jaf, dg, true); });
+      helper(2, [&] {
+        Fs = build_chain_schedule(n, iaf, jaf, dg, true);
+        if (Fs.ok) {
+          upload_chain(Fs, chf);
+          upF = true;
+          release(Fs);
+        }
+      });
     }
     struct Joiner {  // the helpers reference this frame: joined on every way out of it
       std::vector<std::thread>& h;
@@ -491,13 +519,8 @@ struct SparseMatrix {
       for (auto& h : helpers) h.join();
       for (auto& e : helperErr)
         if (e) std::rethrow_exception(e);
-      pt.mark("chain + factor schedules (joined)");
-      if (Fs.ok && Bs.ok) {
-        upload_chain(Fs, chf);
-        upload_chain(Bs, chb);
-        useChain = true;
-      }
-      pt.mark("chain uploads");
+      pt.mark("chain + factor schedules, sweep uploads (joined)");
+      useChain = upF && upB;
     }
     useChainFactor = false;
     facWave = false;
@@ -515,16 +538,22 @@ struct SparseMatrix {
       // otherwise one wavefront per row (3D rows: 45 ms -> see DESIGN.md §7) where the rows fit it;
       // MMX_FACTOR=level keeps the level-scheduled lane-per-row factor
       if (!useChainFactor && facLds && !(fm && (std::strcmp(fm, "level") == 0 || std::strcmp(fm, "global") == 0))) {
-        bool fits = true;
-        std::vector<int> stamp(jaf.size(), -1);
-        for (int i = 0; i < n && fits; ++i) {
-          if (dg[i] - iaf[i] > kFacWaveNL || iaf[i + 1] - dg[i] - 1 > 64) fits = false;
-          // the row image is scattered by all lanes at once: no two entries of A onto one factor slot
-          for (int k = ia[i]; k < ia[i + 1] && fits; ++k) {
-            if (stamp[amap[k]] == i) fits = false;
-            stamp[amap[k]] = i;
+        // the row image is scattered by all lanes at once: no two entries of A onto one factor slot
+        // (rows in parallel; a row's amap is increasing when its columns are, else sorted here)
+        int fitsAll = 1;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(min : fitsAll)
+        for (int i = 0; i < n; ++i) {
+          int ok = (dg[i] - iaf[i] <= kFacWaveNL && iaf[i + 1] - dg[i] - 1 <= 64) ? 1 : 0;
+          bool inc = true;
+          for (int k = ia[i] + 1; k < ia[i + 1] && inc; ++k) inc = amap[k] > amap[k - 1];
+          if (ok && !inc) {
+            std::vector<int> v(amap.begin() + ia[i], amap.begin() + ia[i + 1]);
+            std::sort(v.begin(), v.end());
+            ok = std::adjacent_find(v.begin(), v.end()) == v.end() ? 1 : 0;
           }
+          fitsAll = std::min(fitsAll, ok);
         }
+        const bool fits = fitsAll != 0;
         if (fits) {  // every row once, in forward level order (the forward sweep's levels)
           const std::vector<int>& lv = levF;
           std::vector<int> cnt;
@@ -551,7 +580,17 @@ struct SparseMatrix {
     }
     MMX_HIP(hipStreamSynchronize(st));
     pt.mark("factor set-up + uploads");
+    release(FS);
     symbolic = true;
+  }
+
+  // the schedules' host images (GBs at C4) are freed on a detached thread: their pages go back to
+  // the system off the set-up's critical path
+  template <class T>
+  static void release(T& obj) {
+    auto* dead = new T(std::move(obj));
+    obj = T();
+    std::thread([dead] { delete dead; }).detach();
   }
 
   static int chain_trim() {
@@ -629,10 +668,6 @@ struct SparseMatrix {
     c.val.alloc(std::max<long long>(c.nent, 1));
     c.dval.alloc(std::max<long long>(c.nslot, 1));
     const char* pe = getenv("MMX_CHAIN_PROF");
-    if (pe && atoi(pe) && !d_cprof.p) {
-      d_cprof.alloc(1024);
-      MMX_HIP(hipMemsetAsync(d_cprof.p, 0, 1024 * sizeof(unsigned long long), st));
-    }
     c.args = ChainArgs{c.bandSlot.p, c.bandT.p, c.bandImp.p, c.bandNImp.p, c.laneStart.p, c.laneLen.p, c.laneSkew.p,
                        c.laneNs.p, c.bandE.p, c.val.p, codePtr, c.dval.p, c.impRow.p, c.impSlot.p, c.impWait.p, c.impNeed.p,
                        c.bandOrder.p, S.nbands, S.R, S.RI, S.seg ? 1 : 0, S.G,
@@ -956,18 +991,28 @@ int mmx_struc_mesh_pattern(mmx_struc s, int dim, int nF, const int32_t* F) {
     const int D = dim, nP = s->s.n / D;
     if (nP * D != s->s.n) throw Error(MMADMM_ERR_INVALID, "structure size is not dim * nodes");
     // node adjacency first (every vertex pair of every simplex, flat CSR), then D x D blocks
+    // (counts and fills in parallel: a node's list is sorted below, so the order it is filled in
+    // does not matter)
     std::vector<int> cnt(nP + 1, 0);
+    int badv = 0;
+#pragma omp parallel for schedule(static) reduction(max : badv)
     for (long long k = 0; k < (long long)nF * (D + 1); ++k) {
       const int va = F[k];
-      if (va < 0 || va >= nP) throw Error(MMADMM_ERR_INVALID, "simplex vertex out of range");
-      cnt[va + 1] += D + 1;
+      if (va < 0 || va >= nP) {
+        badv = 1;
+        continue;
+      }
+      __atomic_fetch_add(&cnt[va + 1], D + 1, __ATOMIC_RELAXED);
     }
+    if (badv) throw Error(MMADMM_ERR_INVALID, "simplex vertex out of range");
     for (int v = 0; v < nP; ++v) cnt[v + 1] += cnt[v];
     std::vector<int> nb(cnt[nP]), fill(cnt.begin(), cnt.end() - 1);
+#pragma omp parallel for schedule(static)
     for (int t = 0; t < nF; ++t)
       for (int a = 0; a <= D; ++a) {
         const int va = F[(size_t)t * (D + 1) + a];
-        for (int b = 0; b <= D; ++b) nb[fill[va]++] = F[(size_t)t * (D + 1) + b];
+        const int o = __atomic_fetch_add(&fill[va], D + 1, __ATOMIC_RELAXED);
+        for (int b = 0; b <= D; ++b) nb[o + b] = F[(size_t)t * (D + 1) + b];
       }
     std::vector<int> nu(nP);  // distinct neighbours (itself included) of every node
 #pragma omp parallel for schedule(dynamic, 4096)
