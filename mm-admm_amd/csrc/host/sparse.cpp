@@ -802,10 +802,16 @@ struct SparseMatrix {
       launch_sweep(true, pro, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permf.p, nchf, src, p, d_res.p, d_avbar.p, d_sc.p,
                    nullptr, d_gy.p, nullptr, ey, tk, errw(), st);
     const unsigned ex = next_epoch();
-    if (useChain)
-      launch_chain_sweep(false, 0, chb.E, chb.args, nullptr, nullptr, nullptr, nullptr, nullptr, d_gy.p, d_gx.p, out, ex,
-                         tk + 1, errw(), st);
-    else
+    // the backward sweep's result taken from the granules it publishes for every row anyway, by a
+    // vector pass after it: one store less per row on the compute wave (n = 2 M: sweeps 2.14-2.17 ->
+    // 2.02 ms, solve 47.7-48.2 -> 45.8-46.0 ms; MMX_BWD_GRAN=0: the sweep stores it)
+    const char* bg = getenv("MMX_BWD_GRAN");
+    const bool fromGran = !(bg && atoi(bg) == 0);
+    if (useChain) {
+      launch_chain_sweep(false, 0, chb.E, chb.args, nullptr, nullptr, nullptr, nullptr, nullptr, d_gy.p, d_gx.p,
+                         fromGran ? nullptr : out, ex, tk + 1, errw(), st);
+      if (fromGran) launch_gran_extract(n, d_gx.p, out, st);
+    } else
       launch_sweep(false, 0, d_iaf.p, d_jaf.p, d_dg.p, d_af.p, d_permb.p, nchb, nullptr, nullptr, nullptr, nullptr,
                    nullptr, d_gy.p, d_gx.p, out, ex, tk + 1, errw(), st);
     MMX_HIP(hipGetLastError());
@@ -859,14 +865,29 @@ struct SparseMatrix {
     MMX_HIP(hipMemcpyAsync(&d_sc.p->ctol, &ctol, sizeof(double), hipMemcpyHostToDevice, st));
     launch_cgs_fin(0, d_part.p, gv, d_sc.p, st);
     const double* tol = tolSet ? d_tol.p : nullptr;
+    // the forward sweeps' CG-STAB prologues (p and s updates) as vector passes before them, so the
+    // sweeps read one operand and store nothing but their results (n = 2 M: average sweep 2.61 ->
+    // 2.16-2.20 ms, solve 55.6 -> 48.5-49.0 ms; MMX_CGS_UNFUSE=0: fused into the forward sweeps)
+    const char* uf = getenv("MMX_CGS_UNFUSE");
+    const bool unfuse = !(uf && atoi(uf) == 0);
     int conv = 0, it = 0;
     for (int iter = 1; iter <= p.nitmax; ++iter) {
       ++it;
       MMX_HIP(hipMemsetAsync(tickets(), 0, 8 * sizeof(unsigned), st));
-      ilu_apply(1, nullptr, d_p.p, d_vbar.p, tickets());          // p update; vbar = (LU)^-1 p
+      if (unfuse) {  // the prologues as vector passes, the forward sweeps reading one operand
+        launch_cgs_pro(1, n, d_res.p, d_avbar.p, d_p.p, d_sc.p, st);
+        ilu_apply(0, d_p.p, nullptr, d_vbar.p, tickets());
+      } else {
+        ilu_apply(1, nullptr, d_p.p, d_vbar.p, tickets());          // p update; vbar = (LU)^-1 p
+      }
       spmv(1, d_vbar.p, d_avbar.p, d_res0.p);                      // avbar = A vbar; (res0, avbar)
       launch_cgs_fin(1, d_part.p, nblk, d_sc.p, st);               // alpha
-      ilu_apply(2, nullptr, d_s.p, d_z.p, tickets() + 2);          // s = res - alpha avbar; z = (LU)^-1 s
+      if (unfuse) {
+        launch_cgs_pro(2, n, d_res.p, d_avbar.p, d_s.p, d_sc.p, st);
+        ilu_apply(0, d_s.p, nullptr, d_z.p, tickets() + 2);
+      } else {
+        ilu_apply(2, nullptr, d_s.p, d_z.p, tickets() + 2);          // s = res - alpha avbar; z = (LU)^-1 s
+      }
       spmv(2, d_z.p, d_t.p, d_s.p);                                // t = A z; (t, s), (t, t)
       launch_cgs_fin(2, d_part.p, nblk, d_sc.p, st);               // omega
       launch_cgs_update(n, d_vbar.p, d_z.p, d_s.p, d_t.p, d_res0.p, tol, d_xout, d_res.p, d_sc.p, d_part.p, st);

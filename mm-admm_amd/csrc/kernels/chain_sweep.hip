@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(256) k_chain_sweep(ChainArgs ca, const double*
                                    __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(gout + 2 * (size_t)row + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-                if (!FWD) out[row] = acc;
+                if (!FWD && out) out[row] = acc;  // (out = nullptr: taken from the granules afterwards)
                 if (FWD && PRO != 0) pvec[row] = f.init[g];
                 prev = acc;
               }

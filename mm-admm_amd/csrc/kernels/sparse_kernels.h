@@ -154,6 +154,11 @@ void launch_cgs_init(int mode, int n, const double* b, double* x, double* res, d
 // partials[b*2+1] = block sum of x.y
 void launch_dot_into(int n, const double* x, const double* y, double* partials, hipStream_t st);
 // sol += alpha vbar + omega z; res = s - omega t; partials [res^2, res0.res, #|step|>|toler|].
+// out[i] = the value in row i's granule (gx / gy: {tag | lo, tag | hi})
+void launch_gran_extract(int n, const uint64_t* g, double* out, hipStream_t st);
+// the forward sweep's prologue as its own pass: mode 1 out = res + beta (out - omega avbar), 2 out = res - alpha avbar
+void launch_cgs_pro(int mode, int n, const double* res, const double* avbar, double* out, const CgsScalars* sc,
+                    hipStream_t st);
 void launch_cgs_update(int n, const double* vbar, const double* z, const double* s, const double* t,
                        const double* res0, const double* toler, double* x, double* res, const CgsScalars* sc,
                        double* partials, hipStream_t st);

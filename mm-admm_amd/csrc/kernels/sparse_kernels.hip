@@ -812,6 +812,33 @@ __global__ void __launch_bounds__(kVecBlock) k_cgs_update(int n, const double* _
   }
 }
 
+// The forward sweeps' CG-STAB prologues as a vector pass (MMX_CGS_UNFUSE): MODE 1 p = res + beta
+// (p - omega avbar), MODE 2 s = res - alpha avbar -- the operations of the fused forms in
+// chain_sweep.hip / k_sweep, so the sweep that follows reads one operand
+template <int MODE>
+__global__ void __launch_bounds__(kVecBlock) k_cgs_pro(int n, const double* __restrict__ res,
+                                                      const double* __restrict__ avbar, double* __restrict__ out,
+                                                      const CgsScalars* __restrict__ sc) {
+  const double beta = sc->beta, omega = sc->omega, alpha = sc->alpha;
+  for (int i = blockIdx.x * kVecBlock + threadIdx.x; i < n; i += gridDim.x * kVecBlock) {
+    if constexpr (MODE == 1)
+      out[i] = res[i] + beta * (out[i] - omega * avbar[i]);
+    else
+      out[i] = res[i] - alpha * avbar[i];
+  }
+}
+
+// a sweep's result from its granules {tag | lo, tag | hi} (every row publishes one)
+__global__ void __launch_bounds__(kVecBlock) k_gran_extract(int n, const uint64_t* __restrict__ g, double* __restrict__ out) {
+  for (int i = blockIdx.x * kVecBlock + threadIdx.x; i < n; i += gridDim.x * kVecBlock) {
+    const uint64_t lo = g[2 * (size_t)i] & 0xffffffffull, hi = g[2 * (size_t)i + 1] & 0xffffffffull;
+    out[i] = __longlong_as_double((long long)((hi << 32) | lo));
+  }
+}
+void launch_gran_extract(int n, const uint64_t* g, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_gran_extract, dim3(vec_grid(n)), dim3(kVecBlock), 0, st, n, g, out);
+}
+
 // Scalar finalisers: fixed-shape reduction of the per-block partials, then the CG-STAB scalar
 // recurrences exactly as written in acc_scaler.
 template <int MODE>
@@ -1059,6 +1086,13 @@ void launch_dot_into(int n, const double* x, const double* y, double* partials, 
   hipLaunchKernelGGL(k_dot_into, dim3(vec_grid(n)), dim3(kVecBlock), 0, st, n, x, y, partials);
 }
 
+void launch_cgs_pro(int mode, int n, const double* res, const double* avbar, double* out, const CgsScalars* sc,
+                    hipStream_t st) {
+  if (mode == 1)
+    hipLaunchKernelGGL(k_cgs_pro<1>, dim3(vec_grid(n)), dim3(kVecBlock), 0, st, n, res, avbar, out, sc);
+  else
+    hipLaunchKernelGGL(k_cgs_pro<2>, dim3(vec_grid(n)), dim3(kVecBlock), 0, st, n, res, avbar, out, sc);
+}
 void launch_cgs_update(int n, const double* vbar, const double* z, const double* s, const double* t, const double* res0,
                        const double* toler, double* x, double* res, const CgsScalars* sc, double* partials,
                        hipStream_t st) {
