@@ -145,6 +145,40 @@ def test_mesh_jacobian_vs_restatement(la, dim, n, seed, shift):
     assert A.solve(p, x2) == it and _bit(x, x2)
 
 
+@pytest.mark.parametrize("dim,n", [(2, 101), (3, 12)])
+@pytest.mark.parametrize("unfuse,gran", [("0", "0"), ("0", "1"), ("1", "0")])
+def test_cgstab_prologue_and_result_paths_bitwise(la, dim, n, unfuse, gran, monkeypatch):
+    """Round 6: the CG-STAB p / s updates as vector passes before plain forward sweeps
+    (MMX_CGS_UNFUSE, default 1) and the backward sweep's result taken from its granules
+    (MMX_BWD_GRAN, default 1) against the fused / stored forms: iterates and counts bit-identical,
+    and equal to the restatement in the GPU's reduction order."""
+    m = oracle_py.Mesh.rect(dim, n)
+    ia, ja = L.mesh_pattern(dim, m.nP, m.F)
+    N = len(ia) - 1
+    rng = np.random.default_rng(7)
+    a = rng.uniform(-1, 1, len(ja))
+    rows = np.repeat(np.arange(N), np.diff(ia))
+    a[np.nonzero(ja == rows)[0]] = np.add.reduceat(np.abs(a), ia[:-1]) * 0.3 + 1.0
+    b = rng.uniform(-1, 1, N)
+
+    def run():
+        A = _matrix(la, ia, ja, a, b)
+        p = la.ParamIter.mesh()
+        A.sfac(p)
+        x = np.zeros(N)
+        it = A.solve(p, x)
+        A.close()
+        return it, x
+
+    it0, x0 = run()
+    monkeypatch.setenv("MMX_CGS_UNFUSE", unfuse)
+    monkeypatch.setenv("MMX_BWD_GRAN", gran)
+    it1, x1 = run()
+    assert it0 == it1 and _bit(x0, x1)
+    xt, itt, _ = L.solve(ia, ja, a, b, tree=True)
+    assert it0 == itt and _bit(x0, xt)
+
+
 def test_long_rows_arrow(la):
     # an arrow matrix: row 0 and column 0 full (row 0 longer than one SpMV tile, and every
     # backward-sweep row depends on the last ones)
