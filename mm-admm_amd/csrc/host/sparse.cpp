@@ -520,7 +520,8 @@ struct SparseMatrix {
       for (auto& e : helperErr)
         if (e) std::rethrow_exception(e);
       pt.mark("chain + factor schedules, sweep uploads (joined)");
-      useChain = upF && upB;
+      // (the sweeps address their granules through 32-bit byte offsets: rows < 2^27)
+      useChain = upF && upB && n < (1 << 27);
     }
     useChainFactor = false;
     facWave = false;
@@ -529,7 +530,7 @@ struct SparseMatrix {
       // 12.3 ms against 25.0 ms at n = 2 M (profiles/r03/chain_factor/);
       // MMX_FACTOR=level (or global) keeps the level-scheduled factor
       const char* fm = fmode;
-      if (useChain && tryChainFactor) {
+      if (useChain && tryChainFactor && jaf.size() < ((size_t)1 << 27)) {  // (32-bit granule byte offsets)
         if (FS.ok && !(fm && std::strcmp(fm, "wave") == 0)) {
           upload_factor(FS, dg);
           useChainFactor = true;
