@@ -676,6 +676,7 @@ class Engine final : public EngineBase {
 
   // host mirror of bidx<D> (admm_kernels.hip)
   static size_t bIndex(int s, int ij) {
+    if (D == 3 && MMX_B3_PAIRS) return ((size_t)(s >> 6) * K * K + (ij & ~1)) * 64 + 2 * (s & 63) + (ij & 1);
     return ((size_t)(s >> 6) * K * K + ij) * 64 + (s & 63);
   }
 

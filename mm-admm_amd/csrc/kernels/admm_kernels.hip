@@ -550,15 +550,20 @@ struct WaveB {
   // the held rows of the entry matrix DMA'd into LDS at the start of the block (prox_wave_block),
   // so the first pass 1 reads them from there
   static constexpr bool kPre = MMX_WAVE_DMA && kHeld > 0;
+  // 3D with MMX_B3_PAIRS (bidx): the lane's base is 2 lane and entry e at (e & ~1) 64 + (e & 1), so
+  // a row's twelve entries are six 16-byte accesses; otherwise base lane, entry e at e 64
+  static constexpr bool kPairs = !k2 && MMX_B3_PAIRS;
+  static constexpr int kLaneMul = kPairs ? 2 : 1;
+  static __device__ __forceinline__ int eo(int e) { return kPairs ? (e & ~1) * 64 + (e & 1) : e * 64; }
   const gdouble* rd;
   gdouble* wr;
-  ldouble* held;  // &lds[lane], kHeld rows, entries strided by 64
-  __device__ __forceinline__ double get(int i, int j) const { return rd[(i * K + j) * 64]; }
-  __device__ __forceinline__ double heldRow(int i, int j) const { return held[(i * K + j) * 64]; }
-  __device__ __forceinline__ void holdRow(int i, int j, double v) const { held[(i * K + j) * 64] = v; }
+  ldouble* held;  // &lds[kLaneMul lane], kHeld rows in the same layout
+  __device__ __forceinline__ double get(int i, int j) const { return rd[eo(i * K + j)]; }
+  __device__ __forceinline__ double heldRow(int i, int j) const { return held[eo(i * K + j)]; }
+  __device__ __forceinline__ void holdRow(int i, int j, double v) const { held[eo(i * K + j)] = v; }
   // the new Bkinv is read by the next prox only: nontemporal stores keep it out of the way of the
   // rows still to be re-read (C4 prox 2.97 -> 2.77 ms; nontemporal loads: no gain)
-  __device__ __forceinline__ void set(int i, int j, double v) const { __builtin_nontemporal_store(v, &wr[(i * K + j) * 64]); }
+  __device__ __forceinline__ void set(int i, int j, double v) const { __builtin_nontemporal_store(v, &wr[eo(i * K + j)]); }
   __device__ __forceinline__ void advance() { rd = wr; }
   // a pass over the matrix re-reads it: an opaque pointer stops the compiler from forwarding the
   // previous pass's K*K = 144 loads in registers (3D spilled)
@@ -571,6 +576,8 @@ struct WaveB {
 template <int D>
 __device__ __forceinline__ size_t bidx(int s, int ij) {
   constexpr int KK = D * (D + 1) * D * (D + 1);
+  if constexpr (D == 3 && MMX_B3_PAIRS)  // (layout.h) a lane's entries ij, ij + 1 (ij even) adjacent
+    return ((size_t)(s >> 6) * KK + (ij & ~1)) * 64 + 2 * (s & 63) + (ij & 1);
   return ((size_t)(s >> 6) * KK + ij) * 64 + (s & 63);
 }
 
@@ -1275,10 +1282,10 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     zeroFixed<D>(G, fixedBits);
     const double Ihsave = Igt;
     if constexpr (!EXACT) WPROF(1, G[K - 1]);
-    const size_t gb = (size_t)lb * KK * 64 + tid;
+    const size_t gb = (size_t)lb * KK * 64 + WaveB<K>::kLaneMul * tid;
     int its;
     {
-      WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsHeld + tid)};
+      WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsHeld + WaveB<K>::kLaneMul * tid)};
       its = tie ? 0
                 : bfgs_iterations<D, WaveB<K>, EXACT>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     }
@@ -1642,11 +1649,22 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
     // through LDS with 16-byte coalesced loads, then this lane's three rows into registers
     // the block's TB tets in their group of 64: entry ij of tet s0 + t at gb + ij 64 + t
     const size_t gb = (size_t)(s0 >> 6) * KK * 64 + (s0 & 63);
+    static_assert(!MMX_B3_PAIRS || TB == 64, "paired Bkinv layout: whole wave blocks per quad workgroup");
 #pragma unroll 6
     for (int e = tid * 2; e < KK * TB; e += 2 * QW) {
-      const int ij = e / TB, t = e % TB, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
-      const v2nt v = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(Bin + gb + (size_t)ij * 64 + t));
-      *reinterpret_cast<v2nt*>(&img[kk * KB + (r * K + j) * TB + t]) = v;
+      if constexpr (MMX_B3_PAIRS) {  // 16 bytes = entries ij, ij + 1 of one tet (bidx<3>)
+        const int ij = (e / (2 * TB)) * 2, t = (e % (2 * TB)) / 2;
+        const v2nt v = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(Bin + gb - (s0 & 63) + (size_t)e));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = (ij + h) / K, j = ij + h - K * i, kk = i / 3, r = i - 3 * kk;
+          img[kk * KB + (r * K + j) * TB + t] = v[h];
+        }
+      } else {
+        const int ij = e / TB, t = e % TB, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
+        const v2nt v = __builtin_nontemporal_load(reinterpret_cast<const v2nt*>(Bin + gb + (size_t)ij * 64 + t));
+        *reinterpret_cast<v2nt*>(&img[kk * KB + (r * K + j) * TB + t]) = v;
+      }
     }
     // entry (r, j) of this lane's rows at mine[(r K + j) 64]: read into registers by each pass (not
     // held across the blockGrad), the new values written back by the update pass
@@ -1847,9 +1865,20 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
     // the new Bkinv chunk back with 16-byte coalesced stores (inactive tets: the unchanged image)
 #pragma unroll 6
     for (int e = tid * 2; e < KK * TB; e += 2 * QW) {
-      const int ij = e / TB, t = e % TB, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
-      const v2nt v = *reinterpret_cast<const v2nt*>(&img[kk * KB + (r * K + j) * TB + t]);
-      __builtin_nontemporal_store(v, reinterpret_cast<v2nt*>(Bout + gb + (size_t)ij * 64 + t));
+      if constexpr (MMX_B3_PAIRS) {
+        const int ij = (e / (2 * TB)) * 2, t = (e % (2 * TB)) / 2;
+        v2nt v;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = (ij + h) / K, j = ij + h - K * i, kk = i / 3, r = i - 3 * kk;
+          v[h] = img[kk * KB + (r * K + j) * TB + t];
+        }
+        __builtin_nontemporal_store(v, reinterpret_cast<v2nt*>(Bout + gb - (s0 & 63) + (size_t)e));
+      } else {
+        const int ij = e / TB, t = e % TB, i = ij / K, j = ij - K * i, kk = i / 3, r = i - 3 * kk;
+        const v2nt v = *reinterpret_cast<const v2nt*>(&img[kk * KB + (r * K + j) * TB + t]);
+        __builtin_nontemporal_store(v, reinterpret_cast<v2nt*>(Bout + gb + (size_t)ij * 64 + t));
+      }
     }
     block_partials<6, QW>(pv, partials, lb);
     if constexpr (EXACT) __syncthreads();  // the partials scratch is reused by the next block

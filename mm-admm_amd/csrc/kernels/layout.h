@@ -22,6 +22,11 @@
 // chain-sweep stage images (chain_sweep.hip, host/sparse.cpp upload_chain): entries lane-interleaved
 // for 16-byte LDS reads (MMX_CHAIN_VEC), entry codes 16-bit (MMX_CHAIN_CODE16; 32-bit otherwise,
 // except the 48-entry stages, always 16-bit)
+// 3D Bkinv wave blocks with each lane's entries in pairs: entry ij of simplex s at
+// ((s / 64) K^2 + (ij & ~1)) 64 + 2 (s % 64) + (ij & 1), so a lane's row is 16-byte accesses
+#ifndef MMX_B3_PAIRS
+#define MMX_B3_PAIRS 1
+#endif
 #ifndef MMX_CHAIN_VEC
 #define MMX_CHAIN_VEC 1
 #endif
@@ -38,5 +43,5 @@ constexpr unsigned kLayoutWord = 0x4d000000u | ((unsigned)(MMX_ZU_INTER != 0) <<
                                  ((unsigned)(MMX_CHAIN_VEC != 0) << 1) | ((unsigned)(MMX_CHAIN_CODE16 != 0) << 2) |
                                  (((unsigned)MMX_SPMV_TILE / 256u & 0xFu) << 4) |
                                  (((unsigned)MMX_SPMV_BLOCK / 64u & 0xFu) << 8) | ((kLayoutPartials & 0xFu) << 12) |
-                                 ((kLayoutBkinvBlock / 64u & 0x3u) << 16);
+                                 ((kLayoutBkinvBlock / 64u & 0x3u) << 16) | ((unsigned)(MMX_B3_PAIRS != 0) << 18);
 }  // namespace mmx
