@@ -528,6 +528,9 @@ typedef __attribute__((address_space(3))) double ldouble;
 #ifndef MMX_WAVE_DMA
 #define MMX_WAVE_DMA 1
 #endif
+#ifndef MMX_ROW_PIPE_FULL
+#define MMX_ROW_PIPE_FULL 3  // the same for the 3D prox with a general (full-row) monitor grid
+#endif
 #ifndef MMX_ROW_PIPE1
 #define MMX_ROW_PIPE1 6  // pass 1: global rows requested ahead (with kPre all of rows 6-11 while 0-5 come from LDS); C4 2 -> 6: -1.1%
 #endif
@@ -538,12 +541,12 @@ typedef __attribute__((address_space(3))) double ldouble;
 #define MMX_ROW_PIPE3 2  // pass 3
 #endif
 // 2D (K = 6, k_prox_wave<2>): every row held in LDS, so no streamed-row queues
-template <int K>
+template <int K, int PIPE = MMX_ROW_PIPE>
 struct WaveB {
   static constexpr bool k2 = (K == 6);
   static constexpr bool kRowFence = true;
   static constexpr bool kRolled = true;
-  static constexpr int kPipe = k2 ? 0 : MMX_ROW_PIPE;
+  static constexpr int kPipe = k2 ? 0 : PIPE;
   static constexpr int kPipe1 = k2 ? 0 : MMX_ROW_PIPE1, kPipe2 = k2 ? 0 : MMX_ROW_PIPE2, kPipe3 = k2 ? 0 : MMX_ROW_PIPE3;
   static constexpr int kHeld = k2 ? K : MMX_WAVE_HELD;  // rows kept in LDS from pass 1 to passes 2 and 3
   static constexpr bool kCarry = !k2 && MMX_WAVE_CARRY;
@@ -1285,9 +1288,11 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
     const size_t gb = (size_t)lb * KK * 64 + WaveB<K>::kLaneMul * tid;
     int its;
     {
-      WaveB<K> Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsHeld + WaveB<K>::kLaneMul * tid)};
-      its = tie ? 0
-                : bfgs_iterations<D, WaveB<K>, EXACT>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
+      // the general-monitor instance requests its update-pass rows one further ahead (C4 prox
+      // 2.291 -> 2.264 ms; the isotropic instance is slower with it: C4 moving bump 408 -> 405 it/s)
+      using WB = WaveB<K, ISO ? MMX_ROW_PIPE : MMX_ROW_PIPE_FULL>;
+      WB Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsHeld + WaveB<K>::kLaneMul * tid)};
+      its = tie ? 0 : bfgs_iterations<D, WB, EXACT>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     }
     double dual2 = 0.0;
 #pragma unroll
