@@ -676,7 +676,7 @@ __device__ __forceinline__ void bfgs_update_row(BA& B, int i, double pki, const 
 // UR consecutive rows i..i+UR-1 of the update in one trip (3D): the products y_q p_j are formed
 // once for the UR rows instead of once per row; every entry's operations are bfgs_update_row's.
 #ifndef MMX_UPD_ROWS
-#define MMX_UPD_ROWS 3  // 3D: rows of the update pass per trip (C4 prox 2.755 -> 2.719 ms; 2 and 4 rows: no gain)
+#define MMX_UPD_ROWS 2  // 3D: rows of the update pass per trip (round 3: 1 -> 3 rows 2.755 -> 2.719 ms; round 6, paired layout: 3 -> 2 rows 2.272 -> 2.255 ms, 4 rows 2.29)
 #endif
 template <int D, bool EXACT, int UR, class BA, int K>
 __device__ __forceinline__ void bfgs_update_rows(BA& B, int i, const double (&pki)[UR], const double (&row)[UR][K],
