@@ -12,6 +12,7 @@
 #include <exception>
 #include <string>
 #include <thread>
+#include <queue>
 #include <vector>
 
 #include "../../../include/mmx_sparse.h"
@@ -138,57 +139,53 @@ void symbolic_ilu(int n, const std::vector<int>& ia, const std::vector<int>& ja,
     }
     return;
   }
-  const int END = n + 1, MAXINT = 2 * n;
-  std::vector<int> list(n, END), lrow(n, MAXINT), tmp;
+  // Level of fill, row by row (IKJ order): a row starts from its pattern at level 0; its pivots k < i
+  // are taken in ascending order -- fill columns below i join them as they appear, always above the
+  // pivot that creates them, so a min-heap delivers every pivot after all pivots that can change
+  // its level -- and each pivot's upper entries j propose level lev(i, k) + lev(k, j) + 1: an
+  // existing entry keeps the smaller level, a new one enters when the proposal is at most `level`
+  // (the fill rule of scaler_ILU::sfac2 / merge2, lib/LASolver/ILU_class.cpp:17-90)
+  constexpr int kAbsent = INT32_MAX;
   std::vector<std::vector<int>> rj(n), rl(n);
+  std::vector<int> lev(n, kAbsent), cols;
   dgRel.assign(n, -1);
   for (int i = 0; i < n; ++i) {
-    tmp.assign(ja.begin() + ia[i], ja.begin() + ia[i + 1]);
-    if (tmp.empty()) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " is empty (no diagonal)");
-    std::sort(tmp.begin(), tmp.end());
-    for (size_t q = 1; q < tmp.size(); ++q)
-      if (tmp[q] == tmp[q - 1]) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has duplicate columns");
-    const int first = tmp[0];
-    for (size_t q = 1; q < tmp.size(); ++q) list[tmp[q - 1]] = tmp[q];
-    list[tmp.back()] = END;
-    for (int c : tmp) lrow[c] = 0;
-    // merge2
-    int next = first;
-    while (next < i) {
-      int oldlst = next, nxtlst = list[next];
-      const int row = next, levlow = lrow[oldlst];
-      const std::vector<int>& J = rj[row];
-      const std::vector<int>& Lv = rl[row];
-      for (int ii = dgRel[row] + 1; ii < (int)J.size(); ++ii) {
-        while (J[ii] > nxtlst) {
-          oldlst = nxtlst;
-          nxtlst = list[oldlst];
-        }
-        if (J[ii] < nxtlst) {
-          const int levnew = levlow + Lv[ii] + 1;
-          if (levnew <= level) {
-            list[oldlst] = J[ii];
-            list[J[ii]] = nxtlst;
-            oldlst = J[ii];
-            lrow[oldlst] = levnew;
-          }
-        } else {
-          oldlst = nxtlst;
-          const int levup = Lv[ii];
-          lrow[oldlst] = std::min(levup + levlow + 1, lrow[oldlst]);
-          nxtlst = list[oldlst];
+    cols.assign(ja.begin() + ia[i], ja.begin() + ia[i + 1]);
+    if (cols.empty()) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " is empty (no diagonal)");
+    std::sort(cols.begin(), cols.end());
+    if (std::adjacent_find(cols.begin(), cols.end()) != cols.end())
+      throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has duplicate columns");
+    std::priority_queue<int, std::vector<int>, std::greater<int>> pivots;
+    for (int c : cols) {
+      lev[c] = 0;
+      if (c < i) pivots.push(c);
+    }
+    while (!pivots.empty()) {
+      const int k = pivots.top();
+      pivots.pop();
+      const int lk = lev[k];
+      const std::vector<int>& J = rj[k];
+      const std::vector<int>& Lv = rl[k];
+      for (size_t q = (size_t)dgRel[k] + 1; q < J.size(); ++q) {
+        const int j = J[q], cand = lk + Lv[q] + 1;
+        if (lev[j] != kAbsent) {
+          lev[j] = std::min(lev[j], cand);
+        } else if (cand <= level) {
+          lev[j] = cand;
+          cols.push_back(j);
+          if (j < i) pivots.push(j);
         }
       }
-      next = list[next];
     }
-    for (next = first; next != END; next = list[next]) {
-      if (next == i) dgRel[i] = (int)rj[i].size();
-      rj[i].push_back(next);
-      rl[i].push_back(lrow[next]);
-      lrow[next] = MAXINT;
+    std::sort(cols.begin(), cols.end());
+    rj[i] = cols;
+    rl[i].resize(cols.size());
+    for (size_t q = 0; q < cols.size(); ++q) {
+      if (cols[q] == i) dgRel[i] = (int)q;
+      rl[i][q] = lev[cols[q]];
+      lev[cols[q]] = kAbsent;
     }
     if (dgRel[i] < 0) throw Error(MMADMM_ERR_INVALID, "row " + std::to_string(i) + " has no diagonal entry");
-    if (level == 0) std::vector<int>().swap(rl[i]), rl[i].assign(rj[i].size(), 0);
   }
   iaf.assign(n + 1, 0);
   for (int i = 0; i < n; ++i) iaf[i + 1] = iaf[i] + (int)rj[i].size();

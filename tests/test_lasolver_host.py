@@ -25,6 +25,27 @@ def test_symbolic_ilu_k_matches_reference(tag, level):
     assert np.array_equal(dg, g[f"{tag}_l{level}_diag"])
 
 
+@pytest.mark.skipif(not L.ref_available(), reason="the reference LASolver build (oracle/_ref) is not present")
+@pytest.mark.parametrize("seed", range(6))
+def test_symbolic_ilu_k_random_patterns_match_reference_build(seed):
+    """Round 6: the level-of-fill symbolic factor (a heap-driven row merge, sparse.cpp) against the
+    reference's own scaler_ILU built in place (oracle/_ref) on random unsymmetric patterns, levels
+    1-3, where fill joins the pivots of its own row."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(20, 200))
+    rows, cols = [], []
+    for i in range(n):
+        c = set(rng.integers(0, n, int(rng.integers(1, 8))).tolist()) | {i}
+        rows += [i] * len(c)
+        cols += sorted(c)
+    ia, ja = L.pack(n, np.array(rows, np.int32), np.array(cols, np.int32))
+    ia, ja = np.asarray(ia), np.asarray(ja)
+    for level in (1, 2, 3):
+        iaf, jaf, _ = la.ilu_symbolic(ia, ja, level)
+        riaf, rjaf = L.ref_ilu(ia, ja, np.ones(len(ja)), level)[:2]
+        assert np.array_equal(iaf, riaf) and np.array_equal(jaf, rjaf), level
+
+
 def test_symbolic_ilu0_is_the_pattern():
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "lasolver", "rect2d_9_tight.npz"))
     iaf, jaf, dg = la.ilu_symbolic(g["ia"], g["ja"], 0)
