@@ -190,10 +190,12 @@ class Engine final : public EngineBase {
     interior_.upload(interior.data(), interior.size(), st_);
     incPtr_.upload(plan_.incPtr.data(), plan_.incPtr.size(), st_);
     incOff_.upload(plan_.incSrc.data(), plan_.incSrc.size(), st_);
-    {  // the x-update terms in the slot layout (DeviceMesh::tslot): 3D only (C4: prox +0.09 ms, x-update
-       // 0.36 -> 0.18 ms; 2D C3: prox +0.027 ms, x-update -0.024 ms); MMX_TSLOT=0/1 overrides
+    {  // the x-update terms in the slot layout (DeviceMesh::tslot): 3D (C4: prox +0.09 ms, x-update
+       // 0.36 -> 0.18 ms) and small 2D meshes, whose prox is under two rounds of the chip's resident
+       // waves, so the terms' stores cost it little (C2: 14,754 -> 15,037 it/s; C3: prox +0.034 ms,
+       // x-update -0.018 ms, 2,506 -> 2,412 it/s); MMX_TSLOT=0/1 overrides
       const char* ts = getenv("MMX_TSLOT");
-      tslotOn_ = ts ? atoi(ts) != 0 : (D == 3);
+      tslotOn_ = ts ? atoi(ts) != 0 : (D == 3 || nF_ <= kTslot2dMax);
       const char* sp = getenv("MMX_SPIN");
       spinWait_ = !(sp && atoi(sp) == 0);
       const char* zx = getenv("MMX_ZX");  // 0: the step's z = D x by k_gather_z (DeviceMesh::zx)
@@ -1638,6 +1640,7 @@ class Engine final : public EngineBase {
       MMX_HIP(hipMemsetAsync(u_.p, 0, u_.n * sizeof(double), st_));
   }
   bool spinWait_ = true;         // MMX_SPIN (waitStream)
+  static constexpr int kTslot2dMax = 2 * 2048 * 64;  // 2D slot terms up to two rounds of resident prox waves
   double* res_ = nullptr;        // the reductions' results: results_.p, or the device view of resH_
   double* resH_ = nullptr;       // pinned, mapped results (one rank)
   hipEvent_t evSync_ = nullptr;
