@@ -199,7 +199,7 @@ class Engine final : public EngineBase {
       const char* sp = getenv("MMX_SPIN");
       spinWait_ = !(sp && atoi(sp) == 0);
       const char* zx = getenv("MMX_ZX");  // 0: the step's z = D x by k_gather_z (DeviceMesh::zx)
-      zFromX_ = D == 2 && !(zx && atoi(zx) == 0);  // partitions too: the first pack reads zx (PackZX)
+      zFromX_ = !(zx && atoi(zx) == 0);  // 2D and 3D, partitions too: the first pack reads zx (PackZX)
       const char* ov = getenv("MMX_OVERLAP");  // 0: the halo exchange before the whole x-update
       overlap_ = nranks_ > 1 && !(ov && atoi(ov) == 0);
       const char* fp = getenv("MMX_FUSE_PRED");  // 0: k_predict runs in every step (DeviceMesh::predBar)

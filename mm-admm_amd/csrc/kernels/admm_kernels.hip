@@ -944,7 +944,7 @@ __device__ __forceinline__ void prox_simplex(const DeviceMesh<D>& m, double tol,
   gatherX<D>(x, f, dx);
   double* zs = zg + zu_base<D>(s);
   double* us = ug + zu_base<D>(s);
-  if (D == 2 && m.zx)
+  if (m.zx)
     gatherX<D>(m.zx, f, z);  // the step's first prox: z = D zx (DeviceMesh::zx)
   else
 #pragma unroll
@@ -1236,11 +1236,13 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
   double* us = ug + zu_base<D>(s);
   double* gc = m.gcache + (size_t)s * K;
   double z[K], dx[K], gcv[K];
+  if (m.zx)
+    gatherX<D>(m.zx, f, z);  // the step's first prox: z = D zx (DeviceMesh::zx)
+  else
 #pragma unroll
-  for (int i = 0; i < K; ++i) {
-    z[i] = zs[zu_i<D>(i)];
-    dx[i] = us[zu_i<D>(i)];
-  }
+    for (int i = 0; i < K; ++i) z[i] = zs[zu_i<D>(i)];
+#pragma unroll
+  for (int i = 0; i < K; ++i) dx[i] = us[zu_i<D>(i)];
   if (!EXACT && useCache) {
 #pragma unroll
     for (int i = 0; i < K; ++i) gcv[i] = gc[i];
@@ -1294,10 +1296,15 @@ __device__ __forceinline__ void prox_wave_block(const DeviceMesh<D>& m, double t
       WB Bacc{(const gdouble*)(Bin + gb), (gdouble*)(Bout + gb), (ldouble*)(ldsHeld + WaveB<K>::kLaneMul * tid)};
       its = tie ? 0 : bfgs_iterations<D, WB, EXACT>(Bacc, g, fc, z, xi, dx, G, fixedBits, tol, bad, gc, &tie);
     }
-    double dual2 = 0.0;
+    double dual2 = 0.0, z0[K];  // the entry z again (from zx on a step's first prox)
+    if (m.zx)
+      gatherX<D>(m.zx, f, z0);
+    else
+#pragma unroll
+      for (int i = 0; i < K; ++i) z0[i] = zs[zu_i<D>(i)];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      const double d = z[i] - zs[zu_i<D>(i)];
+      const double d = z[i] - z0[i];
       dual2 += d * d;
     }
     pv[0] = Ihsave;
@@ -1634,7 +1641,7 @@ __global__ void __launch_bounds__(QW, 2) k_prox_quad(DeviceMesh<3> m, double tol
     double zo[3], z0[3], dxo[3], go[3], Igt = 0.0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      zo[c] = zs[c];
+      zo[c] = m.zx ? m.zx[(size_t)fk * 3 + c] : zs[c];  // a step's first prox: z = D zx (DeviceMesh::zx)
       z0[c] = zo[c];
       dxo[c] = x[(size_t)fk * 3 + c] + us[c];  // DXpU = D x + uBar
     }
@@ -2474,7 +2481,7 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   }
   const bool ts = useTslot && m.tslot;
   const bool rem = m.remote != nullptr;
-  if (D == 2 && m.zx && !resid && !ts) {  // a step's first x-update: z from DeviceMesh::zx
+  if (m.zx && !resid && !ts) {  // a step's first x-update: z from DeviceMesh::zx
 #define MMX_XU_ZX(P, R)                                                                                        \
   hipLaunchKernelGGL((k_xupdate<D, false, false, true, P, R>), dim3(*nblocks), dim3(kBlock), 0, st, m, sc, xBar, z, \
                      u, x, partials, xcd_map())
