@@ -290,7 +290,9 @@ class Engine final : public EngineBase {
     }
     // prox workgroups take 16 (3D quad) to 256 simplices; node kernels pad their grid to a multiple of 8 (XCD map)
     // (k_prox_quad: 16 tets per workgroup)
-    const size_t maxBlocks = std::max<size_t>(1, std::max((nF_ + 15) / 16, (nP_ + 255) / 256 + 16));
+    // (at least 16 x 256: the persistent x-update sweep writes one record per workgroup, 256 per CU
+    // count of MMX_XUP_SWEEP, twice on a partition)
+    const size_t maxBlocks = std::max<size_t>(4096, std::max((nF_ + 15) / 16, (nP_ + 255) / 256 + 16));
     maxBlocks_ = maxBlocks;
     partA_.alloc(maxBlocks * kNumPartials);
     partB_.alloc(maxBlocks * kNumPartials);

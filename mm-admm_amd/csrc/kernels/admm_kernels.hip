@@ -404,16 +404,25 @@ __global__ void __launch_bounds__(kBlock) k_xupdate(DeviceMesh<D> m, StepScalars
 // terms a round gathers are mostly still in that XCD's L2 for the neighbouring rounds.
 // CH: incident slots requested at once per node (3D slot terms: 24 covers a grid vertex's
 // tetrahedra in one batch)
-template <int D, bool TS, int CH>
+// RESID: the primal residual too (a step's last iteration, or every iteration with the early exit):
+// each lane sums its nodes' terms in its round order and the workgroup's partial record is
+// blockIdx.x -- a fixed grouping for a fixed grid, so runs are bit-reproducible
+template <int D, bool TS, int CH, bool RESID = false>
 __global__ void __launch_bounds__(kBlock) k_xupdate_sweep(DeviceMesh<D> m, StepScalars sc,
                                                            const double* __restrict__ xBar,
                                                            const double* __restrict__ z, const double* __restrict__ u,
-                                                           double* __restrict__ x, int n8) {
+                                                           double* __restrict__ x, int n8, double* __restrict__ partials) {
   const int c = (int)(blockIdx.x % 8), w = (int)(blockIdx.x / 8), per = (int)(gridDim.x / 8);
   const int lo = m.xupLo + c * n8, hi = min(lo + n8, m.xupHi);
-  double pv[3];
-  for (int idx = lo + w * kBlock + (int)threadIdx.x; idx < hi; idx += per * kBlock)
-    xupdate_node<D, false, TS, CH>(m, sc, xBar, z, u, x, idx, pv);
+  double pv[3], r2 = 0.0;
+  for (int idx = lo + w * kBlock + (int)threadIdx.x; idx < hi; idx += per * kBlock) {
+    xupdate_node<D, RESID, TS, CH>(m, sc, xBar, z, u, x, idx, pv);
+    if constexpr (RESID) r2 += pv[2];
+  }
+  if constexpr (RESID) {
+    double q[3] = {0.0, 0.0, r2};
+    block_partials<3>(q, partials, (int)blockIdx.x);
+  }
 }
 
 // k x k inverse: unblocked partial-pivot LU + substitution (mirrors the oracle's restatement
@@ -2469,6 +2478,10 @@ void launch_predict(const DeviceMesh<D>& m, int mode, const double* gs, double* 
   hipLaunchKernelGGL(k_predict<D>, dim3(nblk_xcd(m.nP)), dim3(kBlock), 0, st, m, mode, gs, x, xPrev, xBar,
                      dt_over_tau, xcd_map());
 }
+static bool xup_sweep_resid() {
+  const char* e = getenv("MMX_XUP_SWEEP_RESID");
+  return !(e && atoi(e) == 0);
+}
 template <int D>
 void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double* xBar, const double* z,
                     const double* u, double* x, double* partials, int* nblocks, bool resid, hipStream_t st,
@@ -2500,18 +2513,25 @@ void launch_xupdate(const DeviceMesh<D>& m, const StepScalars& sc, const double*
   // would lose predictX silently
   if (m.predBar || m.predPrev)
     throw std::logic_error("launch_xupdate: predBar set for an x-update that cannot fuse predictX");
-  if (!resid && m.xupSweep > 0) {  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU
+  // the sweep (persistent) form, MMX_XUP_SWEEP workgroups per CU; with the residual in the slot-term
+  // form (3D): C4's last x-update of a step 0.334 -> ~0.17 ms (MMX_XUP_SWEEP_RESID=0: one node per lane)
+  const bool sweepResid = resid && ts && xup_sweep_resid();
+  if (m.xupSweep > 0 && (!resid || sweepResid)) {
     const int n8 = ((nsub + kBlock - 1) / kBlock + 7) / 8 * kBlock;  // = the node order's XCD groups
     const dim3 g(256 * m.xupSweep);
-    if (ts && m.xupCh >= 24)
-      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 24>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+    if (sweepResid) {
+      *nblocks = (int)g.x;
+      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 8, true>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8,
+                         partials);
+    } else if (ts && m.xupCh >= 24)
+      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 24>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8, nullptr);
     else if (ts && m.xupCh >= 16)
-      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 16>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 16>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8, nullptr);
     else if (ts)
-      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 8>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8);
+      hipLaunchKernelGGL((k_xupdate_sweep<D, true, 8>), g, dim3(kBlock), 0, st, m, sc, xBar, z, u, x, n8, nullptr);
     else
       hipLaunchKernelGGL((k_xupdate_sweep<D, false, (D == 2 ? MMX_XU_CH2D : 8)>), g, dim3(kBlock), 0, st, m, sc, xBar,
-                         z, u, x, n8);
+                         z, u, x, n8, nullptr);
     return;
   }
 #define MMX_XU(R, T)                                                                                               \
