@@ -530,12 +530,11 @@ class Engine final : public EngineBase {
         buildJacobian(dtBE);
         beStepTaken_ = true;
       }
-      streamWait();  // rhs and the Jacobian values are ready for the solver stream
+      waitStream();  // rhs and the Jacobian values are ready for the solver stream (spin: see waitStream)
       const auto tSolve = Clock::now();
       MMX_SP(mmx_matrix_set_rhs_device(jac_, rhs_.p));
       int cgIter = 0;
-      MMX_SP(mmx_matrix_solve_device(jac_, &jprm_, dx_.p, &cgIter, 0));
-      MMX_HIP(hipStreamSynchronize((hipStream_t)mst));
+      MMX_SP(mmx_matrix_solve_device(jac_, &jprm_, dx_.p, &cgIter, 0));  // (returns once its stream is done)
       st_stats_.t_solve_ms += msSince(tSolve);
       if (cgIter > 0) st_stats_.cg_iters += cgIter;
       if (cgIter <= 0)

@@ -359,8 +359,30 @@ struct SparseMatrix {
   }
   ~SparseMatrix() {
     if (st) (void)hipStreamSynchronize(st);
+    if (evSpin) (void)hipEventDestroy(evSpin);
     if (h_sc) (void)hipHostFree(h_sc);
     if (st) (void)hipStreamDestroy(st);
+  }
+
+  // the stream's work so far has completed, waited for by polling an event: the per-iteration
+  // convergence readback of CG-STAB waits in a spin, not in the blocking stream wait, whose wake-up
+  // latency varied by milliseconds on a loaded host (a backward-Euler step 24-34 ms over runs of the
+  // same kernels); MMX_SPIN=0: the stream wait
+  hipEvent_t evSpin = nullptr;
+  void spin_sync() {
+    static const bool spin = [] {
+      const char* e = getenv("MMX_SPIN");
+      return !(e && atoi(e) == 0);
+    }();
+    if (!spin) {
+      MMX_HIP(hipStreamSynchronize(st));
+      return;
+    }
+    if (!evSpin) MMX_HIP(hipEventCreateWithFlags(&evSpin, hipEventDisableTiming));
+    MMX_HIP(hipEventRecord(evSpin, st));
+    hipError_t r;
+    while ((r = hipEventQuery(evSpin)) == hipErrorNotReady) __builtin_ia32_pause();
+    MMX_HIP(r);
   }
 
   unsigned* tickets() { return d_ctl.p; }
@@ -582,13 +604,13 @@ struct SparseMatrix {
     symbolic = true;
   }
 
-  // the schedules' host images (GBs at C4) are freed on a detached thread: their pages go back to
-  // the system off the set-up's critical path
+  // the schedules' host images (GBs at C4) are freed where they are done with: the sweep schedules
+  // by their helper threads, under the factor schedule's build.  (Freed on a detached thread
+  // instead, their page-table teardown went on into the work that followed and slowed it: a 2D
+  // backward-Euler step after the C4-pattern solve 24.0 -> 29-35 ms.)
   template <class T>
   static void release(T& obj) {
-    auto* dead = new T(std::move(obj));
     obj = T();
-    std::thread([dead] { delete dead; }).detach();
   }
 
   static int chain_trim() {
@@ -892,7 +914,7 @@ struct SparseMatrix {
       launch_cgs_fin(3, d_part.p, gv, d_sc.p, st);
       MMX_HIP(hipGetLastError());
       MMX_HIP(hipMemcpyAsync(h_sc, d_sc.p, sizeof(CgsScalars), hipMemcpyDeviceToHost, st));
-      MMX_HIP(hipStreamSynchronize(st));
+      spin_sync();
       stats.iterations++;
       if (h_sc->conv) {
         conv = 1;
